@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Benchmark: rays/s of the fused ray-march hot path at 512x512 (+ SAM feature).
+
+Workload (BASELINE.json configs[2] = "garden --with_sam: RGB + 256-dim SAM
+feature head, 512x512, 1xMI355X"): one STEP renders one 512x512 GUI view
+(262,144 rays: get_rays + 3 proposal rounds 128/64/32 + hash grids + MLPs +
+compositing + 256-d SAM head per ray) on synthetic random-init weights of the
+reference architecture.  With --gpus N > 1 (torchrun, one rank per GPU) the
+view's rows are split into N equal bands (strong scaling on a fixed view) and
+the packed per-ray outputs [rays/N, 3+1+1+256] are all-gathered over RCCL, as
+BASELINE config 4 / SURVEY.md 8e describe.
+
+Prints ONE JSON line (rank 0).  `value` = rays of the whole view x steps /
+(max over ranks of the timed region).  `roofline` prices the dominant kernel
+from HIP events recorded on the launch stream inside the timed steps;
+`cpu_baseline` times the CPU oracle (torch-CPU restatement of the reference
+renderer + C restatement of its encoders) on a bounded sample of rays.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "segment-anything-nerf_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "rays/sec (RGB+256-d SAM feat) at 512×512, 1/2/4/8 MI355X; PSNR vs ref"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+# Algorithmic bytes per ray and stage (SURVEY.md 8d / BASELINE.md 3): fp32
+# embedding gathers (8 corners x C x 4 B per level per sample) + the stage's
+# own ray I/O.  Intermediates that stay in L2 are not counted.
+STAGES = ["prop0", "prop1", "final", "s_grid", "sam_head"]
+ALG_BYTES_PER_RAY = {
+    "prop0": 128 * 5 * 8 * 2 * 4 + 24 + 65 * 4,            # gathers + rays in + bins out
+    "prop1": 64 * 5 * 8 * 2 * 4 + 65 * 4 + 33 * 4,
+    "final": 32 * 16 * 8 * 2 * 4 + 24 + 33 * 4 + 20 + 31 * 4,
+    "s_grid": 32 * 16 * 8 * 8 * 4 + 32 * 4 * 4 + 128 * 4,
+    "sam_head": 164 * 4 + 256 * 4,
+}
+ALG_BYTES_RAY_TOTAL = 226_348
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--H", type=int, default=512)
+    ap.add_argument("--W", type=int, default=512)
+    ap.add_argument("--no-sam", action="store_true", help="config 2 (RGB only)")
+    ap.add_argument("--cpu-rays", type=int, default=4096,
+                    help="rays in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return rank, world, torch.device("cuda", local if world > 1 else 0)
+
+
+def build_net(with_sam, device):
+    from nerf.network import NeRFNetwork, default_opt
+    from oracle import synth
+    spec = synth.ModelSpec(with_sam=with_sam)
+    params = synth.make_params(spec, seed=0, emb_scale=1e-4, ln_jitter=0.0)
+    net = NeRFNetwork(default_opt(with_sam=with_sam))
+    net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    return net.to(device).eval(), spec, params
+
+
+def cpu_baseline(spec, params, pose, intr, H, W, n_rays):
+    """Time the CPU oracle on the first n_rays rays of the same view."""
+    from oracle import renderer as orc
+    threads = len(os.sched_getaffinity(0))
+    torch.set_num_threads(threads)
+    ro, rd = orc.get_rays(pose, intr, H, W)
+    idx = torch.linspace(0, H * W - 1, n_rays).long()          # rays spread over the view
+    model = orc.OracleNeRF(spec, params)
+    model.run(ro[idx[:64]], rd[idx[:64]], return_feats=1)      # warm-up
+    t0 = time.perf_counter()
+    model.render(ro[idx], rd[idx], return_feats=1)
+    dt = time.perf_counter() - t0
+    return {"value": n_rays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{n_rays} rays spread over the {H}x{W} view (same weights); torch-CPU "
+                      f"restatement of nerf/renderer.py+network.py, encoders in C "
+                      f"(OpenMP over points); {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank, world, dev = setup_dist(args)
+    from samnerf_amd import ops
+    from samnerf_amd._lib import lib
+    from samnerf_amd.dist import all_gather_rows, shard_range
+    from samnerf_amd.fused import FusedRenderer
+    from oracle import synth
+
+    with_sam = not args.no_sam
+    net, spec, params = build_net(with_sam, dev)
+    renderer = FusedRenderer(net)
+    H, W = args.H, args.W
+    pose, intr = synth.gui_camera(W, H)
+    r0, r1 = shard_range(H, rank, world)                      # row band of this rank
+    n_total = H * W
+    band_rays = (r1 - r0) * W
+    width = 5 + (256 if with_sam else 0)
+
+    import ctypes
+
+    def make_event_set():
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        for e in evs:                      # create the underlying hipEvent_t
+            e.record()
+        raw = (ctypes.c_void_p * 6)(*[e.cuda_event for e in evs])
+        return evs, raw
+
+    def step(raw=None):
+        lib().samnerf_set_stage_events(raw, 6 if raw is not None else 0)
+        ro, rd = ops.get_rays(pose, intr, H, W, device=dev, row0=r0, rows=r1 - r0)
+        out = renderer.render(ro, rd)
+        if world > 1:
+            cols = [out["image"], out["depth"][:, None], out["weights_sum"][:, None]]
+            if with_sam:
+                cols.append(out["samvit"])
+            return all_gather_rows(torch.cat(cols, 1), n_total)
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    sets = [make_event_set() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(sets[i][1])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    lib().samnerf_set_stage_events(None, 0)
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    stage_avg = {}
+    for j, s in enumerate(STAGES):
+        stage_avg[s] = float(np.mean([evs[j].elapsed_time(evs[j + 1]) for evs, _ in sets]))
+
+    value = n_total * args.steps / dt
+    dom = max(stage_avg, key=stage_avg.get)
+    dom_bytes = ALG_BYTES_PER_RAY[dom] * band_rays
+    achieved = dom_bytes / (stage_avg[dom] * 1e-3) / 1e9 if stage_avg[dom] > 0 else 0.0
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(dom)
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        rec = {
+            "metric": METRIC, "value": value, "unit": "rays/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (random-init weights of the reference architecture, GUI camera)",
+            "config": {"workload": ("cfg3: 512x512 view, RGB + 256-d SAM feature per ray" if with_sam
+                                    else "cfg2: 512x512 view, RGB only") if (H, W) == (512, 512)
+                       else f"{H}x{W} view", "rays_per_step": n_total, "num_steps": [128, 64, 32],
+                       "parallelism": f"ray-sharded row bands x{world}, RCCL all-gather" if world > 1
+                       else "single GPU"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "alg_bytes_per_launch": dom_bytes,
+                         "avg_launch_ms": stage_avg[dom]},
+            "stage_ms": stage_avg,
+        }
+        if world == 1 and args.cpu_rays > 0:
+            rec["cpu_baseline"] = cpu_baseline(spec, params, pose, intr, H, W, args.cpu_rays)
+        else:
+            rec["cpu_baseline"] = None
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

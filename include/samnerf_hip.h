@@ -1,0 +1,216 @@
+/*
+ * samnerf_hip.h -- C ABI of the MI355X (gfx950) NeRF ray-march library
+ * (libsamnerf_hip.so).  Plain pointers and sizes only; no torch types.
+ *
+ * All pointers are DEVICE pointers unless a parameter says "host".  Every
+ * function is asynchronous on `stream` (a hipStream_t; NULL = the legacy
+ * default stream, which is what the reference's <<<>>> launches use,
+ * gridencoder.cu:386), never synchronises the host, never allocates, and
+ * returns 0 on success or a negative SAMNERF_E* code; the message is then
+ * available from samnerf_last_error() (thread-local).
+ *
+ * Drop-in encoder entry points -- one per pybind function of the reference:
+ *   gridencoder/src/gridencoder.h:12-16 (bound at gridencoder/src/bindings.cpp:6-9)
+ *   shencoder/src/shencoder.h:9-10      (bound at shencoder/src/bindings.cpp:6-7)
+ *   freqencoder/src/freqencoder.h:7,10  (bound at freqencoder/src/bindings.cpp:6-7)
+ * Argument order and meaning follow those signatures; tensors become raw
+ * float / int32 pointers (fp32 only: the reference's fp16 dispatch is dead on
+ * this path because main.py:222 forces fp16 off).
+ *
+ * Fused entry points -- the ray-march inner loop of nerf/renderer.py:221-390
+ * + nerf/network.py:221-259 (NeRFRenderer.run), which the reference runs as
+ * ~350 unfused ATen ops per chunk around the encoder kernels.
+ */
+#ifndef SAMNERF_HIP_H
+#define SAMNERF_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* samnerf_stream_t; /* == hipStream_t */
+
+enum {
+    SAMNERF_OK = 0,
+    SAMNERF_EINVAL = -1,   /* bad argument (shape / enum / null pointer) */
+    SAMNERF_ELAUNCH = -2,  /* kernel launch failed */
+    SAMNERF_EWORKSPACE = -3 /* workspace too small */
+};
+
+/* Library identity / diagnostics (host only, no GPU needed). */
+const char* samnerf_version(void);
+const char* samnerf_last_error(void);
+
+/* ------------------------------------------------------------ gridencoder --
+ * Replaces grid_encode_forward (gridencoder.h:12, gridencoder.cu:467-490).
+ * inputs [B,D] in [0,1]; embeddings [rows,C]; offsets [L+1] int32;
+ * outputs [L,B,C] (level-major, as grid.py:49 allocates it); dy_dx
+ * [B, L*D*C] or NULL.  gridtype 0 hash / 1 tiled; interp 0 linear /
+ * 1 smoothstep.  Levels >= max_level are not written (caller zero-fills,
+ * grid.py:52).  C in {1,2,4,8,16,32}, D in {2,3,4,5}. */
+int samnerf_grid_encode_forward(const float* inputs, const float* embeddings,
+                                const int32_t* offsets, float* outputs,
+                                uint32_t B, uint32_t D, uint32_t C, uint32_t L,
+                                uint32_t max_level, float S, uint32_t H,
+                                float* dy_dx, uint32_t gridtype, int align_corners,
+                                uint32_t interp, samnerf_stream_t stream);
+
+/* Replaces grid_encode_backward (gridencoder.h:13, gridencoder.cu:492-522).
+ * grad [L,B,C]; grad_embeddings [rows,C] accumulated into (caller zeroes,
+ * grid.py:83); dy_dx / grad_inputs both NULL or both set ([B,D], written). */
+int samnerf_grid_encode_backward(const float* grad, const float* inputs,
+                                 const float* embeddings, const int32_t* offsets,
+                                 float* grad_embeddings, uint32_t B, uint32_t D,
+                                 uint32_t C, uint32_t L, uint32_t max_level, float S,
+                                 uint32_t H, const float* dy_dx, float* grad_inputs,
+                                 uint32_t gridtype, int align_corners, uint32_t interp,
+                                 samnerf_stream_t stream);
+
+/* Replaces grad_total_variation (gridencoder.h:15, gridencoder.cu:662-668). */
+int samnerf_grad_total_variation(const float* inputs, const float* embeddings, float* grad,
+                                 const int32_t* offsets, float weight, uint32_t B,
+                                 uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+                                 uint32_t gridtype, int align_corners,
+                                 samnerf_stream_t stream);
+
+/* Replaces grad_weight_decay (gridencoder.h:16, gridencoder.cu:705-713).
+ * B = rows of the embeddings table. */
+int samnerf_grad_weight_decay(const float* embeddings, float* grad, const int32_t* offsets,
+                              float weight, uint32_t B, uint32_t C, uint32_t L,
+                              samnerf_stream_t stream);
+
+/* -------------------------------------------------------------- shencoder --
+ * Replaces sh_encode_forward (shencoder.h:9, shencoder.cu:400-417).
+ * inputs [B,D=3] unit vectors; outputs [B,C*C] (C = degree 1..8);
+ * dy_dx [B,D,C*C] or NULL. */
+int samnerf_sh_encode_forward(const float* inputs, float* outputs, uint32_t B, uint32_t D,
+                              uint32_t C, float* dy_dx, samnerf_stream_t stream);
+
+/* Replaces sh_encode_backward (shencoder.h:10, shencoder.cu:419-438).
+ * grad_inputs [B,D] is accumulated into (caller zeroes, sphere_harmonics.py:50). */
+int samnerf_sh_encode_backward(const float* grad, const float* inputs, uint32_t B, uint32_t D,
+                               uint32_t C, const float* dy_dx, float* grad_inputs,
+                               samnerf_stream_t stream);
+
+/* ------------------------------------------------------------ freqencoder --
+ * Replaces freq_encode_forward (freqencoder.h:7, freqencoder.cu:97-110):
+ * outputs [B, C], C = D + 2*D*deg. */
+int samnerf_freq_encode_forward(const float* inputs, uint32_t B, uint32_t D, uint32_t deg,
+                                uint32_t C, float* outputs, samnerf_stream_t stream);
+
+/* Replaces freq_encode_backward (freqencoder.h:10, freqencoder.cu:113-129). */
+int samnerf_freq_encode_backward(const float* grad, const float* outputs, uint32_t B,
+                                 uint32_t D, uint32_t deg, uint32_t C, float* grad_inputs,
+                                 samnerf_stream_t stream);
+
+/* ------------------------------------------------------ ray-march pieces --
+ * Stand-alone kernels of the individual steps, used by the parity tests and
+ * by hosts that keep their own loop.  Each cites the reference op sequence it
+ * reproduces. */
+
+/* get_rays, full-image branch (nerf/utils.py:145-279, N = -1):
+ * pose_host = row-major 4x4 cam2world (host), intrinsics (fx, fy, cx, cy);
+ * rays_o, rays_d [H*W, 3] for pixel rows [row0, row0 + rows). */
+int samnerf_get_rays(const float* pose_host, float fx, float fy, float cx, float cy,
+                     uint32_t H, uint32_t W, uint32_t row0, uint32_t rows,
+                     float* rays_o, float* rays_d, samnerf_stream_t stream);
+
+/* near_far_from_aabb (nerf/renderer.py:122-139); aabb_host = 6 floats. */
+int samnerf_near_far(const float* rays_o, const float* rays_d, uint32_t N,
+                     const float* aabb_host, float min_near, float* nears, float* fars,
+                     samnerf_stream_t stream);
+
+/* contract (nerf/renderer.py:60-69): x, z [N,3]. */
+int samnerf_contract(const float* x, float* z, uint32_t N, samnerf_stream_t stream);
+
+/* sample_pdf (nerf/renderer.py:84-119, perturb = False): bins [N,T0+1],
+ * weights [N,T0] -> out [N,T]; inds [N,T] int32 (searchsorted result, may be
+ * NULL). */
+int samnerf_sample_pdf(const float* bins, const float* weights, uint32_t N, uint32_t T0,
+                       uint32_t T, float* out, int32_t* inds, samnerf_stream_t stream);
+
+/* sigmas -> weights (nerf/renderer.py:310-326, background 'last_sample'):
+ * real_bins [N,T+1], sigmas [N,T] -> weights [N,T]. */
+int samnerf_composite_weights(const float* real_bins, const float* sigmas, uint32_t N,
+                              uint32_t T, float* weights, samnerf_stream_t stream);
+
+/* Host helper: torch.linspace(start, end, steps) in float32 exactly as torch
+ * computes it on the CPU (the sample positions of renderer.py:97, :265). */
+void samnerf_linspace_host(float start, float end, uint32_t steps, float* out_host);
+
+/* ------------------------------------------------------------ fused path --
+ * One hash grid of the model (GridEncoder, gridencoder/grid.py:102-146). */
+typedef struct {
+    const float* embeddings;      /* device [rows, level_dim] */
+    const int32_t* offsets_host;  /* HOST [num_levels + 1] (grid.py:124-135) */
+    uint32_t num_levels;
+    uint32_t level_dim;
+    float S;                      /* log2(per_level_scale), grid.py:38 */
+    uint32_t base_resolution;     /* H */
+} samnerf_grid;
+
+/* NeRFNetwork(opt) weights (nerf/network.py:94-219), torch layout [out, in],
+ * plus the forced options of main.py:222-226. */
+typedef struct {
+    samnerf_grid grid;            /* network.py:102  L16 C2  */
+    samnerf_grid s_grid;          /* network.py:111  L16 C8  (with_sam) */
+    samnerf_grid prop[2];         /* network.py:211, :216  L5 C2 */
+    const float* grid_mlp[3];     /* [64,32] [64,64] [16,64] */
+    const float* view_mlp[3];     /* [32,31] [32,32] [3,32]  */
+    const float* prop_mlp[2][2];  /* [16,10] [1,16] each */
+    const float* sam_w[5];        /* [256,163] [256,256] [256,419] [256,256] [256,256] */
+    const float* sam_b[5];        /* [256] each */
+    const float* ln_w;            /* LayerNorm(256) weight / bias */
+    const float* ln_b;
+    int with_sam;
+    float aabb[6];                /* aabb_infer (renderer.py:163-167) */
+    float grid_bound;             /* 2 under contract (renderer.py:152-153) */
+    float min_near;               /* main.py:69 */
+    uint32_t num_steps[3];        /* (128, 64, 32), main.py:79-80 */
+} samnerf_model;
+
+/* Bytes of device workspace samnerf_render_forward needs for N rays. */
+size_t samnerf_render_workspace_size(const samnerf_model* model, uint32_t N);
+
+/* The whole ray-march inner loop for N rays (NeRFRenderer.run in eval mode:
+ * perturb = False, background 'last_sample', sum_after_mlp = False,
+ * sam_use_view_direction = True): near/far, 3 proposal rounds with
+ * inverse-CDF resampling, hash-grid + SH encoding, sigma / colour MLPs,
+ * compositing, view MLP, and (with_sam) the s_grid feature composite plus the
+ * SkipConnMLP + LayerNorm head.
+ *   rays_o, rays_d [N,3]; cam_near_far [N,2] or [1,2] (n_cnf rows) or NULL;
+ *   bg_color: scalar background (renderer.py:239-240, default 1);
+ *   image [N,3], depth [N], weights_sum [N]; samvit [N,256] (NULL unless
+ *   with_sam); feature_rows [N,164] optional: the per-ray head input
+ *   cat(f_sam, f_image, image, depth) (+1 pad), kept for training.
+ * Outputs are written, never accumulated. */
+int samnerf_render_forward(const samnerf_model* model, const float* rays_o,
+                           const float* rays_d, uint32_t N, const float* cam_near_far,
+                           uint32_t n_cnf, float bg_color, float* image, float* depth,
+                           float* weights_sum, float* samvit, float* feature_rows,
+                           void* workspace, size_t workspace_bytes, samnerf_stream_t stream);
+
+/* Backward of the s_grid feature composite for the SAM-distillation step
+ * (nerf/utils.py:1098-1106 training branch): given the per-ray gradient of
+ * f_sam [N,128] (the first 128 columns of d(loss)/d(feature_rows)), scatter
+ * sum_k w_k * trilinear(corner) * g into grad_embeddings [rows, 8] of s_grid
+ * (accumulated into).  Uses the sample weights/positions the last
+ * samnerf_render_forward call left in `workspace` for the same rays. */
+int samnerf_sgrid_backward(const samnerf_model* model, const float* grad_fsam, uint32_t N,
+                           float* grad_embeddings, const void* workspace,
+                           size_t workspace_bytes, samnerf_stream_t stream);
+
+/* Measurement hook (bench.py): when set, samnerf_render_forward records
+ * events[i] (hipEvent_t) on its stream before stage i (0 prop0, 1 prop1,
+ * 2 final, 3 s_grid, 4 SAM head) and events[5] after the last one.  n = 0 or
+ * events = NULL disables it.  Thread-local; costs one hipEventRecord per stage. */
+int samnerf_set_stage_events(void* const* events, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SAMNERF_HIP_H */

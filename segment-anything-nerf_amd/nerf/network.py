@@ -1,0 +1,140 @@
+"""NeRFNetwork on gfx950 -- interface of nerf/network.py:9-308.
+
+Same submodules, parameter names and shapes as the reference (checkpoint
+state_dicts load with strict=True for the RGB + SAM configuration).  The
+mask heads (--with_mask, network.py:125-203) are out of scope.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from activation import trunc_exp
+from encoding import get_encoder
+
+from .renderer import NeRFRenderer
+
+
+class MLP(nn.Module):
+    """network.py:9-34: Linear (+ReLU between layers)."""
+
+    def __init__(self, dim_in, dim_out, dim_hidden, num_layers, bias=True):
+        super().__init__()
+        self.dim_in, self.dim_out, self.dim_hidden, self.num_layers = dim_in, dim_out, dim_hidden, num_layers
+        self.net = nn.ModuleList([
+            nn.Linear(dim_in if l == 0 else dim_hidden,
+                      dim_out if l == num_layers - 1 else dim_hidden, bias=bias)
+            for l in range(num_layers)])
+
+    def forward(self, x, save_intermedian_results=False):
+        for l, layer in enumerate(self.net):
+            x = layer(x)
+            if l != self.num_layers - 1:
+                x = F.relu(x, inplace=True)
+        return x
+
+
+class SkipConnMLP(nn.Module):
+    """network.py:36-75: Linear + leaky_relu(0.01), input re-concatenated at
+    the skip layers."""
+
+    def __init__(self, dim_in, dim_out, dim_hidden, num_layers, skip_layers=(), bias=True):
+        super().__init__()
+        self.dim_in, self.dim_out, self.dim_hidden, self.num_layers = dim_in, dim_out, dim_hidden, num_layers
+        self.skip_layers = list(skip_layers)
+        layers = []
+        for l in range(num_layers):
+            fin = dim_in if l == 0 else (dim_hidden + dim_in if l in self.skip_layers else dim_hidden)
+            fout = dim_out if l == num_layers - 1 else dim_hidden
+            layers.append(nn.Linear(fin, fout, bias=bias))
+        self.net = nn.ModuleList(layers)
+
+    def forward(self, x, save_intermedian_results=False):
+        x_in = x
+        for l, layer in enumerate(self.net):
+            if l in self.skip_layers:
+                x = torch.cat([x, x_in], dim=-1)
+            x = layer(x)
+            if l != self.num_layers - 1:
+                x = F.leaky_relu(x, inplace=True)
+        return x
+
+
+class NeRFNetwork(NeRFRenderer):
+    def __init__(self, opt):
+        super().__init__(opt)
+        if getattr(opt, "with_mask", False):
+            raise NotImplementedError("--with_mask heads are out of scope (SURVEY.md 8f)")
+        self.geom_feat_dim = 15
+        # table sizes are hard-coded in the reference (19 / 19 / 17); the
+        # optional opt.*_log2 overrides exist for small-table test fixtures
+        g_log2 = getattr(opt, "grid_log2", 19)
+        s_log2 = getattr(opt, "s_grid_log2", 19)
+        p_log2 = getattr(opt, "prop_log2", 17)
+        self.grid, self.grid_in_dim = get_encoder("hashgrid", input_dim=3, level_dim=2,
+                                                  num_levels=16, log2_hashmap_size=g_log2,
+                                                  desired_resolution=2048 * self.bound)
+        self.grid_mlp = MLP(self.grid_in_dim, 1 + self.geom_feat_dim, 64, 3, bias=False)
+        self.view_encoder, self.view_in_dim = get_encoder("sh", input_dim=3, degree=4)
+        self.view_mlp = MLP(self.geom_feat_dim + self.view_in_dim, 3, 32, 3, bias=False)
+        if opt.with_sam:
+            self.s_grid, self.s_dim = get_encoder("hashgrid", input_dim=3, num_levels=16,
+                                                  level_dim=8, base_resolution=16,
+                                                  log2_hashmap_size=s_log2, desired_resolution=512)
+            self.samvit_mlp = nn.Sequential(
+                SkipConnMLP(self.s_dim + self.geom_feat_dim + self.view_in_dim + 4, 256, 256, 5,
+                            skip_layers=[2], bias=True),
+                nn.LayerNorm(256))
+        self.prop_encoders = nn.ModuleList()
+        self.prop_mlp = nn.ModuleList()
+        for desired in (128, 256):
+            enc, dim = get_encoder("hashgrid", input_dim=3, level_dim=2, num_levels=5,
+                                   log2_hashmap_size=p_log2, desired_resolution=desired)
+            self.prop_encoders.append(enc)
+            self.prop_mlp.append(MLP(dim, 1, 16, 2, bias=False))
+
+    def common_forward(self, x, save_intermedian_results=False):
+        grid_output = self.grid(x, bound=self.bound)
+        f = self.grid_mlp(grid_output)
+        return trunc_exp(f[..., 0]), f[..., 1:], grid_output
+
+    def forward(self, x, d, save_intermedian_results=False, **kwargs):
+        sigma, feat, grid_output = self.common_forward(x)
+        d = self.view_encoder(d)
+        return {"sigma": sigma, "geo_feat": feat, "color": torch.cat([feat, d], dim=-1),
+                "grid_output": grid_output}
+
+    def density(self, x, proposal=-1):
+        if 0 <= proposal < len(self.prop_encoders):
+            h = self.prop_encoders[proposal](x, bound=self.bound)
+            sigma = trunc_exp(self.prop_mlp[proposal](h).squeeze(-1))
+        else:
+            sigma, _, _ = self.common_forward(x)
+        return {"sigma": sigma}
+
+    def apply_total_variation(self, w):
+        (self.s_grid if self.opt.with_sam else self.grid).grad_total_variation(w)
+
+    def apply_weight_decay(self, w):
+        (self.s_grid if self.opt.with_sam else self.grid).grad_weight_decay(w)
+
+    def get_params(self, lr):
+        params = [{"params": self.grid.parameters(), "lr": lr},
+                  {"params": self.grid_mlp.parameters(), "lr": lr},
+                  {"params": self.view_mlp.parameters(), "lr": lr},
+                  {"params": self.prop_encoders.parameters(), "lr": lr},
+                  {"params": self.prop_mlp.parameters(), "lr": lr}]
+        if self.opt.with_sam:
+            params += [{"params": self.s_grid.parameters(), "lr": lr},
+                       {"params": self.samvit_mlp.parameters(), "lr": lr}]
+        return params
+
+
+def default_opt(with_sam=True, **kw):
+    """The option namespace NeRFNetwork reads, with main.py's defaults and its
+    forced overrides (main.py:222-226: fp16 off, bound 128, contract on)."""
+    import types
+    o = dict(bound=128.0, contract=True, min_near=0.2, density_thresh=10, with_sam=with_sam,
+             sum_after_mlp=False, sam_use_view_direction=True, with_mask=False,
+             num_steps=[128, 64, 32], background="last_sample", max_ray_batch=4096 * 4, fp16=False)
+    o.update(kw)
+    return types.SimpleNamespace(**o)

@@ -1,0 +1,211 @@
+"""NeRFRenderer on gfx950 -- interface of nerf/renderer.py:142-464.
+
+`run()` keeps the reference's keyword interface (bg_color, perturb,
+cam_near_far, update_proposal, return_feats, return_mask, H, W) and by default
+executes the whole ray-march loop as the fused HIP pipeline
+(samnerf_amd.fused, raymarch.hip).  `run_torch()` is the reference's own
+unfused op sequence on the GPU with the drop-in encoders -- the
+"reference-equivalent" single-GPU baseline of BASELINE.md and the path for
+options the fused kernels do not cover (perturbed sampling, training-mode
+bookkeeping).  Staged rendering chunks rays like renderer.py:185-219 but,
+unlike the reference, also works with return_feats (flat [N,256] rows are
+reshaped once at the end, fixing the SURVEY.md 0.3 crash).
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+
+def near_far_from_aabb(rays_o, rays_d, aabb, min_near=0.05):
+    """renderer.py:122-139 on torch tensors."""
+    tmin = (aabb[:3] - rays_o) / (rays_d + 1e-15)
+    tmax = (aabb[3:] - rays_o) / (rays_d + 1e-15)
+    near = torch.where(tmin < tmax, tmin, tmax).amax(dim=-1, keepdim=True)
+    far = torch.where(tmin > tmax, tmin, tmax).amin(dim=-1, keepdim=True)
+    miss = far < near
+    near[miss] = 1e9
+    far[miss] = 1e9
+    return torch.clamp(near, min=min_near), far
+
+
+def contract(x):
+    """renderer.py:60-69: L-inf contraction of R^3 into [-2, 2]^3."""
+    shape, C = x.shape[:-1], x.shape[-1]
+    x = x.view(-1, C)
+    mag, idx = x.abs().max(1, keepdim=True)
+    scale = 1 / mag.repeat(1, C)
+    scale.scatter_(1, idx, (2 - 1 / mag) / mag)
+    return torch.where(mag < 1, x, x * scale).view(*shape, C)
+
+
+def sample_pdf(bins, weights, T, perturb=False):
+    """renderer.py:84-119: inverse-CDF resampling of T positions."""
+    N, T0 = weights.shape
+    weights = weights + 0.01
+    pdf = weights / torch.sum(weights, -1, keepdim=True)
+    cdf = torch.cumsum(pdf, -1).clamp(max=1)
+    cdf = torch.cat([torch.zeros_like(cdf[..., :1]), cdf], -1)
+    u = torch.linspace(0.5 / T, 1 - 0.5 / T, steps=T, device=weights.device).expand(N, T)
+    if perturb:
+        u = u + (torch.rand_like(u) - 0.5) / T
+    u = u.contiguous()
+    inds = torch.searchsorted(cdf, u, right=True)
+    below = torch.clamp(inds - 1, 0, T0)
+    above = torch.clamp(inds, 0, T0)
+    c0, c1 = torch.gather(cdf, -1, below), torch.gather(cdf, -1, above)
+    b0, b1 = torch.gather(bins, -1, below), torch.gather(bins, -1, above)
+    t = torch.clamp(torch.nan_to_num((u - c0) / (c1 - c0)), 0, 1)
+    return b0 + t * (b1 - b0)
+
+
+def _spacing(x):
+    return torch.where(x < 1, x / 2, 1 - 1 / (2 * x))
+
+
+def _spacing_inv(x):
+    return torch.where(x < 0.5, 2 * x, 1 / (2 - 2 * x))
+
+
+class NeRFRenderer(nn.Module):
+    def __init__(self, opt):
+        super().__init__()
+        self.opt = opt
+        self.real_bound = opt.bound
+        self.bound = 2 if opt.contract else opt.bound
+        self.cascade = 1 + math.ceil(math.log2(self.bound))
+        self.min_near = opt.min_near
+        self.density_thresh = getattr(opt, "density_thresh", 10)
+        box = torch.FloatTensor([-self.real_bound] * 3 + [self.real_bound] * 3)
+        self.register_buffer("aabb_train", box)
+        self.register_buffer("aabb_infer", box.clone())
+        self.fused = True          # fused HIP pipeline for eligible calls
+        self._fused = None
+
+    def forward(self, x, d, **kwargs):
+        raise NotImplementedError()
+
+    def density(self, x, **kwargs):
+        raise NotImplementedError()
+
+    def update_aabb(self, aabb):
+        if not torch.is_tensor(aabb):
+            aabb = torch.from_numpy(aabb).float()
+        self.aabb_train = aabb.clamp(-self.real_bound, self.real_bound).to(self.aabb_train.device)
+        self.aabb_infer = self.aabb_train.clone()
+
+    # ------------------------------------------------------------ render --
+    def render(self, rays_o, rays_d, staged=False, cam_near_far=None, **kwargs):
+        if not staged:
+            return self.run(rays_o, rays_d, cam_near_far=cam_near_far, **kwargs)
+        N = rays_o.shape[0]
+        H, W = kwargs.pop("H", None), kwargs.pop("W", None)
+        results = {}
+        step = self.opt.max_ray_batch
+        for head in range(0, N, step):
+            tail = min(head + step, N)
+            cnf = cam_near_far
+            if cnf is not None and cnf.shape[0] != 1:
+                cnf = cnf[head:tail]
+            part = self.run(rays_o[head:tail], rays_d[head:tail], cam_near_far=cnf, **kwargs)
+            for k, v in part.items():
+                if v is None:
+                    continue
+                if torch.is_tensor(v):
+                    v = v.reshape(tail - head, *v.shape[1:]) if k != "samvit" else v.reshape(tail - head, -1)
+                    if k not in results:
+                        results[k] = torch.empty(N, *v.shape[1:], device=rays_o.device)
+                    results[k][head:tail] = v
+                else:
+                    results[k] = v
+        if "samvit" in results and H is not None and kwargs.get("return_feats", 0):
+            results["samvit"] = results["samvit"].view(H, W, -1)
+        return results
+
+    def _fused_ok(self, rays_o, perturb, return_mask, kwargs):
+        return (self.fused and rays_o.is_cuda and not perturb and not return_mask
+                and not self.training and self.opt.background == "last_sample"
+                and not getattr(self.opt, "sum_after_mlp", False)
+                and list(self.opt.num_steps) == [128, 64, 32]
+                and (not self.opt.with_sam or self.opt.sam_use_view_direction))
+
+    def run(self, rays_o, rays_d, bg_color=None, perturb=False, cam_near_far=None,
+            update_proposal=True, return_feats=0, return_mask=0, H=None, W=None, **kwargs):
+        if self._fused_ok(rays_o, perturb, return_mask, kwargs):
+            from samnerf_amd.fused import FusedRenderer
+            if self._fused is None or self._fused.net is not self:
+                self._fused = FusedRenderer(self)
+            out = self._fused.render(rays_o, rays_d, cam_near_far, bg_color)
+            samvit = out.pop("samvit", None)
+            if return_feats > 0 and samvit is not None:
+                out["samvit"] = samvit.view(H, W, -1) if H is not None else samvit
+            return out
+        return self.run_torch(rays_o, rays_d, bg_color=bg_color, perturb=perturb,
+                              cam_near_far=cam_near_far, update_proposal=update_proposal,
+                              return_feats=return_feats, return_mask=return_mask, H=H, W=W)
+
+    def run_torch(self, rays_o, rays_d, bg_color=None, perturb=False, cam_near_far=None,
+                  update_proposal=True, return_feats=0, return_mask=0, H=None, W=None, **kwargs):
+        """The reference's unfused op sequence (renderer.py:221-390) with the
+        HIP drop-in encoders: ~350 small kernels per call."""
+        if return_mask:
+            raise NotImplementedError("--with_mask heads are out of scope (SURVEY.md 8f)")
+        opt = self.opt
+        rays_o = rays_o.contiguous()
+        rays_d = rays_d.contiguous()
+        N = rays_o.shape[0]
+        dev = rays_o.device
+        nears, fars = near_far_from_aabb(rays_o, rays_d,
+                                         self.aabb_train if self.training else self.aabb_infer,
+                                         self.min_near)
+        if cam_near_far is not None:
+            nears = torch.maximum(nears, cam_near_far[:, [0]])
+            fars = torch.minimum(fars, cam_near_far[:, [1]])
+        if bg_color is None:
+            bg_color = 1
+        results = {}
+        s_n, s_f = _spacing(nears), _spacing(fars)
+        bins = weights = None
+        for it, T in enumerate(opt.num_steps):
+            if it == 0:
+                bins = torch.linspace(0, 1, T + 1, device=dev).unsqueeze(0).expand(N, -1)
+                if perturb:
+                    bins = (bins + (torch.rand_like(bins) - 0.5) / T).clamp(0, 1)
+            else:
+                bins = sample_pdf(bins, weights, T + 1, perturb).detach()
+            real_bins = _spacing_inv(s_n * (1 - bins) + s_f * bins)
+            rays_t = (real_bins[..., 1:] + real_bins[..., :-1]) / 2
+            xyzs = rays_o.unsqueeze(1) + rays_d.unsqueeze(1) * rays_t.unsqueeze(2)
+            if opt.contract:
+                xyzs = contract(xyzs)
+            if it != len(opt.num_steps) - 1:
+                with torch.set_grad_enabled(update_proposal):
+                    sigmas = self.density(xyzs, proposal=it)["sigma"]
+            else:
+                dirs = rays_d.view(-1, 1, 3).expand_as(xyzs)
+                dirs = dirs / torch.norm(dirs, dim=-1, keepdim=True)
+                outputs = self(xyzs, dirs)
+                sigmas, colors = outputs["sigma"], outputs["color"]
+                if opt.with_sam:
+                    features = self.s_grid(xyzs, bound=self.bound)
+            ds = (real_bins[..., 1:] - real_bins[..., :-1]) * sigmas
+            if opt.background == "last_sample":
+                ds = torch.cat([ds[..., :-1], torch.full_like(ds[..., -1:], torch.inf)], dim=-1)
+            alphas = 1 - torch.exp(-ds)
+            trans = torch.cumsum(ds[..., :-1], dim=-1)
+            trans = torch.exp(-torch.cat([torch.zeros_like(trans[..., :1]), trans], dim=-1))
+            weights = alphas * trans
+            weights.nan_to_num_(0)
+        weights_sum = weights.sum(-1)
+        depth = (weights * rays_t).sum(-1)
+        f_image = (weights.unsqueeze(-1) * colors).sum(-2)
+        image = torch.sigmoid(self.view_mlp(f_image))
+        image = image + (1 - weights_sum).unsqueeze(-1) * bg_color
+        results.update(weights_sum=weights_sum, depth=depth, image=image)
+        if opt.with_sam:
+            f_sam = (weights.unsqueeze(-1) * features).sum(-2)
+            f = torch.cat([f_sam, f_image, image, depth.unsqueeze(-1)], dim=-1)
+            samvit = self.samvit_mlp(f)
+            if return_feats > 0:
+                results["samvit"] = samvit.view(H, W, -1) if H is not None else samvit
+        return results

@@ -1,0 +1,97 @@
+"""ctypes binding of libsamnerf_hip.so (include/samnerf_hip.h).
+
+The product path has no fallback: if the HIP library is missing or cannot be
+loaded, every op raises SamnerfUnavailable with the build command.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsamnerf_hip.so")
+
+_u32 = ctypes.c_uint32
+_f32 = ctypes.c_float
+_int = ctypes.c_int
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+
+class SamnerfUnavailable(RuntimeError):
+    pass
+
+
+class SamnerfGrid(ctypes.Structure):
+    _fields_ = [("embeddings", _vp), ("offsets_host", ctypes.POINTER(ctypes.c_int32)),
+                ("num_levels", _u32), ("level_dim", _u32), ("S", _f32),
+                ("base_resolution", _u32)]
+
+
+class SamnerfModel(ctypes.Structure):
+    _fields_ = [("grid", SamnerfGrid), ("s_grid", SamnerfGrid), ("prop", SamnerfGrid * 2),
+                ("grid_mlp", _vp * 3), ("view_mlp", _vp * 3), ("prop_mlp", (_vp * 2) * 2),
+                ("sam_w", _vp * 5), ("sam_b", _vp * 5), ("ln_w", _vp), ("ln_b", _vp),
+                ("with_sam", _int), ("aabb", _f32 * 6), ("grid_bound", _f32),
+                ("min_near", _f32), ("num_steps", _u32 * 3)]
+
+
+_SIGS = {
+    "samnerf_version": ([], ctypes.c_char_p),
+    "samnerf_last_error": ([], ctypes.c_char_p),
+    "samnerf_grid_encode_forward": ([_vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _f32, _u32,
+                                     _vp, _u32, _int, _u32, _vp], _int),
+    "samnerf_grid_encode_backward": ([_vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _f32,
+                                      _u32, _vp, _vp, _u32, _int, _u32, _vp], _int),
+    "samnerf_grad_total_variation": ([_vp, _vp, _vp, _vp, _f32, _u32, _u32, _u32, _u32, _f32, _u32,
+                                      _u32, _int, _vp], _int),
+    "samnerf_grad_weight_decay": ([_vp, _vp, _vp, _f32, _u32, _u32, _u32, _vp], _int),
+    "samnerf_sh_encode_forward": ([_vp, _vp, _u32, _u32, _u32, _vp, _vp], _int),
+    "samnerf_sh_encode_backward": ([_vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp], _int),
+    "samnerf_freq_encode_forward": ([_vp, _u32, _u32, _u32, _u32, _vp, _vp], _int),
+    "samnerf_freq_encode_backward": ([_vp, _vp, _u32, _u32, _u32, _u32, _vp, _vp], _int),
+    "samnerf_get_rays": ([ctypes.POINTER(_f32), _f32, _f32, _f32, _f32, _u32, _u32, _u32, _u32,
+                          _vp, _vp, _vp], _int),
+    "samnerf_near_far": ([_vp, _vp, _u32, ctypes.POINTER(_f32), _f32, _vp, _vp, _vp], _int),
+    "samnerf_contract": ([_vp, _vp, _u32, _vp], _int),
+    "samnerf_sample_pdf": ([_vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp], _int),
+    "samnerf_composite_weights": ([_vp, _vp, _u32, _u32, _vp, _vp], _int),
+    "samnerf_linspace_host": ([_f32, _f32, _u32, ctypes.POINTER(_f32)], None),
+    "samnerf_render_workspace_size": ([ctypes.POINTER(SamnerfModel), _u32], _sz),
+    "samnerf_render_forward": ([ctypes.POINTER(SamnerfModel), _vp, _vp, _u32, _vp, _u32, _f32,
+                                _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp], _int),
+    "samnerf_sgrid_backward": ([ctypes.POINTER(SamnerfModel), _vp, _u32, _vp, _vp, _sz, _vp],
+                               _int),
+    "samnerf_set_stage_events": ([ctypes.POINTER(_vp), _u32], _int),
+}
+
+EXPORTED = tuple(_SIGS)
+_lib = None
+
+
+def lib():
+    """Load the HIP library (once).  Raises SamnerfUnavailable if absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SamnerfUnavailable(
+                f"{LIB_PATH} is not built; run `python segment-anything-nerf_amd/build.py` "
+                "(or __graft_entry__.build()).  There is no CPU fallback.")
+        try:
+            L = ctypes.CDLL(LIB_PATH)
+        except OSError as e:
+            raise SamnerfUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (args, res) in _SIGS.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().samnerf_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what}: {msg} (code {rc})")
+
+
+def last_error():
+    return lib().samnerf_last_error().decode(errors="replace")

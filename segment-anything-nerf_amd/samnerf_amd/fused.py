@@ -1,0 +1,175 @@
+"""Fused ray-march render on gfx950 (samnerf_render_forward, raymarch.hip).
+
+`FusedRenderer(net)` wraps a NeRFNetwork-shaped module (the mirror in
+nerf/network.py, or anything exposing the same attributes / state_dict keys)
+and renders rays with the whole NeRFRenderer.run loop
+(nerf/renderer.py:221-390) in five kernel launches.  Parameters are read in
+place (torch layout); nothing is copied or cached between calls except the
+workspace buffer.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from ._lib import SamnerfGrid, SamnerfModel, check, lib
+from .ops import _ptr, _stream
+
+ROW = 164          # head-input row: f_sam 128 | f_image 31 | image 3 | depth 1 | pad
+
+
+def _param(t, name):
+    if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+        raise RuntimeError(f"fused render: {name} must be a contiguous float32 CUDA tensor")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class FusedRenderer:
+    def __init__(self, net):
+        self.net = net
+        self._ws = None
+        self._keep = []
+
+    # --------------------------------------------------------------- model --
+    def _grid(self, enc, name):
+        offs = np.ascontiguousarray(enc.offsets_host, np.int32)
+        self._keep.append(offs)
+        g = SamnerfGrid()
+        g.embeddings = _param(enc.embeddings, name + ".embeddings")
+        g.offsets_host = offs.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        g.num_levels = enc.num_levels
+        g.level_dim = enc.level_dim
+        g.S = float(np.log2(enc.per_level_scale))
+        g.base_resolution = enc.base_resolution
+        return g
+
+    def model(self):
+        n = self.net
+        opt = n.opt
+        self._keep = []
+        m = SamnerfModel()
+        m.grid = self._grid(n.grid, "grid")
+        m.prop[0] = self._grid(n.prop_encoders[0], "prop_encoders.0")
+        m.prop[1] = self._grid(n.prop_encoders[1], "prop_encoders.1")
+        for i in range(3):
+            m.grid_mlp[i] = _param(n.grid_mlp.net[i].weight, f"grid_mlp.net.{i}.weight")
+            m.view_mlp[i] = _param(n.view_mlp.net[i].weight, f"view_mlp.net.{i}.weight")
+        for p in range(2):
+            for i in range(2):
+                m.prop_mlp[p][i] = _param(n.prop_mlp[p].net[i].weight, f"prop_mlp.{p}.net.{i}.weight")
+        m.with_sam = int(bool(opt.with_sam))
+        if opt.with_sam:
+            m.s_grid = self._grid(n.s_grid, "s_grid")
+            skip = n.samvit_mlp[0]
+            for i in range(5):
+                m.sam_w[i] = _param(skip.net[i].weight, f"samvit_mlp.0.net.{i}.weight")
+                m.sam_b[i] = _param(skip.net[i].bias, f"samvit_mlp.0.net.{i}.bias")
+            m.ln_w = _param(n.samvit_mlp[1].weight, "samvit_mlp.1.weight")
+            m.ln_b = _param(n.samvit_mlp[1].bias, "samvit_mlp.1.bias")
+        aabb = n.aabb_train if n.training else n.aabb_infer
+        for i, v in enumerate(aabb.detach().cpu().tolist()):
+            m.aabb[i] = v
+        m.grid_bound = float(n.bound)
+        m.min_near = float(opt.min_near)
+        for i, v in enumerate(opt.num_steps):
+            m.num_steps[i] = int(v)
+        return m
+
+    def workspace(self, m, N, device):
+        need = lib().samnerf_render_workspace_size(ctypes.byref(m), N)
+        if self._ws is None or self._ws.numel() < need or self._ws.device != device:
+            self._ws = torch.empty(max(need, 1), dtype=torch.uint8, device=device)
+        return self._ws, need
+
+    # -------------------------------------------------------------- render --
+    @torch.no_grad()
+    def render(self, rays_o, rays_d, cam_near_far=None, bg_color=None, rows=None,
+               keep_workspace=False):
+        """rays_o, rays_d [N,3] (CUDA fp32) -> dict(image [N,3], depth [N],
+        weights_sum [N], samvit [N,256] if with_sam).  `rows` (optional
+        [N,164] tensor) receives the head input cat(f_sam, f_image, image,
+        depth)."""
+        rays_o = rays_o.contiguous().float()
+        rays_d = rays_d.contiguous().float()
+        N = rays_o.shape[0]
+        dev = rays_o.device
+        m = self.model()
+        ws, need = self.workspace(m, N, dev)
+        if bg_color is None:
+            bg = 1.0
+        elif torch.is_tensor(bg_color):
+            if bg_color.numel() != 1:
+                raise NotImplementedError("fused render: per-ray background colours")
+            bg = float(bg_color)
+        else:
+            bg = float(bg_color)
+        image = torch.empty(N, 3, device=dev)
+        depth = torch.empty(N, device=dev)
+        wsum = torch.empty(N, device=dev)
+        samvit = torch.empty(N, 256, device=dev) if m.with_sam else None
+        cnf = None
+        n_cnf = 0
+        if cam_near_far is not None:
+            cnf = cam_near_far.contiguous().float()
+            n_cnf = cnf.shape[0]
+        if rows is not None:
+            assert rows.shape == (N, ROW) and rows.is_contiguous()
+        check(lib().samnerf_render_forward(
+            ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, _ptr(cnf), n_cnf, bg, _ptr(image),
+            _ptr(depth), _ptr(wsum), _ptr(samvit), _ptr(rows), _ptr(ws), need, _stream(rays_o)),
+            "render_forward")
+        out = {"image": image, "depth": depth, "weights_sum": wsum}
+        if samvit is not None:
+            out["samvit"] = samvit
+        if keep_workspace:
+            out["_workspace"] = (ws, need, m)
+        return out
+
+    def sgrid_backward(self, grad_rows, workspace, grad_embeddings):
+        ws, need, m = workspace
+        N = grad_rows.shape[0]
+        grad_rows = grad_rows.contiguous()
+        assert grad_rows.shape[1] == ROW
+        check(lib().samnerf_sgrid_backward(ctypes.byref(m), _ptr(grad_rows), N,
+                                           _ptr(grad_embeddings), _ptr(ws), need,
+                                           _stream(grad_rows)), "sgrid_backward")
+
+
+class _FusedSamRows(torch.autograd.Function):
+    """Head-input rows with gradient w.r.t. s_grid.embeddings only (RGB params
+    are frozen in the distillation stage, main.py:255-262; proposal grads are
+    cut by sample_pdf(...).detach(), renderer.py:274-275)."""
+
+    @staticmethod
+    def forward(ctx, s_emb, renderer, rays_o, rays_d, cam_near_far, bg_color):
+        N = rays_o.shape[0]
+        rows = torch.empty(N, ROW, device=rays_o.device)
+        out = renderer.render(rays_o, rays_d, cam_near_far, bg_color, rows=rows,
+                              keep_workspace=True)
+        ws = out.pop("_workspace")
+        # own a private workspace copy: the renderer reuses its buffer
+        ctx.ws = (ws[0][:ws[1]].clone(), ws[1], ws[2])
+        ctx.renderer = renderer
+        ctx.keep = list(renderer._keep)
+        ctx.emb_shape = s_emb.shape
+        ctx.mark_non_differentiable(out["image"], out["depth"], out["weights_sum"])
+        return rows, out["image"], out["depth"], out["weights_sum"]
+
+    @staticmethod
+    def backward(ctx, g_rows, g_img, g_depth, g_wsum):
+        grad = None
+        if ctx.needs_input_grad[0] and g_rows is not None:
+            grad = torch.zeros(ctx.emb_shape, device=g_rows.device)
+            ctx.renderer.sgrid_backward(g_rows, ctx.ws, grad)
+        return grad, None, None, None, None, None
+
+
+def render_sam_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None):
+    """Differentiable SAM-feature render for the distillation step
+    (nerf/utils.py:1098-1099): returns samvit [N,256] with autograd to
+    s_grid.embeddings (HIP scatter) and samvit_mlp (torch)."""
+    net = renderer.net
+    rows, image, depth, wsum = _FusedSamRows.apply(net.s_grid.embeddings, renderer, rays_o,
+                                                    rays_d, cam_near_far, bg_color)
+    samvit = net.samvit_mlp(rows[:, :163])
+    return {"samvit": samvit, "image": image, "depth": depth, "weights_sum": wsum}

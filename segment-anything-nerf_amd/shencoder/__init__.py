@@ -1,0 +1,1 @@
+from .sphere_harmonics import SHEncoder  # noqa: F401

@@ -1,0 +1,195 @@
+"""Drop-in encoders on the MI355X vs the CPU oracle (oracle/encoders_oracle.c).
+
+Bar: the forward grid encoder is BIT-EXACT (same corner rows, same fma
+order); SH / freq forward within fp32 rounding; backward passes (float
+atomics, order-dependent) within a stated tolerance.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import encoders as enc
+from oracle import synth
+
+pytestmark = pytest.mark.gpu
+
+GRID_CONFIGS = {
+    # name: (GridSpec, emb_scale)  -- the four NeRFNetwork grids (network.py:102,111,211,216)
+    "grid_L16C2": (synth.ModelSpec().grid, 0.5),
+    "s_grid_L16C8": (synth.ModelSpec().s_grid, 0.5),
+    "prop0_L5C2": (synth.ModelSpec().prop[0], 0.5),
+    "prop1_L5C2": (synth.ModelSpec().prop[1], 0.5),
+}
+
+
+def _points(n, seed, oob=True):
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    if oob:
+        x[:64] = rng.uniform(-0.02, 1.02, (64, 3))             # out-of-range -> zeros
+        x[64:72] = [[0, 0, 0], [1, 1, 1], [0, 1, 0], [1, 0, 1], [0.5, 0.5, 0.5],
+                    [1e-8, 1 - 1e-7, 0.25], [0.9999999, 0.0, 0.75], [0.5, 1.0, 0.0]]
+    return x
+
+
+def _grid_forward_gpu(x, emb, offs, spec, max_level=None, dy=False, gridtype=0, align=False,
+                      interp=0, cuda=None):
+    import _gridencoder
+    L, C = spec.num_levels, spec.level_dim
+    B = x.shape[0]
+    max_level = L if max_level is None else max_level
+    xi = torch.from_numpy(x).to(cuda)
+    ei = torch.from_numpy(emb).to(cuda)
+    oi = torch.from_numpy(offs).to(cuda)
+    out = torch.zeros(L, B, C, device=cuda)
+    dyt = torch.zeros(B, L * 3 * C, device=cuda) if dy else None
+    _gridencoder.grid_encode_forward(xi, ei, oi, out, B, 3, C, L, max_level, spec.S,
+                                     spec.base_resolution, dyt, gridtype, align, interp)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), (dyt.cpu().numpy() if dy else None)
+
+
+@pytest.mark.parametrize("name", list(GRID_CONFIGS))
+def test_grid_forward_bit_exact(hip_lib, oracle_lib, cuda, name):
+    spec, scale = GRID_CONFIGS[name]
+    offs = spec.offsets()
+    emb = synth.uniform(11, name, (int(offs[-1]), spec.level_dim), -scale, scale)
+    x = _points(20000, 1)
+    got, _ = _grid_forward_gpu(x, emb, offs, spec, cuda=cuda)
+    ref = enc.grid_encode_forward(x, emb, offs, spec.num_levels, spec.S, spec.base_resolution)
+    assert np.array_equal(got, ref), f"max |d| = {np.abs(got - ref).max()}"
+
+
+@pytest.mark.parametrize("C,gridtype,align,interp,max_level", [
+    (1, 0, False, 0, None), (4, 1, False, 0, None), (16, 0, True, 0, None),
+    (32, 0, False, 1, None), (2, 1, True, 1, 3), (8, 0, False, 0, 2)])
+def test_grid_forward_variants_with_dy_dx(hip_lib, oracle_lib, cuda, C, gridtype, align, interp,
+                                          max_level):
+    spec = synth.GridSpec(num_levels=6, level_dim=C, log2_hashmap_size=12, desired_resolution=200)
+    offs = spec.offsets()
+    emb = synth.uniform(3, f"v{C}", (int(offs[-1]), C), -1, 1)
+    x = _points(3000, C)
+    got, gdy = _grid_forward_gpu(x, emb, offs, spec, max_level=max_level, dy=True,
+                                 gridtype=gridtype, align=align, interp=interp, cuda=cuda)
+    ref, rdy = enc.grid_encode_forward(x, emb, offs, spec.num_levels, spec.S, 16,
+                                       max_level=max_level, calc_dy_dx=True, gridtype=gridtype,
+                                       align_corners=align, interp=interp)
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_allclose(gdy, rdy, rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("name", ["s_grid_L16C8", "prop0_L5C2"])
+def test_grid_backward_matches_oracle(hip_lib, oracle_lib, cuda, name):
+    import _gridencoder
+    spec, scale = GRID_CONFIGS[name]
+    offs = spec.offsets()
+    L, C = spec.num_levels, spec.level_dim
+    emb = synth.uniform(12, name, (int(offs[-1]), C), -scale, scale)
+    x = _points(8192, 2)
+    g = np.random.default_rng(4).standard_normal((L, x.shape[0], C)).astype(np.float32)
+    ge = torch.zeros(emb.shape, device=cuda)
+    _gridencoder.grid_encode_backward(torch.from_numpy(g).to(cuda), torch.from_numpy(x).to(cuda),
+                                      torch.from_numpy(emb).to(cuda), torch.from_numpy(offs).to(cuda),
+                                      ge, x.shape[0], 3, C, L, L, spec.S, 16, None, None, 0, False, 0)
+    ref = enc.grid_encode_backward(g, x, emb, offs, L, spec.S, 16)
+    # float atomics: order-dependent rounding; coarse rows collect ~1e4 adds
+    np.testing.assert_allclose(ge.cpu().numpy(), ref, rtol=1e-4, atol=2e-5)
+
+
+def test_grid_input_backward_matches_oracle(hip_lib, oracle_lib, cuda):
+    import _gridencoder
+    spec = synth.GridSpec(5, 4, 12, 100)
+    offs = spec.offsets()
+    emb = synth.uniform(5, "ib", (int(offs[-1]), 4), -1, 1)
+    x = _points(2048, 3, oob=False)
+    _, rdy = enc.grid_encode_forward(x, emb, offs, 5, spec.S, 16, calc_dy_dx=True)
+    g = np.random.default_rng(5).standard_normal((5, 2048, 4)).astype(np.float32)
+    ref_ge, ref_gi = enc.grid_encode_backward(g, x, emb, offs, 5, spec.S, 16, dy_dx=rdy)
+    ge = torch.zeros(emb.shape, device=cuda)
+    gi = torch.zeros(2048, 3, device=cuda)
+    _gridencoder.grid_encode_backward(torch.from_numpy(g).to(cuda), torch.from_numpy(x).to(cuda),
+                                      torch.from_numpy(emb).to(cuda), torch.from_numpy(offs).to(cuda),
+                                      ge, 2048, 3, 4, 5, 5, spec.S, 16,
+                                      torch.from_numpy(rdy).to(cuda), gi, 0, False, 0)
+    np.testing.assert_allclose(gi.cpu().numpy(), ref_gi, rtol=1e-5, atol=1e-4)
+
+
+def test_grid_encoder_module_autograd(hip_lib, oracle_lib, cuda):
+    """GridEncoder.forward/backward through torch autograd (grid.py contract)."""
+    from gridencoder import GridEncoder
+    g = GridEncoder(num_levels=5, level_dim=2, log2_hashmap_size=17, desired_resolution=128).to(cuda)
+    with torch.no_grad():
+        g.embeddings.uniform_(-0.5, 0.5)
+    x = (torch.rand(4096, 3, device=cuda) * 4 - 2)
+    y = g(x, bound=2)
+    assert y.shape == (4096, 10)
+    ref = enc.grid_encode_forward(((x + 2) / 4).cpu().numpy(), g.embeddings.detach().cpu().numpy(),
+                                  g.offsets_host, 5, g.S, 16)
+    np.testing.assert_array_equal(y.detach().cpu().numpy(), ref.transpose(1, 0, 2).reshape(4096, 10))
+    w = torch.randn_like(y)
+    (y * w).sum().backward()
+    refg = enc.grid_encode_backward(w.cpu().numpy().reshape(4096, 5, 2).transpose(1, 0, 2),
+                                    ((x + 2) / 4).cpu().numpy(), g.embeddings.detach().cpu().numpy(),
+                                    g.offsets_host, 5, g.S, 16)
+    np.testing.assert_allclose(g.embeddings.grad.cpu().numpy(), refg, rtol=1e-4, atol=1e-5)
+
+
+def test_tv_and_weight_decay_match_oracle(hip_lib, oracle_lib, cuda):
+    from gridencoder import GridEncoder
+    g = GridEncoder(num_levels=5, level_dim=2, log2_hashmap_size=12, desired_resolution=64).to(cuda)
+    with torch.no_grad():
+        g.embeddings.uniform_(-1, 1)
+    g.embeddings.grad = torch.zeros_like(g.embeddings)
+    pts = torch.rand(2000, 3, device=cuda) * 2 - 1
+    g.grad_total_variation(1e-2, inputs=pts, bound=1)
+    ref = enc.grad_total_variation(((pts + 1) / 2).cpu().numpy(), g.embeddings.detach().cpu().numpy(),
+                                   np.zeros(g.embeddings.shape, np.float32), g.offsets_host, 1e-2,
+                                   5, g.S, 16)
+    np.testing.assert_allclose(g.embeddings.grad.cpu().numpy(), ref, rtol=1e-4, atol=1e-7)
+    g.embeddings.grad.zero_()
+    g.grad_weight_decay(0.1)
+    ref = enc.grad_weight_decay(g.embeddings.detach().cpu().numpy(),
+                                np.zeros(g.embeddings.shape, np.float32), g.offsets_host, 0.1, 5)
+    np.testing.assert_allclose(g.embeddings.grad.cpu().numpy(), ref, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("degree", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_sh_forward_backward_match_oracle(hip_lib, oracle_lib, cuda, degree):
+    import _shencoder
+    rng = np.random.default_rng(degree)
+    d = rng.standard_normal((5000, 3))
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    ref, rdy = enc.sh_encode_forward(d, degree, calc_dy_dx=True)
+    di = torch.from_numpy(d).to(cuda)
+    out = torch.empty(5000, degree * degree, device=cuda)
+    dy = torch.empty(5000, 3 * degree * degree, device=cuda)
+    _shencoder.sh_encode_forward(di, out, 5000, 3, degree, dy)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(dy.cpu().numpy(), rdy, rtol=1e-5, atol=1e-5)
+    g = rng.standard_normal((5000, degree * degree)).astype(np.float32)
+    gi = torch.zeros(5000, 3, device=cuda)
+    _shencoder.sh_encode_backward(torch.from_numpy(g).to(cuda), di, 5000, 3, degree, dy, gi)
+    np.testing.assert_allclose(gi.cpu().numpy(), enc.sh_encode_backward(g, d, degree, rdy),
+                               rtol=1e-4, atol=1e-4)
+
+
+def test_sh_module_normalises_inputs(hip_lib, cuda):
+    from shencoder import SHEncoder
+    e = SHEncoder(3, 4).to(cuda)
+    d = torch.randn(100, 3, device=cuda)
+    assert torch.allclose(e(d), e(d * 7.5), atol=1e-6)
+
+
+def test_freq_forward_backward_match_oracle(hip_lib, oracle_lib, cuda):
+    from freqencoder import FreqEncoder
+    f = FreqEncoder(3, 6)
+    x = (torch.rand(4000, 3) * 2 - 1)
+    xi = x.to(cuda).requires_grad_(True)
+    y = f(xi)
+    ref = enc.freq_encode_forward(x.numpy(), 6)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), ref, rtol=1e-6, atol=1e-6)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    np.testing.assert_allclose(xi.grad.cpu().numpy(),
+                               enc.freq_encode_backward(g.cpu().numpy(), ref, 6),
+                               rtol=1e-4, atol=1e-4)
