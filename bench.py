@@ -88,7 +88,9 @@ def build_net(with_sam, device):
 def cpu_baseline(spec, params, pose, intr, H, W, n_rays):
     """Time the CPU oracle on the first n_rays rays of the same view."""
     from oracle import renderer as orc
-    threads = len(os.sched_getaffinity(0))
+    # the box exposes every host CPU but grants this job a share of them
+    # (OMP_NUM_THREADS, 16 per GPU); use the share, not the machine
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     torch.set_num_threads(threads)
     ro, rd = orc.get_rays(pose, intr, H, W)
     idx = torch.linspace(0, H * W - 1, n_rays).long()          # rays spread over the view

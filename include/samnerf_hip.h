@@ -113,7 +113,7 @@ int samnerf_freq_encode_backward(const float* grad, const float* outputs, uint32
 
 /* get_rays, full-image branch (nerf/utils.py:145-279, N = -1):
  * pose_host = row-major 4x4 cam2world (host), intrinsics (fx, fy, cx, cy);
- * rays_o, rays_d [H*W, 3] for pixel rows [row0, row0 + rows). */
+ * rays_o, rays_d [rows*W, 3]: the rays of pixel rows [row0, row0 + rows). */
 int samnerf_get_rays(const float* pose_host, float fx, float fy, float cx, float cy,
                      uint32_t H, uint32_t W, uint32_t row0, uint32_t rows,
                      float* rays_o, float* rays_d, samnerf_stream_t stream);

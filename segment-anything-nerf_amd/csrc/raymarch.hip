@@ -67,11 +67,16 @@ __device__ __forceinline__ void dense(const float* __restrict__ W, const float* 
     }
 }
 
-template <int L, int C>
+// Levels are issued in groups of GROUP (8 corner loads each) separated by a
+// scheduling barrier, bounding the loads in flight (and their VGPRs) per lane.
+template <int L, int C, int GROUP = 4>
 __device__ __forceinline__ void grid_features(const GridDesc<16>& g, float ux, float uy, float uz,
                                               float* feat) {
 #pragma unroll
-    for (int l = 0; l < L; ++l) lookup_level3<C>(g.emb, g.lv[l], ux, uy, uz, feat + l * C);
+    for (int l = 0; l < L; ++l) {
+        lookup_level3<C>(g.emb, g.lv[l], ux, uy, uz, feat + l * C);
+        if ((l + 1) % GROUP == 0 && l + 1 < L) __builtin_amdgcn_sched_barrier(0);
+    }
 }
 
 struct PropArgs {
@@ -152,12 +157,13 @@ __global__ void __launch_bounds__(256) k_prop(PropArgs a) {
         [&](int j, float v, int) { a.bins_out[(size_t)j * N + r] = v; });
 }
 
+struct Tables;
 struct FinalArgs {
     const float* rays_o;
     const float* rays_d;
     uint32_t N;
     float bound, bg;
-    GridDesc<16> grid;
+    const Tables* tab;
     const float* G0;   // grid_mlp [64,32]
     const float* G1;   // [64,64]
     const float* G2;   // [16,64]
@@ -174,76 +180,236 @@ struct FinalArgs {
     float* rows;       // [N, kRow] or null
 };
 
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// Per-call grid geometry, copied into the workspace by k_put_tables so the
+// march kernels read it with scalar loads at a runtime level index (a
+// by-value kernel argument indexed dynamically would go through scratch).
+struct Tables {
+    GridDesc<16> grid, s_grid, prop0, prop1;
+};
+
+__global__ void k_put_tables(Tables t, Tables* __restrict__ dst) {
+    if (threadIdx.x == 0) *dst = t;
+}
+
+// ---- MFMA weight fragments (v_mfma_f32_32x32x2_f32, transposed orientation:
+// rows = hidden units, columns = 32 rays).  ρ(q) = (q&3) + 8(q>>2) is the row
+// that accumulator register q holds in the lower half-wave (+4 in the upper),
+// so a layer's accumulator is the next layer's B operand as it stands and the
+// weights (A operand) are stored permuted to match.
+constexpr int kW1 = 0;               // grid_mlp.0 [ob 2][level 16][lane]   W[64,32]
+constexpr int kW2 = 2048;            // grid_mlp.1 [ob 2][ob' 2][q 16][lane] W[64,64]
+constexpr int kW3 = 6144;            // grid_mlp.2 [ob' 2][q 16][lane]       W[16,64]
+constexpr int kV1 = 8192;            // view_mlp.0 [q 16][lane]  q<8: geo acc rows, q>=8: sh pairs
+constexpr int kV2 = 9216;            // view_mlp.1 [q 16][lane]              W[32,32]
+constexpr int kV3 = 10240;           // view_mlp.2 [q 16][lane]              W[3,32]
+constexpr int kWTotal = 11264;
+
+__device__ __forceinline__ int rho(int q) { return (q & 3) + 8 * (q >> 2); }
+
+__device__ float weight_fragment(const FinalArgs& a, int idx) {
+    const int lane = idx & 63, i = lane & 31, h = lane >> 5;
+    if (idx < kW2) {                           // k = 2*level + h
+        const int s = (idx >> 6) & 15, ob = idx >> 10;
+        return a.G0[(ob * 32 + i) * 32 + 2 * s + h];
+    }
+    if (idx < kW3) {
+        const int q = idx - kW2;
+        const int r = (q >> 6) & 15, obp = (q >> 10) & 1, ob = q >> 11;
+        return a.G1[(ob * 32 + i) * 64 + obp * 32 + rho(r) + 4 * h];
+    }
+    if (idx < kV1) {
+        const int q = idx - kW3;
+        const int r = (q >> 6) & 15, obp = q >> 10;
+        return i < 16 ? a.G2[i * 64 + obp * 32 + rho(r) + 4 * h] : 0.0f;
+    }
+    if (idx < kV2) {                           // f_image = [geo (units 1..15), sh * wsum]
+        const int r = (idx - kV1) >> 6;
+        if (r < 8) {
+            const int unit = rho(r) + 4 * h;   // grid_mlp output row; unit 0 is sigma
+            return unit >= 1 ? a.V0[i * 31 + unit - 1] : 0.0f;
+        }
+        return a.V0[i * 31 + 15 + 2 * (r - 8) + h];
+    }
+    if (idx < kV3) {
+        const int r = (idx - kV2) >> 6;
+        return a.V1[i * 32 + rho(r) + 4 * h];
+    }
+    const int r = (idx - kV3) >> 6;
+    return i < 3 ? a.V2[i * 32 + rho(r) + 4 * h] : 0.0f;
+}
+
+#define MFMA32(A, B, C) __builtin_amdgcn_mfma_f32_32x32x2f32((A), (B), (C), 0, 0, 0)
+
+// One wave marches 32 rays.  Lane (h, j) owns ray j and feature channel h:
+// for level l it gathers channel h of the 8 corners of ray j -- which is
+// exactly the B operand of k-step l of the first layer -- so the hash-grid
+// gather feeds the matrix cores with no data movement.  grid_mlp
+// 32->64->64->16 and view_mlp 31->32->32->3 run as 32x32x2 f32 MFMAs
+// (exact fp32 fma chains); compositing runs in-lane (both half-waves hold
+// the same ray and compute the same weights).
 template <int T>
 __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= a.N) return;
+    __shared__ float Wl[kWTotal];
+    for (int i = threadIdx.x; i < kWTotal; i += 256) Wl[i] = weight_fragment(a, i);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int hh = lane >> 5, jj = lane & 31;
+    const uint32_t ray0 = blockIdx.x * 128u + wave * 32u;
+    if (ray0 >= a.N) return;                             // wave-uniform
+    const uint32_t r = ray0 + jj;
+    const bool live = r < a.N;
+    const uint32_t rr = live ? r : a.N - 1;
+    const bool writer = live && hh == 0;
     const uint32_t N = a.N;
+    const GridDesc<16>* __restrict__ G = &a.tab->grid;
+    const float* __restrict__ emb = a.tab->grid.emb;
+
     float o[3], d[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        o[c] = a.rays_o[(size_t)r * 3 + c];
-        d[c] = a.rays_d[(size_t)r * 3 + c];
+        o[c] = a.rays_o[(size_t)rr * 3 + c];
+        d[c] = a.rays_d[(size_t)rr * 3 + c];
     }
-    const float sn = a.snf[r], sf = a.snf[N + r];
-    // view direction: normalised by the renderer (renderer.py:295) and again
-    // by SHEncoder.forward (sphere_harmonics.py:82); SH degree 4 per ray.
+    const float sn = a.snf[rr], sf = a.snf[N + rr];
+    const float b2 = 2.0f * a.bound;
+    float rb_prev = real_bin(sn, sf, a.bins_in[rr]);
+    double cum = 0.0, wsum = 0.0, depth = 0.0;
+    float fg[8];                                          // sum_k w_k * grid_mlp rows (acc layout)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) fg[q] = 0.0f;
+
+    for (int k = 0; k < T; ++k) {
+        const float rb_next = real_bin(sn, sf, a.bins_in[(size_t)(k + 1) * N + rr]);
+        const float t = (rb_next + rb_prev) / 2.0f;
+        float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
+        contract3(x, y, z);
+        const float ux = (x + a.bound) / b2, uy = (y + a.bound) / b2, uz = (z + a.bound) / b2;
+        if (writer) {
+            a.u_out[((size_t)k * 3 + 0) * N + r] = ux;
+            a.u_out[((size_t)k * 3 + 1) * N + r] = uy;
+            a.u_out[((size_t)k * 3 + 2) * N + r] = uz;
+        }
+        // weight fragments are re-read from LDS each sample (1 ds_read per
+        // 64-cycle MFMA) rather than hoisted into VGPRs for the whole loop
+        int wo = lane;
+        asm volatile("" : "+v"(wo));
+        const float* W = Wl + wo;
+        // gather + layer 1, level by level
+        floatx16 h1a = {}, h1b = {};
+#pragma unroll 2
+        for (int l = 0; l < 16; ++l) {
+            const LevelDesc dl = G->lv[l];
+            uint32_t cx, cy, cz;
+            float fx, fy, fz;
+            locate_axis(ux, dl.res, cx, fx);
+            locate_axis(uy, dl.res, cy, fy);
+            locate_axis(uz, dl.res, cz, fz);
+            const uint32_t top = dl.res - 1u;
+            const uint32_t nx = min(cx + 1u, top), ny = min(cy + 1u, top), nz = min(cz + 1u, top);
+            const float* base = emb + dl.off * 2u + (uint32_t)hh;
+            float f = 0.0f;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float wx = (c & 1) ? fx : 1.0f - fx;
+                const float wy = (c & 2) ? fy : 1.0f - fy;
+                const float wz = (c & 4) ? fz : 1.0f - fz;
+                const uint32_t row = dense_or_hash_row((c & 1) ? nx : cx, (c & 2) ? ny : cy,
+                                                       (c & 4) ? nz : cz, dl);
+                f = __builtin_fmaf((wx * wy) * wz, base[row * 2u], f);
+            }
+            h1a = MFMA32(W[kW1 + (0 * 16 + l) * 64], f, h1a);
+            h1b = MFMA32(W[kW1 + (1 * 16 + l) * 64], f, h1b);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            h1a[i] = fmaxf(h1a[i], 0.0f);
+            h1b[i] = fmaxf(h1b[i], 0.0f);
+        }
+        floatx16 h2a = {}, h2b = {};
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            h2a = MFMA32(W[kW2 + ((0 * 2 + 0) * 16 + q) * 64], h1a[q], h2a);
+            h2b = MFMA32(W[kW2 + ((1 * 2 + 0) * 16 + q) * 64], h1a[q], h2b);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            h2a = MFMA32(W[kW2 + ((0 * 2 + 1) * 16 + q) * 64], h1b[q], h2a);
+            h2b = MFMA32(W[kW2 + ((1 * 2 + 1) * 16 + q) * 64], h1b[q], h2b);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            h2a[i] = fmaxf(h2a[i], 0.0f);
+            h2b[i] = fmaxf(h2b[i], 0.0f);
+        }
+        floatx16 o3 = {};
+#pragma unroll
+        for (int q = 0; q < 16; ++q) o3 = MFMA32(W[kW3 + (0 * 16 + q) * 64], h2a[q], o3);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) o3 = MFMA32(W[kW3 + (1 * 16 + q) * 64], h2b[q], o3);
+
+        // sigma pre-activation = row 0, held by the lower half-wave
+        const float s_lo = o3[0];
+        const float s_hi = __shfl_xor(s_lo, 32);
+        const float sigma = expf(hh == 0 ? s_lo : s_hi);
+        const float w = composite_step((rb_next - rb_prev) * sigma, cum, k == T - 1);
+        if (writer) a.w_out[(size_t)k * N + r] = w;
+        wsum += (double)w;
+        depth += (double)(w * t);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) fg[q] = fg[q] + w * o3[q];
+        rb_prev = rb_next;
+    }
+
+    // view MLP on the accumulated colour features: rows 1..15 of fg are
+    // f_image[0..14] (geo), f_image[15..30] = sh * sum(w) (colour = cat(geo, sh)
+    // with sh constant along the ray, renderer.py:338; a rounding-level
+    // reassociation of the reference's sum of products)
     float dx = d[0], dy = d[1], dz = d[2];
     normalize3(dx, dy, dz);
     normalize3(dx, dy, dz);
     float sh[16];
     sh_values<4>(dx, dy, dz, sh);
-
-    const float b2 = 2.0f * a.bound;
-    float rb_prev = real_bin(sn, sf, a.bins_in[r]);
-    double cum = 0.0, wsum = 0.0, depth = 0.0;
-    float fimg[31];
-#pragma unroll
-    for (int i = 0; i < 31; ++i) fimg[i] = 0.0f;
-
-    for (int k = 0; k < T; ++k) {
-        const float rb_next = real_bin(sn, sf, a.bins_in[(size_t)(k + 1) * N + r]);
-        const float t = (rb_next + rb_prev) / 2.0f;
-        float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
-        contract3(x, y, z);
-        const float ux = (x + a.bound) / b2, uy = (y + a.bound) / b2, uz = (z + a.bound) / b2;
-        a.u_out[((size_t)k * 3 + 0) * N + r] = ux;
-        a.u_out[((size_t)k * 3 + 1) * N + r] = uy;
-        a.u_out[((size_t)k * 3 + 2) * N + r] = uz;
-        float feat[32];
-        grid_features<16, 2>(a.grid, ux, uy, uz, feat);
-        float h1[64], h2[64], out[16];
-        dense<64, 32, true>(a.G0, feat, h1);
-        dense<64, 64, true>(a.G1, h1, h2);
-        dense<16, 64, false>(a.G2, h2, out);
-        const float sigma = expf(out[0]);
-        const float w = composite_step((rb_next - rb_prev) * sigma, cum, k == T - 1);
-        a.w_out[(size_t)k * N + r] = w;
-        wsum += (double)w;
-        depth += (double)(w * t);
-#pragma unroll
-        for (int i = 0; i < 15; ++i) fimg[i] = fimg[i] + w * out[1 + i];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) fimg[15 + i] = fimg[15 + i] + w * sh[i];
-        rb_prev = rb_next;
-    }
-    float v1[32], v2[32], v3[3];
-    dense<32, 31, true>(a.V0, fimg, v1);
-    dense<32, 32, true>(a.V1, v1, v2);
-    dense<3, 32, false>(a.V2, v2, v3);
     const float ws = (float)wsum, dp = (float)depth;
+    floatx16 v1 = {};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v1 = MFMA32(Wl[kV1 + q * 64 + lane], fg[q], v1);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) v1 = MFMA32(Wl[kV1 + (8 + s) * 64 + lane], sh[2 * s + hh] * ws, v1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v1[i] = fmaxf(v1[i], 0.0f);
+    floatx16 v2 = {};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v2 = MFMA32(Wl[kV2 + q * 64 + lane], v1[q], v2);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v2[i] = fmaxf(v2[i], 0.0f);
+    floatx16 v3 = {};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v3 = MFMA32(Wl[kV3 + q * 64 + lane], v2[q], v3);
+
+    if (!live) return;
+    float* row = a.rows ? a.rows + (size_t)r * kRow : nullptr;
+    if (row) {                                 // geo units owned by this half-wave
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int unit = rho(q) + 4 * hh;
+            if (unit >= 1) row[128 + unit - 1] = fg[q];
+        }
+    }
+    if (hh != 0) return;
     float img[3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
+    for (int c = 0; c < 3; ++c) {                // rows 0..2 of v3 = registers 0..2, lower half
         img[c] = sigmoidf(v3[c]) + (1.0f - ws) * a.bg;
         a.image[(size_t)r * 3 + c] = img[c];
     }
     a.depth[r] = dp;
     a.wsum[r] = ws;
-    if (a.rows) {
-        float* row = a.rows + (size_t)r * kRow;
+    if (row) {
 #pragma unroll
-        for (int i = 0; i < 31; ++i) row[128 + i] = fimg[i];
+        for (int i = 0; i < 16; ++i) row[143 + i] = sh[i] * ws;
         row[159] = img[0];
         row[160] = img[1];
         row[161] = img[2];
@@ -342,12 +508,13 @@ k_get_rays(float r00, float r01, float r02, float r10, float r11, float r12, flo
     const float ys = -((j - cy) / fy);
     const float zs = -1.0f;
     // directions @ R^T  (utils.py:255-256)
-    rays_d[(size_t)p * 3 + 0] = __builtin_fmaf(zs, r02, __builtin_fmaf(ys, r01, xs * r00));
-    rays_d[(size_t)p * 3 + 1] = __builtin_fmaf(zs, r12, __builtin_fmaf(ys, r11, xs * r10));
-    rays_d[(size_t)p * 3 + 2] = __builtin_fmaf(zs, r22, __builtin_fmaf(ys, r21, xs * r20));
-    rays_o[(size_t)p * 3 + 0] = tx;
-    rays_o[(size_t)p * 3 + 1] = ty;
-    rays_o[(size_t)p * 3 + 2] = tz;
+    // outputs hold only this band: local ray index t
+    rays_d[(size_t)t * 3 + 0] = __builtin_fmaf(zs, r02, __builtin_fmaf(ys, r01, xs * r00));
+    rays_d[(size_t)t * 3 + 1] = __builtin_fmaf(zs, r12, __builtin_fmaf(ys, r11, xs * r10));
+    rays_d[(size_t)t * 3 + 2] = __builtin_fmaf(zs, r22, __builtin_fmaf(ys, r21, xs * r20));
+    rays_o[(size_t)t * 3 + 0] = tx;
+    rays_o[(size_t)t * 3 + 1] = ty;
+    rays_o[(size_t)t * 3 + 2] = tz;
 }
 
 struct Aabb {
@@ -425,6 +592,7 @@ struct Workspace {
     float* w_f;
     float* rows;
     float* packed;
+    Tables* tables;
     size_t bytes;
 };
 
@@ -434,7 +602,7 @@ thread_local hipEvent_t g_stage_events[8];
 thread_local uint32_t g_n_stage_events = 0;
 
 void mark_stage(uint32_t i, hipStream_t s) {
-    if (i < g_n_stage_events && g_stage_events[i]) hipEventRecord(g_stage_events[i], s);
+    if (i < g_n_stage_events && g_stage_events[i]) (void)hipEventRecord(g_stage_events[i], s);
 }
 
 Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
@@ -455,6 +623,7 @@ Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
     w.w_f = take((size_t)m->num_steps[2] * n);
     w.rows = take((size_t)kRow * n);
     w.packed = take(m->with_sam ? sam_head_packed_floats() : 0);
+    w.tables = reinterpret_cast<Tables*>(take((sizeof(Tables) + 3) / 4));
     w.bytes = off;
     return w;
 }
@@ -473,9 +642,14 @@ int make_grid_desc(const samnerf_grid& g, uint32_t C, uint32_t L, GridDesc<16>& 
             const uint32_t off = (uint32_t)g.offsets_host[l];
             const uint32_t size = (uint32_t)(g.offsets_host[l + 1] - g.offsets_host[l]);
             d.lv[l] = make_level(off, size, rt.res[l], 0u);
-            if (!(d.lv[l].flags & kHashed) &&
-                (uint64_t)rt.res[l] * rt.res[l] * rt.res[l] > size)
+            const bool hashed = d.lv[l].flags & kHashed;
+            if (!hashed && (uint64_t)rt.res[l] * rt.res[l] * rt.res[l] > size)
                 return fail(SAMNERF_EINVAL, "render: %s level %u is neither dense nor hashed", name, l);
+            if (hashed && (size & (size - 1u)))
+                return fail(SAMNERF_EINVAL, "render: %s level %u hashes into a non power-of-two table",
+                            name, l);
+            if ((uint64_t)(off + size) * C >= (1ull << 32))
+                return fail(SAMNERF_EINVAL, "render: %s exceeds 2^32 elements", name);
         } else {
             d.lv[l] = LevelDesc{0, 1, 1, 0};
         }
@@ -575,6 +749,12 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     if (m->with_sam && (rc = make_grid_desc(m->s_grid, 8, 16, gs, "s_grid"))) return rc;
 
     const uint32_t nb = div_up(N, 256);
+    Tables tabs;
+    tabs.grid = gg;
+    tabs.s_grid = m->with_sam ? gs : gg;
+    tabs.prop0 = gp0;
+    tabs.prop1 = gp1;
+    k_put_tables<<<1, 64, 0, s>>>(tabs, w.tables);
     PropArgs pa{};
     pa.rays_o = rays_o;
     pa.rays_d = rays_d;
@@ -615,7 +795,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.N = N;
     fa.bound = m->grid_bound;
     fa.bg = bg_color;
-    fa.grid = gg;
+    fa.tab = w.tables;
     fa.G0 = m->grid_mlp[0];
     fa.G1 = m->grid_mlp[1];
     fa.G2 = m->grid_mlp[2];
@@ -631,7 +811,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.wsum = weights_sum;
     fa.rows = m->with_sam || feature_rows ? rows : nullptr;
     mark_stage(2, s);
-    k_final<32><<<nb, 256, 0, s>>>(fa);
+    k_final<32><<<div_up(N, 128), 256, 0, s>>>(fa);
 
     if (m->with_sam) {
         SgridArgs sa{};

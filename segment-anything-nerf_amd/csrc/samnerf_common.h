@@ -64,14 +64,14 @@ __device__ __forceinline__ void locate_axis(float u, uint32_t res, uint32_t& cel
     frac = p - (float)cell;
 }
 
+// Fused-path row index.  The host (make_grid_desc) only admits levels that
+// are either dense with res^3 <= size (row < size, the reference's
+// `% size` is the identity) or hashed into a power-of-two table (`% size` is a
+// mask), so no integer division is ever emitted.
 __device__ __forceinline__ uint32_t dense_or_hash_row(uint32_t x, uint32_t y, uint32_t z,
                                                       const LevelDesc& d) {
-    uint32_t r;
-    if (d.flags & kHashed)
-        r = x ^ (y * kPrime1) ^ (z * kPrime2);
-    else
-        r = x + y * d.res + z * (d.res * d.res);
-    return (d.flags & kPow2) ? (r & (d.size - 1u)) : (r % d.size);
+    if (d.flags & kHashed) return (x ^ (y * kPrime1) ^ (z * kPrime2)) & (d.size - 1u);
+    return x + y * d.res + z * (d.res * d.res);
 }
 
 template <int N>
@@ -109,7 +109,7 @@ __device__ __forceinline__ void lookup_level3(const float* __restrict__ emb, con
     locate_axis(uz, d.res, cz, fz);
     const uint32_t top = d.res - 1u;
     const uint32_t nx = min(cx + 1u, top), ny = min(cy + 1u, top), nz = min(cz + 1u, top);
-    const float* base = emb + (size_t)d.off * C;
+    const float* base = emb + d.off * (uint32_t)C;      // 32-bit element offsets
 #pragma unroll
     for (int i = 0; i < C; ++i) acc[i] = 0.0f;
 #pragma unroll
@@ -121,7 +121,7 @@ __device__ __forceinline__ void lookup_level3(const float* __restrict__ emb, con
         const uint32_t row = dense_or_hash_row((c & 1) ? nx : cx, (c & 2) ? ny : cy,
                                                (c & 4) ? nz : cz, d);
         float e[C];
-        load_row<C>(base + (size_t)row * C, e);
+        load_row<C>(base + row * (uint32_t)C, e);
 #pragma unroll
         for (int i = 0; i < C; ++i) acc[i] = __builtin_fmaf(w, e[i], acc[i]);
     }

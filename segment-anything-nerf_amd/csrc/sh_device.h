@@ -32,6 +32,22 @@ constexpr double sh_q0(int m) {  // Q_m^m = (-1)^m (2m-1)!!
     return (m & 1) ? -d : d;
 }
 
+// All recurrence constants, evaluated at compile time.
+struct ShConst {
+    float k[8][8];     // sh_k(l, m)
+    float q0[8];       // Q_m^m
+    float inv[9];      // 1 / n
+};
+constexpr ShConst make_sh_const() {
+    ShConst c{};
+    for (int l = 0; l < 8; ++l)
+        for (int m = 0; m <= l; ++m) c.k[l][m] = (float)sh_k(l, m);
+    for (int m = 0; m < 8; ++m) c.q0[m] = (float)sh_q0(m);
+    for (int n = 1; n < 9; ++n) c.inv[n] = (float)(1.0 / (double)n);
+    return c;
+}
+constexpr ShConst kShConst = make_sh_const();
+
 struct Dual {
     float v, dx, dy, dz;
 };
@@ -59,16 +75,16 @@ __device__ __forceinline__ void sh_values(float x, float y, float z, float* out)
     }
 #pragma unroll
     for (int m = 0; m < DEG; ++m) {
-        float qp = 0.0f, q = (float)sh_q0(m);
+        float qp = 0.0f, q = kShConst.q0[m];
 #pragma unroll
         for (int l = m; l < DEG; ++l) {
             if (l > m) {
                 float t = ((float)(2 * l - 1) * (z * q) - (float)(l + m - 1) * qp) *
-                          (float)(1.0 / (double)(l - m));
+                          kShConst.inv[l - m];
                 qp = q;
                 q = t;
             }
-            const float k = (float)sh_k(l, m);
+            const float k = kShConst.k[l][m];
             out[l * l + l + m] = (q * cm[m]) * k;
             if (m > 0) out[l * l + l - m] = (q * sm[m]) * k;
         }
@@ -90,16 +106,16 @@ __device__ __forceinline__ void sh_values_grad(float x, float y, float z, float*
     }
 #pragma unroll
     for (int m = 0; m < DEG; ++m) {
-        Dual qp{0, 0, 0, 0}, q{(float)sh_q0(m), 0, 0, 0};
+        Dual qp{0, 0, 0, 0}, q{kShConst.q0[m], 0, 0, 0};
 #pragma unroll
         for (int l = m; l < DEG; ++l) {
             if (l > m) {
                 Dual t = dsub(dsc(dmul(Z, q), (float)(2 * l - 1)), dsc(qp, (float)(l + m - 1)));
-                t = dsc(t, (float)(1.0 / (double)(l - m)));
+                t = dsc(t, kShConst.inv[l - m]);
                 qp = q;
                 q = t;
             }
-            const float k = (float)sh_k(l, m);
+            const float k = kShConst.k[l][m];
             const Dual p = dsc(dmul(q, cm[m]), k);
             const int ip = l * l + l + m;
             out[ip] = p.v;
