@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--H", type=int, default=512)
     ap.add_argument("--W", type=int, default=512)
     ap.add_argument("--no-sam", action="store_true", help="config 2 (RGB only)")
-    ap.add_argument("--cpu-rays", type=int, default=4096,
+    ap.add_argument("--cpu-rays", type=int, default=262144,
                     help="rays in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
@@ -100,7 +100,7 @@ def cpu_baseline(spec, params, pose, intr, H, W, n_rays):
     model.render(ro[idx], rd[idx], return_feats=1)
     dt = time.perf_counter() - t0
     return {"value": n_rays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
-            "sample": f"{n_rays} rays spread over the {H}x{W} view (same weights); torch-CPU "
+            "sample": f"{n_rays} rays of the {H}x{W} view (same weights, chunks of 16384 as renderer.py:195); torch-CPU "
                       f"restatement of nerf/renderer.py+network.py, encoders in C "
                       f"(OpenMP over points); {dt:.1f} s"}
 

@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(256) k_prop(PropArgs a) {
 
     const float b2 = 2.0f * a.bound;
     float rb_prev = real_bin(sn, sf, bin(0));
-    double cum = 0.0, wacc = 0.0;
+    double cum = 0.0;
     for (int k = 0; k < T; ++k) {
         const float rb_next = real_bin(sn, sf, bin(k + 1));
         const float t = (rb_next + rb_prev) / 2.0f;
@@ -148,10 +148,9 @@ __global__ void __launch_bounds__(256) k_prop(PropArgs a) {
         const float sigma = expf(s);                       // trunc_exp forward
         const float w = composite_step((rb_next - rb_prev) * sigma, cum, k == T - 1);
         a.wtmp[(size_t)k * N + r] = w;
-        wacc += (double)(w + 0.01f);
         rb_prev = rb_next;
     }
-    const float wsum = (float)wacc;
+    const float wsum = torch_row_sum(T, [&](int i) { return a.wtmp[(size_t)i * N + r] + 0.01f; });
     sample_pdf_walk(
         T, TN, a.u, wsum, [&](int i) { return a.wtmp[(size_t)i * N + r]; }, bin,
         [&](int j, float v, int) { a.bins_out[(size_t)j * N + r] = v; });
@@ -552,10 +551,9 @@ k_sample_pdf(const float* __restrict__ bins, const float* __restrict__ weights, 
     if (r >= N) return;
     const float* w = weights + (size_t)r * T0;
     const float* b = bins + (size_t)r * (T0 + 1);
-    double acc = 0.0;
-    for (uint32_t i = 0; i < T0; ++i) acc += (double)(w[i] + 0.01f);
+    const float wsum = torch_row_sum((int)T0, [&](int i) { return w[i] + 0.01f; });
     sample_pdf_walk(
-        (int)T0, (int)T, u, (float)acc, [&](int i) { return w[i]; },
+        (int)T0, (int)T, u, wsum, [&](int i) { return w[i]; },
         [&](int i) { return b[i]; },
         [&](int j, float v, int ind) {
             out[(size_t)r * T + j] = v;

@@ -81,10 +81,47 @@ __device__ __forceinline__ float composite_step(float ds, double& cum, bool last
     return nan_to_num(alpha * trans);
 }
 
+// torch.sum over a contiguous float row exactly as ATen's CPU kernel orders
+// it (vectorized_inner_sum: Vectorized<float> of 8 lanes, 4 accumulators
+// taking vectors round-robin, combined in sequence, scalar tail first, then
+// the 8 lanes in sequence) -- the order tests/test_oracle.py pins against
+// torch.sum.  Used for the pdf normaliser of sample_pdf (renderer.py:92) so
+// searchsorted indices match the reference on identical inputs.
+template <class XF>
+__device__ __forceinline__ float torch_row_sum(int n, XF X) {
+    float acc[4][8];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int l = 0; l < 8; ++l) acc[m][l] = 0.0f;
+    const int nv = n / 8;
+    int v = 0;
+    for (; v + 4 <= nv; v += 4)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc[m][l] = acc[m][l] + X((v + m) * 8 + l);
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+        if (v + m < nv)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc[m][l] = acc[m][l] + X((v + m) * 8 + l);
+    float t = 0.0f;
+    for (int k = nv * 8; k < n; ++k) t = t + X(k);
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        float a = acc[0][l];
+#pragma unroll
+        for (int m = 1; m < 4; ++m) a = a + acc[m][l];
+        t = t + a;
+    }
+    return t;
+}
+
 // Inverse-CDF resampling of one ray (renderer.py:84-119, perturb = False) by a
 // merge walk: cdf is the clamped double cumsum of (w + 0.01) / sum, u the
 // sorted linspace table, so searchsorted(right=True) is the number of cdf
-// entries <= u_j.  `wsum` = sum_i (w_i + 0.01) rounded to float.
+// entries <= u_j.  `wsum` = torch_row_sum of (w_i + 0.01).
 // U(j) returns u_j, W(i) weight i, BINS(i) bin i of the ray; EMIT(j, value, inds).
 template <class UF, class WF, class BF, class EF>
 __device__ __forceinline__ void sample_pdf_walk(int T0, int T, UF U, float wsum, WF W, BF BINS,

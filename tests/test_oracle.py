@@ -275,3 +275,32 @@ def test_freq_oracle_closed_form(oracle_lib):
         s = 3 + 6 * f
         ref = ref + 2.0 ** f * (g[:, s:s + 3] * np.cos(x * 2.0 ** f) - g[:, s + 3:s + 6] * np.sin(x * 2.0 ** f))
     np.testing.assert_allclose(gin, ref, rtol=1e-4, atol=1e-4)
+
+
+def test_torch_cpu_row_sum_order():
+    """The summation order the HIP sample_pdf normaliser reproduces
+    (raymarch_device.h torch_row_sum): 8-lane vectors, 4 round-robin
+    accumulators, scalar tail first, lanes in sequence -- equal to torch.sum
+    on the CPU bit for bit, for every row length on the path."""
+    f = np.float32
+
+    def emulate(x):
+        n = x.shape[1]
+        nv = n // 8
+        acc = [np.zeros((x.shape[0], 8), f) for _ in range(4)]
+        for v in range(nv):
+            acc[v % 4] = (acc[v % 4] + x[:, v * 8:(v + 1) * 8]).astype(f)
+        a = acc[0]
+        for m in range(1, 4):
+            a = (a + acc[m]).astype(f)
+        t = np.zeros(x.shape[0], f)
+        for k in range(nv * 8, n):
+            t = (t + x[:, k]).astype(f)
+        for l in range(8):
+            t = (t + a[:, l]).astype(f)
+        return t
+
+    g = torch.Generator().manual_seed(0)
+    for n in (32, 33, 64, 65, 128, 129):
+        x = torch.rand(2048, n, generator=g) ** 4 * 3 + 0.01
+        assert np.array_equal(emulate(x.numpy()), torch.sum(x, -1).numpy()), n

@@ -1,8 +1,23 @@
+#!/bin/bash
+# GPU-box check: build, smoke, parity tests, bench, rocprofv3 trace + PMC passes.
+# Every GPU step has its own time limit; a crash/timeout stops the script.
 set -o pipefail
-cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo BUILD FAIL; tail -30 gpurun_out/build.log; exit 1; }
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; echo "smoke rc=$?"; tail -5 gpurun_out/smoke.log
-timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
-[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-timeout -k 10 300 python bench.py --steps 5 --warmup 2 --cpu-rays 2048 > gpurun_out/bench.log 2>&1; echo "bench rc=$?"; tail -5 gpurun_out/bench.log
+cd "$GRAFT_REPO_ROOT"
+OUT="$GRAFT_REPO_ROOT/gpurun_out"
+mkdir -p "$OUT"
+stop_if_fatal() {  # $1 = rc, $2 = step
+  if [ "$1" -ge 124 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; then echo "FATAL rc=$1 in $2"; exit "$1"; fi
+}
+python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || { echo BUILD FAIL; tail -30 "$OUT/build.log"; exit 1; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"; stop_if_fatal $rc smoke
+if [ "${SKIP_TESTS:-0}" != "1" ]; then
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -rA > "$OUT/pytest_gpu.log" 2>&1; rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error" "$OUT/pytest_gpu.log" | tail -15; stop_if_fatal $rc pytest
+fi
+timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1; rc=$?; echo "bench rc=$rc"; tail -2 "$OUT/bench.log"; stop_if_fatal $rc bench
+if [ "${SKIP_PROF:-0}" != "1" ]; then
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_trace" -o trace -- python "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --cpu-rays 0 > "$OUT/prof_trace.log" 2>&1; rc=$?; echo "prof trace rc=$rc"; stop_if_fatal $rc prof_trace
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/prof_fetch" -o fetch -- python "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-rays 0 > "$OUT/prof_fetch.log" 2>&1; rc=$?; echo "prof fetch rc=$rc"; stop_if_fatal $rc prof_fetch
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/prof_write" -o write -- python "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-rays 0 > "$OUT/prof_write.log" 2>&1; rc=$?; echo "prof write rc=$rc"; stop_if_fatal $rc prof_write
+fi
+find "$OUT" -name "*.csv" | head -20
