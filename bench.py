@@ -175,7 +175,8 @@ def main():
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get(dom)
+            t = json.load(open(pmc)).get(dom)
+            traffic = t["hbm_bytes"] * band_rays / n_total if t else None
         except Exception:
             traffic = None
 

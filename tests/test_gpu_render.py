@@ -139,14 +139,16 @@ def test_fused_full_view_parity_on_sampled_rays(hip_lib, cuda):
     assert torch.isfinite(out["image"]).all() and torch.isfinite(sv).all()
     ws = out["weights_sum"]
     assert (ws > 0.999).all() and (ws < 1.001).all()          # last_sample background
-    # LayerNorm with unit gain / zero bias: every row has mean 0, variance 1
-    assert sv.mean(1).abs().max() < 1e-4 and (sv.var(1, unbiased=False) - 1).abs().max() < 1e-3
     idx = torch.from_numpy(np.random.default_rng(0).choice(512 * 512, 192, replace=False))
     ref = oracle_for(spec, params).run(ro[idx.to(cuda)].cpu(), rd[idx.to(cuda)].cpu(), return_feats=1)
     sub = {k: v[idx.to(cuda)] for k, v in out.items() if k != "samvit"}
     sub["samvit"] = sv[idx.to(cuda)]
     errs = _check_outputs(sub, ref)
     print("512x512 sampled", errs)
+    # LayerNorm with unit gain / zero bias: every row has mean 0 and variance
+    # var(x) / (var(x) + 1e-5) <= 1
+    var = sv.var(1, unbiased=False)
+    assert sv.mean(1).abs().max() < 1e-4 and var.max() < 1 + 1e-4 and var.median() > 0.9
 
 
 def test_fused_staged_and_cam_near_far(hip_lib, cuda):

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 outputs (gpurun_out/prof_*) into profiles/.
+
+  profiles/<tag>_kernel_stats.csv  -- rocprofv3 --kernel-trace --stats summary
+  profiles/<tag>_pmc.csv           -- per-kernel FETCH_SIZE / WRITE_SIZE averages
+  profiles/pmc_traffic.json        -- {stage: HBM bytes per launch} read by bench.py
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC EA requests).  Per
+MI355X_MICROARCH.md (HBM section) FETCH_SIZE reads 1/2 of the bytes of a WIDE
+(16 B/lane) coalesced stream; the gathers here are 4-8 B per lane, a width the
+guide lists as uncalibrated, so the raw (uncorrected) value is reported and
+`fetch_x2` gives the corrected upper bound.  Passes are separate runs
+(FETCH_SIZE needs 3 TCC slots, WRITE_SIZE 2).
+usage: python tools/summarize_prof.py --tag r1
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(REPO, "gpurun_out")
+PROF = os.path.join(REPO, "profiles")
+
+STAGE_OF = {"k_prop<128": "prop0", "k_prop<64": "prop1", "k_final": "final",
+            "k_sgrid<": "s_grid", "k_sam_head": "sam_head", "k_pack": "sam_pack",
+            "k_get_rays": "get_rays", "k_put_tables": "tables"}
+
+
+def stage(name):
+    for k, v in STAGE_OF.items():
+        if k in name:
+            return v
+    return None
+
+
+def pmc(path, counter):
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in d.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", default="r1")
+    a = ap.parse_args()
+    os.makedirs(PROF, exist_ok=True)
+    stats = os.path.join(OUT, "prof_trace", "trace_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(PROF, f"{a.tag}_kernel_stats.csv"))
+    fetch = pmc(os.path.join(OUT, "prof_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
+    write = pmc(os.path.join(OUT, "prof_write", "write_counter_collection.csv"), "WRITE_SIZE")
+    rows, traffic = [], {}
+    for k in sorted(set(fetch) | set(write)):
+        s = stage(k)
+        f, w = fetch.get(k, 0.0) * 1024, write.get(k, 0.0) * 1024
+        rows.append({"kernel": k[:90], "stage": s or "", "fetch_bytes": int(f),
+                     "write_bytes": int(w), "fetch_x2_bytes": int(2 * f)})
+        if s:
+            traffic[s] = {"hbm_bytes": int(f + w), "fetch_bytes": int(f), "write_bytes": int(w),
+                          "fetch_x2_bytes": int(2 * f),
+                          "note": "per launch; FETCH_SIZE uncorrected (gather width uncalibrated)"}
+    with open(os.path.join(PROF, f"{a.tag}_pmc.csv"), "w", newline="") as fh:
+        w = csv.DictWriter(fh, fieldnames=list(rows[0]))
+        w.writeheader()
+        w.writerows(rows)
+    json.dump(traffic, open(os.path.join(PROF, "pmc_traffic.json"), "w"), indent=1)
+    for r in rows:
+        print(r)
+
+
+if __name__ == "__main__":
+    main()
