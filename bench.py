@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--no-sam", action="store_true", help="config 2 (RGB only)")
     ap.add_argument("--cpu-rays", type=int, default=262144,
                     help="rays in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--head-mode", type=int, default=0, help="0 bf16x3 SAM head, 1 exact fp32")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="row chunks per rank band for the pipelined all-gather (0 = auto)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -110,19 +113,23 @@ def main():
     rank, world, dev = setup_dist(args)
     from samnerf_amd import ops
     from samnerf_amd._lib import lib
-    from samnerf_amd.dist import all_gather_rows, shard_range
+    from samnerf_amd.dist import render_view_sharded, shard_range
     from samnerf_amd.fused import FusedRenderer
     from oracle import synth
 
     with_sam = not args.no_sam
     net, spec, params = build_net(with_sam, dev)
-    renderer = FusedRenderer(net)
+    renderer = FusedRenderer(net, head_mode=args.head_mode)
     H, W = args.H, args.W
     pose, intr = synth.gui_camera(W, H)
     r0, r1 = shard_range(H, rank, world)                      # row band of this rank
     n_total = H * W
     band_rays = (r1 - r0) * W
-    width = 5 + (256 if with_sam else 0)
+    chunks = 1
+    if world > 1:
+        # enough chunks to hide the all-gather, each still large enough to
+        # fill the chip (>= 16384 rays)
+        chunks = args.chunks or max(1, min(4, band_rays // 16384))
 
     import ctypes
 
@@ -133,27 +140,31 @@ def main():
         raw = (ctypes.c_void_p * 6)(*[e.cuda_event for e in evs])
         return evs, raw
 
-    def step(raw=None):
-        lib().samnerf_set_stage_events(raw, 6 if raw is not None else 0)
-        ro, rd = ops.get_rays(pose, intr, H, W, device=dev, row0=r0, rows=r1 - r0)
-        out = renderer.render(ro, rd)
+    def step(raws=None):
+        it = iter(raws or [])
+
+        def ray_fn(row0, rows):
+            return ops.get_rays(pose, intr, H, W, device=dev, row0=row0, rows=rows)
+
+        def render_fn(ro, rd):
+            raw = next(it, None)
+            lib().samnerf_set_stage_events(raw, 6 if raw is not None else 0)
+            return renderer.render(ro, rd)
+
         if world > 1:
-            cols = [out["image"], out["depth"][:, None], out["weights_sum"][:, None]]
-            if with_sam:
-                cols.append(out["samvit"])
-            return all_gather_rows(torch.cat(cols, 1), n_total)
-        return out
+            return render_view_sharded(render_fn, ray_fn, H, W, chunks=chunks)
+        return render_fn(*ray_fn(r0, r1 - r0))
 
     for _ in range(args.warmup):
         step()
-    sets = [make_event_set() for _ in range(args.steps)]
+    sets = [[make_event_set() for _ in range(chunks)] for _ in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(sets[i][1])
+        step([raw for _, raw in sets[i]])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -163,9 +174,10 @@ def main():
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
-    stage_avg = {}
+    stage_avg = {}          # per step: summed over the chunks of the rank's band
     for j, s in enumerate(STAGES):
-        stage_avg[s] = float(np.mean([evs[j].elapsed_time(evs[j + 1]) for evs, _ in sets]))
+        stage_avg[s] = float(np.mean([sum(evs[j].elapsed_time(evs[j + 1]) for evs, _ in chunk_sets)
+                                      for chunk_sets in sets]))
 
     value = n_total * args.steps / dt
     dom = max(stage_avg, key=stage_avg.get)
@@ -184,12 +196,13 @@ def main():
         rec = {
             "metric": METRIC, "value": value, "unit": "rays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt * 1e3 / args.steps,
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32" if args.head_mode == 1 else "fp32 (SAM head: bf16x3 split-precision MFMA, fp32 accumulate)",
             "data": "synthetic (random-init weights of the reference architecture, GUI camera)",
             "config": {"workload": ("cfg3: 512x512 view, RGB + 256-d SAM feature per ray" if with_sam
                                     else "cfg2: 512x512 view, RGB only") if (H, W) == (512, 512)
                        else f"{H}x{W} view", "rays_per_step": n_total, "num_steps": [128, 64, 32],
-                       "parallelism": f"ray-sharded row bands x{world}, RCCL all-gather" if world > 1
+                       "parallelism": f"ray-sharded row bands x{world}, {chunks} chunk(s) per band, "
+                                      "async RCCL all-gather per chunk" if world > 1
                        else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

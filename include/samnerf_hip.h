@@ -170,6 +170,8 @@ typedef struct {
     float grid_bound;             /* 2 under contract (renderer.py:152-153) */
     float min_near;               /* main.py:69 */
     uint32_t num_steps[3];        /* (128, 64, 32), main.py:79-80 */
+    int head_mode;                /* SAM head GEMMs: 0 = bf16x3 split precision on bf16
+                                     MFMA (~1e-5 relative, default), 1 = exact fp32 MFMA */
 } samnerf_model;
 
 /* Bytes of device workspace samnerf_render_forward needs for N rays. */

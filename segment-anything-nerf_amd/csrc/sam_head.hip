@@ -205,12 +205,258 @@ __global__ void __launch_bounds__(256) k_sam_head(HeadArgs a) {
     }
 }
 
+
+// ===================================================================== bf16x3
+// Split-precision head: x = x_hi + x_lo with x_hi = bf16(x), x_lo =
+// bf16(x - x_hi); A.B ~= A_lo.B_hi + A_hi.B_lo + A_hi.B_hi on
+// v_mfma_f32_32x32x16_bf16 (fp32 accumulate).  Relative error per product
+// ~2^-16 (the dropped A_lo.B_lo term and the rounding of the lo parts),
+// i.e. ~1e-5 on the head output against the 1e-3 budget, at 3 bf16 MFMAs per
+// 16-deep k-block instead of 8 fp32 ones (5.3x fewer matrix cycles).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kXkB = 176;                 // head input padded to 11 k-blocks of 16
+constexpr int kRowB = 264;                // LDS row stride in bf16 (528 B = 16 mod 256: conflict-free b128 reads)
+constexpr int kRowsB = 64;                // rays per workgroup (2 row tiles x 4 column groups = 8 waves)
+constexpr int kThreadsB = 512;
+// k-block segments: 0 = W0 (x, 11), 1 = W1 (16), 2 = W2[:, :256] (h, 16),
+// 3 = W3 (16), 4 = W4 (16), 5 = W2[:, 256:] (x part of the skip layer, 11)
+constexpr int kKbB[6] = {11, 16, 16, 16, 16, 11};
+constexpr int kbBase(int seg) {
+    int b = 0;
+    for (int i = 0; i < seg; ++i) b += kKbB[i];
+    return b;
+}
+constexpr int kKbTotal = kbBase(6);       // 86
+
+__device__ __forceinline__ uint32_t bf16_rne(float x) {
+    uint32_t u = __float_as_uint(x);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return u >> 16;
+}
+__device__ __forceinline__ void split_bf16(float x, uint32_t& hi, uint32_t& lo) {
+    hi = bf16_rne(x);
+    lo = bf16_rne(x - __uint_as_float(hi << 16));
+}
+
+// packed_{hi,lo}[tile 8][global k-block 86][lane 64] : 8 bf16 (16 B) each
+__global__ void __launch_bounds__(256)
+k_pack_bf3(const float* __restrict__ w0, const float* __restrict__ w1, const float* __restrict__ w2,
+           const float* __restrict__ w3, const float* __restrict__ w4, uint4* __restrict__ phi,
+           uint4* __restrict__ plo) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 8u * kKbTotal * 64u) return;
+    const uint32_t lane = t & 63u, rest = t >> 6;
+    const uint32_t tile = rest / kKbTotal, gkb = rest % kKbTotal;
+    int seg = 0;
+    while (seg < 5 && (int)gkb >= kbBase(seg + 1)) ++seg;
+    const int kb = (int)gkb - kbBase(seg);
+    const float* W = seg == 0 ? w0 : seg == 1 ? w1 : (seg == 2 || seg == 5) ? w2 : seg == 3 ? w3 : w4;
+    const int ldw = seg == 0 ? kIn : (seg == 2 || seg == 5) ? 256 + kIn : 256;
+    const int col = (int)(tile * 32u + (lane & 31u));
+    uint32_t hi[8], lo[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int kp = kb * 16 + 8 * (int)(lane >> 5) + j;
+        int k = kp;                                   // logical weight column
+        if (seg == 0) k = kp < kIn ? kp : -1;
+        if (seg == 5) k = kp < kIn ? 256 + kp : -1;
+        const float v = k >= 0 ? W[(size_t)col * ldw + k] : 0.0f;
+        split_bf16(v, hi[j], lo[j]);
+    }
+    phi[t] = make_uint4(hi[0] | hi[1] << 16, hi[2] | hi[3] << 16, hi[4] | hi[5] << 16, hi[6] | hi[7] << 16);
+    plo[t] = make_uint4(lo[0] | lo[1] << 16, lo[2] | lo[3] << 16, lo[4] | lo[5] << 16, lo[6] | lo[7] << 16);
+}
+
+struct HeadArgsB {
+    const float* rows;
+    uint32_t N;
+    const uint4* phi;
+    const uint4* plo;
+    const float* b[5];
+    const float* ln_w;
+    const float* ln_b;
+    float* out;
+};
+
+#define MFMA_BF16(A, B, C) __builtin_amdgcn_mfma_f32_32x32x16_bf16((A), (B), (C), 0, 0, 0)
+
+// acc_c += A(act rows of this wave's row tile) . B(segment seg, tiles t0, t1)
+template <int SEG>
+__device__ __forceinline__ void kloop_bf3(const HeadArgsB& a, const uint16_t* Ah, const uint16_t* Al,
+                                          int t0, int t1, int lane, floatx16& acc0, floatx16& acc1) {
+    const int r = lane & 31, h = lane >> 5;
+    const uint4* ph0 = a.phi + ((size_t)t0 * kKbTotal + kbBase(SEG)) * 64 + lane;
+    const uint4* ph1 = a.phi + ((size_t)t1 * kKbTotal + kbBase(SEG)) * 64 + lane;
+    const uint4* pl0 = a.plo + ((size_t)t0 * kKbTotal + kbBase(SEG)) * 64 + lane;
+    const uint4* pl1 = a.plo + ((size_t)t1 * kKbTotal + kbBase(SEG)) * 64 + lane;
+    uint4 bh0 = ph0[0], bl0 = pl0[0], bh1 = ph1[0], bl1 = pl1[0];
+    for (int kb = 0; kb < kKbB[SEG]; ++kb) {
+        uint4 nh0 = bh0, nl0 = bl0, nh1 = bh1, nl1 = bl1;
+        if (kb + 1 < kKbB[SEG]) {           // prefetch the next k-block's B fragments (L2)
+            nh0 = ph0[(kb + 1) * 64];
+            nl0 = pl0[(kb + 1) * 64];
+            nh1 = ph1[(kb + 1) * 64];
+            nl1 = pl1[(kb + 1) * 64];
+        }
+        const int kk = kb * 16 + 8 * h;
+        const bf16x8 ah = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Ah + r * kRowB + kk));
+        const bf16x8 al = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Al + r * kRowB + kk));
+        const bf16x8 b0h = __builtin_bit_cast(bf16x8, bh0), b0l = __builtin_bit_cast(bf16x8, bl0);
+        const bf16x8 b1h = __builtin_bit_cast(bf16x8, bh1), b1l = __builtin_bit_cast(bf16x8, bl1);
+        acc0 = MFMA_BF16(al, b0h, acc0);
+        acc1 = MFMA_BF16(al, b1h, acc1);
+        acc0 = MFMA_BF16(ah, b0l, acc0);
+        acc1 = MFMA_BF16(ah, b1l, acc1);
+        acc0 = MFMA_BF16(ah, b0h, acc0);
+        acc1 = MFMA_BF16(ah, b1h, acc1);
+        bh0 = nh0; bl0 = nl0; bh1 = nh1; bl1 = nl1;
+    }
+}
+
+// bias + activation, written back in place as bf16 hi/lo planes (or fp32 for
+// the LayerNorm), after every wave has finished reading the planes.
+template <bool LAST>
+__device__ __forceinline__ void epilogue_bf3(const float* __restrict__ bias, uint16_t* Ah, uint16_t* Al,
+                                             float* F, int t0, int t1, int lane,
+                                             const floatx16& acc0, const floatx16& acc1) {
+    const int r = lane & 31, h = lane >> 5;
+    const float bc0 = bias[t0 * 32 + r], bc1 = bias[t1 * 32 + r];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+        float v0 = acc0[i] + bc0, v1 = acc1[i] + bc1;
+        if constexpr (!LAST) {
+            v0 = leaky(v0);
+            v1 = leaky(v1);
+            uint32_t hi, lo;
+            split_bf16(v0, hi, lo);
+            Ah[row * kRowB + t0 * 32 + r] = (uint16_t)hi;
+            Al[row * kRowB + t0 * 32 + r] = (uint16_t)lo;
+            split_bf16(v1, hi, lo);
+            Ah[row * kRowB + t1 * 32 + r] = (uint16_t)hi;
+            Al[row * kRowB + t1 * 32 + r] = (uint16_t)lo;
+        } else {
+            F[row * kHStride + t0 * 32 + r] = v0;
+            F[row * kHStride + t1 * 32 + r] = v1;
+        }
+    }
+}
+
+// One workgroup = 64 rays, 8 waves: wave (row tile rt, column group cg) owns
+// rows 32rt.. and the two 32-column tiles 2cg, 2cg+1 of every layer, so each
+// weight fragment is fetched by 2 waves per 64 rays.  The skip layer's input
+// half W2[:, 256:] . x is accumulated during layer 0 (while x is resident),
+// so the activations need one in-place buffer.
+__global__ void __launch_bounds__(kThreadsB) k_sam_head_bf3(HeadArgsB a) {
+    __shared__ __attribute__((aligned(16))) uint16_t lds[2 * kRowsB * kRowB];
+    uint16_t* Ph = lds;                       // bf16 hi plane [64][kRowB]
+    uint16_t* Pl = lds + kRowsB * kRowB;      // bf16 lo plane
+    float* F = reinterpret_cast<float*>(lds); // fp32 pre-LayerNorm tile [64][257] (aliases the planes)
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int rt = wave >> 2, cg = wave & 3;
+    const int t0 = 2 * cg, t1 = 2 * cg + 1;
+    const uint32_t ray0 = blockIdx.x * kRowsB;
+    for (int i = tid; i < kRowsB * kXkB; i += kThreadsB) {
+        const int rr = i / kXkB, c = i % kXkB;
+        const uint32_t ray = ray0 + rr;
+        float v = 0.0f;
+        if (ray < a.N && c < kIn) v = a.rows[(size_t)ray * kRowIn + c];
+        uint32_t hi, lo;
+        split_bf16(v, hi, lo);
+        Ph[rr * kRowB + c] = (uint16_t)hi;
+        Pl[rr * kRowB + c] = (uint16_t)lo;
+    }
+    __syncthreads();
+    uint16_t* Ah = Ph + rt * 32 * kRowB;      // this wave's 32 rows
+    uint16_t* Al = Pl + rt * 32 * kRowB;
+    float* Fw = F + rt * 32 * kHStride;
+
+    floatx16 acc0 = {}, acc1 = {}, skip0 = {}, skip1 = {};
+    kloop_bf3<0>(a, Ah, Al, t0, t1, lane, acc0, acc1);       // layer 0: W0 . x
+    kloop_bf3<5>(a, Ah, Al, t0, t1, lane, skip0, skip1);     // layer 2's W2[:, 256:] . x
+    __syncthreads();
+    epilogue_bf3<false>(a.b[0], Ah, Al, Fw, t0, t1, lane, acc0, acc1);
+    __syncthreads();
+    acc0 = {}; acc1 = {};
+    kloop_bf3<1>(a, Ah, Al, t0, t1, lane, acc0, acc1);       // layer 1
+    __syncthreads();
+    epilogue_bf3<false>(a.b[1], Ah, Al, Fw, t0, t1, lane, acc0, acc1);
+    __syncthreads();
+    kloop_bf3<2>(a, Ah, Al, t0, t1, lane, skip0, skip1);     // layer 2: + W2[:, :256] . h
+    __syncthreads();
+    epilogue_bf3<false>(a.b[2], Ah, Al, Fw, t0, t1, lane, skip0, skip1);
+    __syncthreads();
+    acc0 = {}; acc1 = {};
+    kloop_bf3<3>(a, Ah, Al, t0, t1, lane, acc0, acc1);       // layer 3
+    __syncthreads();
+    epilogue_bf3<false>(a.b[3], Ah, Al, Fw, t0, t1, lane, acc0, acc1);
+    __syncthreads();
+    acc0 = {}; acc1 = {};
+    kloop_bf3<4>(a, Ah, Al, t0, t1, lane, acc0, acc1);       // layer 4 (no activation)
+    __syncthreads();
+    epilogue_bf3<true>(a.b[4], Ah, Al, Fw, t0, t1, lane, acc0, acc1);
+    __syncthreads();
+
+    // LayerNorm(256, eps=1e-5): 8 threads per row, 32 columns each
+    const int row = tid >> 3, q = tid & 7;
+    const float* hr = F + row * kHStride + q * 32;
+    double s = 0.0;
+    for (int c = 0; c < 32; ++c) s += (double)hr[c];
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) s += __shfl_xor(s, m, 8);
+    const double mean = s / 256.0;
+    double v = 0.0;
+    for (int c = 0; c < 32; ++c) {
+        const double dlt = (double)hr[c] - mean;
+        v += dlt * dlt;
+    }
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) v += __shfl_xor(v, m, 8);
+    const float rstd = (float)(1.0 / sqrt(v / 256.0 + 1e-5));
+    const float mf = (float)mean;
+    const uint32_t ray = ray0 + row;
+    if (ray < a.N) {
+        float* o = a.out + (size_t)ray * 256 + q * 32;
+        for (int c = 0; c < 32; c += 4) {
+            float4 y;
+            y.x = ((hr[c + 0] - mf) * rstd) * a.ln_w[q * 32 + c + 0] + a.ln_b[q * 32 + c + 0];
+            y.y = ((hr[c + 1] - mf) * rstd) * a.ln_w[q * 32 + c + 1] + a.ln_b[q * 32 + c + 1];
+            y.z = ((hr[c + 2] - mf) * rstd) * a.ln_w[q * 32 + c + 2] + a.ln_b[q * 32 + c + 2];
+            y.w = ((hr[c + 3] - mf) * rstd) * a.ln_w[q * 32 + c + 3] + a.ln_b[q * 32 + c + 3];
+            *reinterpret_cast<float4*>(o + c) = y;
+        }
+    }
+}
+
 }  // namespace
 
-size_t sam_head_packed_floats() { return (size_t)8 * kTotalGroups * 64 * 4; }
+size_t sam_head_packed_floats() {
+    const size_t f32 = (size_t)8 * kTotalGroups * 64 * 4;
+    const size_t bf3 = (size_t)2 * 8 * kKbTotal * 64 * 4;      // hi + lo uint4 planes
+    return f32 > bf3 ? f32 : bf3;
+}
 
 int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, float* samvit,
                      float* packed, hipStream_t s) {
+    if (m->head_mode == 0) {                                     // bf16x3 (default)
+        const uint32_t nvec = 8u * kKbTotal * 64u;
+        uint4* phi = reinterpret_cast<uint4*>(packed);
+        uint4* plo = phi + nvec;
+        k_pack_bf3<<<div_up(nvec, 256), 256, 0, s>>>(m->sam_w[0], m->sam_w[1], m->sam_w[2],
+                                                     m->sam_w[3], m->sam_w[4], phi, plo);
+        HeadArgsB a;
+        a.rows = rows;
+        a.N = N;
+        a.phi = phi;
+        a.plo = plo;
+        for (int i = 0; i < 5; ++i) a.b[i] = m->sam_b[i];
+        a.ln_w = m->ln_w;
+        a.ln_b = m->ln_b;
+        a.out = samvit;
+        k_sam_head_bf3<<<div_up(N, kRowsB), kThreadsB, 0, s>>>(a);
+        return check_launch("sam_head_bf3");
+    }
     const uint32_t nvec = 8u * kTotalGroups * 64u;
     k_pack<<<div_up(nvec, 256), 256, 0, s>>>(m->sam_w[0], m->sam_w[1], m->sam_w[2], m->sam_w[3],
                                              m->sam_w[4], packed);

@@ -2,11 +2,15 @@
 
 Every ray does identical work (fixed 128/64/32 samples), so a
 view is split into contiguous row bands of equal size -- perfectly balanced
-with no data-path communication -- and the only exchange is one all-gather of
-the packed per-ray output tile [rays_per_rank, 3 + 1 + 1 (+ 256)] fp32 so every
-rank ends with the whole image/feature map.  With the `nccl`
+with no data-path communication -- and the only exchange is the all-gather
+of the packed per-ray outputs [rays, 3 + 1 + 1 (+ 256)] fp32 so every rank
+ends with the whole image / feature map.  With the `nccl`
 backend (RCCL on ROCm) this is ncclAllGather over xGMI; `gloo` is used by the
 CPU tests.
+
+`render_view_sharded` pipelines the band in chunks: the all-gather of chunk
+i is issued asynchronously (RCCL runs on its own stream after the chunk's
+kernels) while chunk i+1 renders, so communication hides behind compute.
 """
 import torch
 import torch.distributed as dist
@@ -21,11 +25,7 @@ def shard_range(n, rank, world):
 
 
 def pack_outputs(out, keys):
-    cols = []
-    for k in keys:
-        v = out[k]
-        cols.append(v.reshape(v.shape[0], -1).float())
-    return torch.cat(cols, dim=1)
+    return torch.cat([out[k].reshape(out[k].shape[0], -1).float() for k in keys], dim=1)
 
 
 def unpack_outputs(tile, keys, widths):
@@ -37,6 +37,15 @@ def unpack_outputs(tile, keys, widths):
     return res
 
 
+def _all_gather(buf_out, local, group, async_op=False):
+    """all_gather of equal-size row blocks into buf_out [world * n, C]."""
+    if dist.get_backend(group) == "nccl":
+        return dist.all_gather_into_tensor(buf_out, local, group=group, async_op=async_op)
+    world = dist.get_world_size(group)
+    parts = list(buf_out.chunk(world, 0))
+    return dist.all_gather(parts, local, group=group, async_op=async_op)
+
+
 def all_gather_rows(local, n_total, group=None):
     """Gather per-rank row blocks (possibly ragged by one row) into [n_total, C]."""
     world = dist.get_world_size(group)
@@ -45,21 +54,17 @@ def all_gather_rows(local, n_total, group=None):
     cap = max(b - a for a, b in sizes)
     padded = local.new_zeros(cap, C)
     padded[:local.shape[0]] = local
-    if dist.get_backend(group) == "nccl":
-        buf = local.new_empty(world * cap, C)
-        dist.all_gather_into_tensor(buf, padded, group=group)
-        parts = buf.view(world, cap, C)
-    else:
-        parts = [torch.empty_like(padded) for _ in range(world)]
-        dist.all_gather(parts, padded, group=group)
+    buf = local.new_empty(world * cap, C)
+    _all_gather(buf, padded, group)
+    parts = buf.view(world, cap, C)
     return torch.cat([parts[r][:b - a] for r, (a, b) in enumerate(sizes)], dim=0)
 
 
 def render_sharded(render_fn, rays_o, rays_d, keys=("image", "depth", "weights_sum", "samvit"),
                    group=None, gather=True):
-    """Render this rank's band of rays with `render_fn(rays_o, rays_d) -> dict`
-    and (optionally) all-gather the packed outputs.  rays_* are the full [N,3]
-    view on every rank (or only the local band if `gather` knows N)."""
+    """Render this rank's contiguous block of the given rays with
+    `render_fn(rays_o, rays_d) -> dict` and (optionally) all-gather the packed
+    outputs back into the original ray order."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     N = rays_o.shape[0]
     a, b = shard_range(N, rank, world)
@@ -69,4 +74,45 @@ def render_sharded(render_fn, rays_o, rays_d, keys=("image", "depth", "weights_s
     if not gather:
         return out
     full = all_gather_rows(pack_outputs(out, keys), N, group)
+    return unpack_outputs(full, keys, widths)
+
+
+def render_view_sharded(render_fn, ray_fn, H, W, keys=("image", "depth", "weights_sum", "samvit"),
+                        chunks=4, group=None):
+    """Strong-scaled render of one HxW view over the ranks of `group`.
+
+    ray_fn(row0, rows) -> (rays_o, rays_d) for pixel rows [row0, row0+rows);
+    render_fn(rays_o, rays_d) -> dict of per-ray outputs.  Each rank takes the
+    row band `shard_range(H, rank, world)` (H must split evenly so every
+    all-gather has equal blocks), renders it in `chunks` row chunks and
+    all-gathers each chunk asynchronously behind the next chunk's rendering.
+    Returns the full view's outputs in image order on every rank."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    if H % world:
+        raise ValueError(f"H={H} must be divisible by the world size {world}")
+    band = H // world
+    chunks = max(1, min(chunks, band))
+    while band % chunks:
+        chunks -= 1
+    crow = band // chunks
+    r0 = rank * band
+    pending, bufs = [], []
+    widths = None
+    for c in range(chunks):
+        ro, rd = ray_fn(r0 + c * crow, crow)
+        out = render_fn(ro, rd)
+        ks = [k for k in keys if k in out]
+        if widths is None:
+            keys = ks
+            widths = [out[k].reshape(out[k].shape[0], -1).shape[1] for k in keys]
+        tile = pack_outputs(out, keys)
+        buf = tile.new_empty(world * tile.shape[0], tile.shape[1])
+        pending.append(_all_gather(buf, tile, group, async_op=True))
+        bufs.append(buf)
+    for p in pending:
+        p.wait()
+    n_c = crow * W
+    C = bufs[0].shape[1]
+    # bufs[c] = [world, n_c, C] (rank-major); image order is (rank, chunk, ray)
+    full = torch.stack([b.view(world, n_c, C) for b in bufs], dim=1).reshape(world * chunks * n_c, C)
     return unpack_outputs(full, keys, widths)

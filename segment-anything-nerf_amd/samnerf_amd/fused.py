@@ -25,10 +25,14 @@ def _param(t, name):
 
 
 class FusedRenderer:
-    def __init__(self, net):
+    """head_mode: 0 = bf16x3 split-precision SAM head (default), 1 = exact fp32."""
+
+    def __init__(self, net, head_mode=None):
+        import os
         self.net = net
         self._ws = None
         self._keep = []
+        self.head_mode = int(os.environ.get("SAMNERF_HEAD_MODE", "0")) if head_mode is None else head_mode
 
     # --------------------------------------------------------------- model --
     def _grid(self, enc, name):
@@ -73,6 +77,7 @@ class FusedRenderer:
         m.min_near = float(opt.min_near)
         for i, v in enumerate(opt.num_steps):
             m.num_steps[i] = int(v)
+        m.head_mode = int(self.head_mode)
         return m
 
     def workspace(self, m, N, device):

@@ -23,13 +23,24 @@ def _worker(rank, world, port, n, q):
         import sys
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                         "segment-anything-nerf_amd"))
-        from samnerf_amd.dist import render_sharded
+        from samnerf_amd.dist import render_sharded, render_view_sharded
         g = torch.Generator().manual_seed(0)
         o = torch.randn(n, 3, generator=g)
         d = torch.randn(n, 3, generator=g)
         out = render_sharded(_fake_render, o, d)
         ref = _fake_render(o, d)
         ok = all(torch.equal(out[k], ref[k]) for k in ref)
+        # the pipelined per-view path: rows x W rays, chunked async all-gather
+        H, W = 16, n // 16
+        calls = []
+
+        def ray_fn(row0, rows):
+            calls.append((row0, rows))
+            return o[row0 * W:(row0 + rows) * W], d[row0 * W:(row0 + rows) * W]
+
+        view = render_view_sharded(_fake_render, ray_fn, H, W, chunks=4)
+        ok = ok and all(torch.equal(view[k], ref[k][:H * W]) for k in ref)
+        ok = ok and len(calls) == 4 and all(r == 2 for _, r in calls)
         q.put((rank, ok, {k: tuple(v.shape) for k, v in out.items()}))
     finally:
         dist.destroy_process_group()

@@ -14,6 +14,10 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
 timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -rA > "$OUT/pytest_gpu.log" 2>&1; rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error" "$OUT/pytest_gpu.log" | tail -15; stop_if_fatal $rc pytest
 fi
 timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1; rc=$?; echo "bench rc=$rc"; tail -2 "$OUT/bench.log"; stop_if_fatal $rc bench
+# per-rank loads of an N-GPU strong-scaled 512x512 view: H = 512/N rows
+for h in ${SWEEP_H:-}; do
+timeout -k 10 200 python bench.py --H $h --cpu-rays 0 --steps 20 > "$OUT/bench_h$h.log" 2>&1; rc=$?; echo "bench H=$h rc=$rc"; tail -1 "$OUT/bench_h$h.log" | python -c "import json,sys; r=json.loads(sys.stdin.read()); print(r['value'], r['ms_per_step'], {k: round(v,3) for k,v in r['stage_ms'].items()})"; stop_if_fatal $rc bench_h$h
+done
 if [ "${SKIP_PROF:-0}" != "1" ]; then
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_trace" -o trace -- python "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --cpu-rays 0 > "$OUT/prof_trace.log" 2>&1; rc=$?; echo "prof trace rc=$rc"; stop_if_fatal $rc prof_trace
