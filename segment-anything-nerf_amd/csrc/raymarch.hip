@@ -5,17 +5,20 @@
 // Fused pipeline for N rays (all intermediates stay in one workspace; nothing
 // of shape [N, T, C] is ever materialised, unlike the reference's ~350 ATen
 // ops per chunk):
-//   k_prop<128, 65, true>   near/far + uniform bins + prop0 grid/MLP +
-//                           compositing + inverse-CDF resampling -> 65 bins
-//   k_prop<64, 33, false>   same for prop1 -> 33 bins
+//   k_prop_sigma<128>       one thread per (ray, sample): near/far + uniform
+//                           bins + prop0 grid/MLP -> ds = delta * sigma
+//   k_prop_pdf<128, 65>     one thread per ray: compositing (double cumsum) +
+//                           torch-ordered normaliser + inverse-CDF -> 65 bins
+//   k_prop_sigma/pdf<64,33> the same for prop1 -> 33 bins
 //   k_final<32>             final samples: hash grid L16C2 + sigma/geo MLP +
 //                           SH(4) + compositing + view MLP -> image, depth,
 //                           weights_sum, head-input row; keeps (u_k, w_k)
 //   k_sgrid<32>             s_grid L16C8 gather, weighted by w_k -> f_sam
 //   sam_head (sam_head.hip) SkipConnMLP(163->256 x5) + LayerNorm on MFMA
 // Rays are independent and every ray does the same work (fixed 128/64/32
-// samples), so one thread per ray (64 neighbouring pixels per
-// wave -> coherent gathers) needs no compaction and no load balancing.
+// samples), so no compaction or load balancing is needed; the
+// proposal gathers run one thread per sample (enough waves to hide gather
+// latency even at the 32K rays of one rank of an 8-GPU view).
 #include <algorithm>
 #include <type_traits>
 
@@ -93,13 +96,29 @@ struct PropArgs {
     Lin u;                 // sample_pdf positions for the next stage
     const float* bins_in;  // [T+1][N] (stages > 0)
     float* snf;            // [2][N] spacing(near), spacing(far)
-    float* wtmp;           // [T][N]
+    float* wtmp;           // [T][N]: ds per sample
     float* bins_out;       // [TN][N]
 };
 
-template <int T, int TN, bool FIRST>
-__global__ void __launch_bounds__(256) k_prop(PropArgs a) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+// Proposal stage, part 1: one thread per (ray, sample).  A wave is 64
+// neighbouring rays at one sample index (their corner gathers share cache
+// lines) and a block is 4 consecutive sample indices of those rays.  Blocks
+// are ordered so that all T/4 sample groups of a ray group are dispatched to
+// the same XCD (block b runs on XCD b % 8) and share its L2.  Writes ds_k =
+// (real_bin_{k+1} - real_bin_k) * trunc_exp(density) (renderer.py:282-300)
+// to wtmp[k][r]; the serial part of compositing is in k_prop_pdf.
+template <int T>
+constexpr uint32_t prop_sigma_blocks(uint32_t N) {
+    return ((N + 511u) / 512u) * 8u * (T / 4);
+}
+
+template <int T, bool FIRST>
+__global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
+    static_assert(T % 4 == 0, "T must be a multiple of 4");
+    constexpr uint32_t Q = T / 4;
+    const uint32_t b = blockIdx.x;
+    const uint32_t q = (b >> 3) % Q, g = ((b >> 3) / Q) * 8u + (b & 7u);
+    const uint32_t r = g * 64u + (threadIdx.x & 63u), k = q * 4u + (threadIdx.x >> 6);
     if (r >= a.N) return;
     const uint32_t N = a.N;
     float o[3], d[3];
@@ -108,7 +127,7 @@ __global__ void __launch_bounds__(256) k_prop(PropArgs a) {
         o[c] = a.rays_o[(size_t)r * 3 + c];
         d[c] = a.rays_d[(size_t)r * 3 + c];
     }
-    float sn, sf;
+    float sn, sf, b0, b1;
     if constexpr (FIRST) {
         float near, far;
         near_far_aabb(o, d, a.aabb, a.min_near, near, far);
@@ -120,39 +139,58 @@ __global__ void __launch_bounds__(256) k_prop(PropArgs a) {
         }
         sn = spacing(near);
         sf = spacing(far);
-        a.snf[r] = sn;
-        a.snf[N + r] = sf;
+        if (k == 0) {
+            a.snf[r] = sn;
+            a.snf[N + r] = sf;
+        }
+        b0 = a.bins0(k);
+        b1 = a.bins0(k + 1);
     } else {
         sn = a.snf[r];
         sf = a.snf[N + r];
+        b0 = a.bins_in[(size_t)k * N + r];
+        b1 = a.bins_in[(size_t)(k + 1) * N + r];
     }
+    const float b2 = 2.0f * a.bound;
+    const float rb_prev = real_bin(sn, sf, b0), rb_next = real_bin(sn, sf, b1);
+    const float t = (rb_next + rb_prev) / 2.0f;
+    float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
+    contract3(x, y, z);
+    float feat[10];
+    grid_features<5, 2>(a.grid, (x + a.bound) / b2, (y + a.bound) / b2, (z + a.bound) / b2, feat);
+    float h[16], sv;
+    dense<16, 10, true>(a.W0, feat, h);
+    dense<1, 16, false>(a.W1, h, &sv);
+    a.wtmp[(size_t)k * N + r] = (rb_next - rb_prev) * expf(sv);          // trunc_exp forward
+}
+
+// Proposal stage, part 2: one thread per ray, in the reference's sequential
+// order -- composite weights with the double cumulative sum (renderer.py:
+// 300-307), the torch-ordered pdf normaliser and the sample_pdf merge walk
+// (renderer.py:84-119) -> TN new bins, sample-major [TN][N].
+template <int T, int TN, bool FIRST>
+__global__ void __launch_bounds__(64) k_prop_pdf(PropArgs a) {
+    // one wave = 64 rays; their ds rows are staged through LDS with coalesced
+    // loads from the sample-major wtmp (odd row stride: lane r at column k
+    // hits bank (r + k) % 64)
+    constexpr int SW = T + 1;
+    __shared__ float sw[64 * SW];
+    const uint32_t lane = threadIdx.x, r0 = blockIdx.x * 64u;
+    const uint32_t nr = min(64u, a.N - r0);
+    if (lane < nr)
+        for (int k = 0; k < T; ++k) sw[lane * SW + k] = a.wtmp[(size_t)k * a.N + r0 + lane];
+    if (lane >= nr) return;
+    const uint32_t r = r0 + lane, N = a.N;
+    float* row = sw + lane * SW;
+    double cum = 0.0;
+    for (int k = 0; k < T; ++k) row[k] = composite_step(row[k], cum, k == T - 1);
     auto bin = [&](int i) -> float {
         if constexpr (FIRST) return a.bins0(i);
         else return a.bins_in[(size_t)i * N + r];
     };
-
-    const float b2 = 2.0f * a.bound;
-    float rb_prev = real_bin(sn, sf, bin(0));
-    double cum = 0.0;
-    for (int k = 0; k < T; ++k) {
-        const float rb_next = real_bin(sn, sf, bin(k + 1));
-        const float t = (rb_next + rb_prev) / 2.0f;
-        float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
-        contract3(x, y, z);
-        float feat[10];
-        grid_features<5, 2>(a.grid, (x + a.bound) / b2, (y + a.bound) / b2, (z + a.bound) / b2,
-                            feat);
-        float h[16], s;
-        dense<16, 10, true>(a.W0, feat, h);
-        dense<1, 16, false>(a.W1, h, &s);
-        const float sigma = expf(s);                       // trunc_exp forward
-        const float w = composite_step((rb_next - rb_prev) * sigma, cum, k == T - 1);
-        a.wtmp[(size_t)k * N + r] = w;
-        rb_prev = rb_next;
-    }
-    const float wsum = torch_row_sum(T, [&](int i) { return a.wtmp[(size_t)i * N + r] + 0.01f; });
+    const float wsum = torch_row_sum(T, [&](int i) { return row[i] + 0.01f; });
     sample_pdf_walk(
-        T, TN, a.u, wsum, [&](int i) { return a.wtmp[(size_t)i * N + r]; }, bin,
+        T, TN, a.u, wsum, [&](int i) { return row[i]; }, bin,
         [&](int j, float v, int) { a.bins_out[(size_t)j * N + r] = v; });
 }
 
@@ -774,7 +812,8 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.bins_in = nullptr;
     pa.bins_out = w.bins1;
     mark_stage(0, s);
-    k_prop<128, 65, true><<<nb, 256, 0, s>>>(pa);
+    k_prop_sigma<128, true><<<prop_sigma_blocks<128>(N), 256, 0, s>>>(pa);
+    k_prop_pdf<128, 65, true><<<div_up(N, 64), 64, 0, s>>>(pa);
 
     // stage 1: 64 samples -> 33 bins
     pa.grid = gp1;
@@ -784,7 +823,8 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.bins_in = w.bins1;
     pa.bins_out = w.bins2;
     mark_stage(1, s);
-    k_prop<64, 33, false><<<nb, 256, 0, s>>>(pa);
+    k_prop_sigma<64, false><<<prop_sigma_blocks<64>(N), 256, 0, s>>>(pa);
+    k_prop_pdf<64, 33, false><<<div_up(N, 64), 64, 0, s>>>(pa);
 
     // stage 2: 32 samples through the full network
     FinalArgs fa{};

@@ -217,8 +217,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kXkB = 176;                 // head input padded to 11 k-blocks of 16
 constexpr int kRowB = 264;                // LDS row stride in bf16 (528 B = 16 mod 256: conflict-free b128 reads)
-constexpr int kRowsB = 64;                // rays per workgroup (2 row tiles x 4 column groups = 8 waves)
-constexpr int kThreadsB = 512;
+constexpr int kThreadsB = 512;            // 8 waves = the 8 output column tiles
 // k-block segments: 0 = W0 (x, 11), 1 = W1 (16), 2 = W2[:, :256] (h, 16),
 // 3 = W3 (16), 4 = W4 (16), 5 = W2[:, 256:] (x part of the skip layer, 11)
 constexpr int kKbB[6] = {11, 16, 16, 16, 16, 11};
@@ -281,83 +280,86 @@ struct HeadArgsB {
 
 #define MFMA_BF16(A, B, C) __builtin_amdgcn_mfma_f32_32x32x16_bf16((A), (B), (C), 0, 0, 0)
 
-// acc_c += A(act rows of this wave's row tile) . B(segment seg, tiles t0, t1)
-template <int SEG>
-__device__ __forceinline__ void kloop_bf3(const HeadArgsB& a, const uint16_t* Ah, const uint16_t* Al,
-                                          int t0, int t1, int lane, floatx16& acc0, floatx16& acc1) {
+// One workgroup = RT row tiles of 32 rays, 8 waves; wave ct owns output
+// columns 32ct..32ct+31 of every layer for ALL the block's rows, so each
+// weight fragment it streams from L2 feeds 3 x RT MFMAs (the head is bound by
+// that stream: ~11 KB of fragments per ray at RT = 4).  The skip layer's input
+// half W2[:, 256:] . x is accumulated during layer 0 (while x is resident), so
+// the activations need one in-place hi/lo buffer.
+template <int SEG, int RT>
+__device__ __forceinline__ void kloop_bf3(const HeadArgsB& a, const uint16_t* Ph, const uint16_t* Pl,
+                                          int ct, int lane, floatx16 (&acc)[RT]) {
     const int r = lane & 31, h = lane >> 5;
-    const uint4* ph0 = a.phi + ((size_t)t0 * kKbTotal + kbBase(SEG)) * 64 + lane;
-    const uint4* ph1 = a.phi + ((size_t)t1 * kKbTotal + kbBase(SEG)) * 64 + lane;
-    const uint4* pl0 = a.plo + ((size_t)t0 * kKbTotal + kbBase(SEG)) * 64 + lane;
-    const uint4* pl1 = a.plo + ((size_t)t1 * kKbTotal + kbBase(SEG)) * 64 + lane;
-    uint4 bh0 = ph0[0], bl0 = pl0[0], bh1 = ph1[0], bl1 = pl1[0];
+    const uint4* ph = a.phi + ((size_t)ct * kKbTotal + kbBase(SEG)) * 64 + lane;
+    const uint4* pl = a.plo + ((size_t)ct * kKbTotal + kbBase(SEG)) * 64 + lane;
+    uint4 bh = ph[0], bl = pl[0];
+#pragma unroll 1
     for (int kb = 0; kb < kKbB[SEG]; ++kb) {
-        uint4 nh0 = bh0, nl0 = bl0, nh1 = bh1, nl1 = bl1;
+        uint4 nh = bh, nl = bl;
         if (kb + 1 < kKbB[SEG]) {           // prefetch the next k-block's B fragments (L2)
-            nh0 = ph0[(kb + 1) * 64];
-            nl0 = pl0[(kb + 1) * 64];
-            nh1 = ph1[(kb + 1) * 64];
-            nl1 = pl1[(kb + 1) * 64];
+            nh = ph[(kb + 1) * 64];
+            nl = pl[(kb + 1) * 64];
         }
         const int kk = kb * 16 + 8 * h;
-        const bf16x8 ah = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Ah + r * kRowB + kk));
-        const bf16x8 al = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Al + r * kRowB + kk));
-        const bf16x8 b0h = __builtin_bit_cast(bf16x8, bh0), b0l = __builtin_bit_cast(bf16x8, bl0);
-        const bf16x8 b1h = __builtin_bit_cast(bf16x8, bh1), b1l = __builtin_bit_cast(bf16x8, bl1);
-        acc0 = MFMA_BF16(al, b0h, acc0);
-        acc1 = MFMA_BF16(al, b1h, acc1);
-        acc0 = MFMA_BF16(ah, b0l, acc0);
-        acc1 = MFMA_BF16(ah, b1l, acc1);
-        acc0 = MFMA_BF16(ah, b0h, acc0);
-        acc1 = MFMA_BF16(ah, b1h, acc1);
-        bh0 = nh0; bl0 = nl0; bh1 = nh1; bl1 = nl1;
+        bf16x8 ah[RT], al[RT];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+            ah[t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Ph + (t * 32 + r) * kRowB + kk));
+            al[t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Pl + (t * 32 + r) * kRowB + kk));
+        }
+        const bf16x8 b_h = __builtin_bit_cast(bf16x8, bh), b_l = __builtin_bit_cast(bf16x8, bl);
+        // small terms first, RT independent accumulators between dependent MFMAs
+#pragma unroll
+        for (int t = 0; t < RT; ++t) acc[t] = MFMA_BF16(al[t], b_h, acc[t]);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) acc[t] = MFMA_BF16(ah[t], b_l, acc[t]);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) acc[t] = MFMA_BF16(ah[t], b_h, acc[t]);
+        bh = nh;
+        bl = nl;
     }
 }
 
 // bias + activation, written back in place as bf16 hi/lo planes (or fp32 for
 // the LayerNorm), after every wave has finished reading the planes.
-template <bool LAST>
-__device__ __forceinline__ void epilogue_bf3(const float* __restrict__ bias, uint16_t* Ah, uint16_t* Al,
-                                             float* F, int t0, int t1, int lane,
-                                             const floatx16& acc0, const floatx16& acc1) {
+template <bool LAST, int RT>
+__device__ __forceinline__ void epilogue_bf3(const float* __restrict__ bias, uint16_t* Ph, uint16_t* Pl,
+                                             float* F, int ct, int lane, const floatx16 (&acc)[RT]) {
     const int r = lane & 31, h = lane >> 5;
-    const float bc0 = bias[t0 * 32 + r], bc1 = bias[t1 * 32 + r];
+    const int col = ct * 32 + r;
+    const float bc = bias[col];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
-        float v0 = acc0[i] + bc0, v1 = acc1[i] + bc1;
-        if constexpr (!LAST) {
-            v0 = leaky(v0);
-            v1 = leaky(v1);
-            uint32_t hi, lo;
-            split_bf16(v0, hi, lo);
-            Ah[row * kRowB + t0 * 32 + r] = (uint16_t)hi;
-            Al[row * kRowB + t0 * 32 + r] = (uint16_t)lo;
-            split_bf16(v1, hi, lo);
-            Ah[row * kRowB + t1 * 32 + r] = (uint16_t)hi;
-            Al[row * kRowB + t1 * 32 + r] = (uint16_t)lo;
-        } else {
-            F[row * kHStride + t0 * 32 + r] = v0;
-            F[row * kHStride + t1 * 32 + r] = v1;
+    for (int t = 0; t < RT; ++t) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            const float v = acc[t][i] + bc;
+            if constexpr (!LAST) {
+                uint32_t hi, lo;
+                split_bf16(leaky(v), hi, lo);
+                Ph[row * kRowB + col] = (uint16_t)hi;
+                Pl[row * kRowB + col] = (uint16_t)lo;
+            } else {
+                F[row * kHStride + col] = v;
+            }
         }
     }
 }
 
-// One workgroup = 64 rays, 8 waves: wave (row tile rt, column group cg) owns
-// rows 32rt.. and the two 32-column tiles 2cg, 2cg+1 of every layer, so each
-// weight fragment is fetched by 2 waves per 64 rays.  The skip layer's input
-// half W2[:, 256:] . x is accumulated during layer 0 (while x is resident),
-// so the activations need one in-place buffer.
+template <int RT>
+constexpr size_t head_lds_bytes() { return (size_t)2 * RT * 32 * kRowB * sizeof(uint16_t); }
+
+template <int RT>
 __global__ void __launch_bounds__(kThreadsB) k_sam_head_bf3(HeadArgsB a) {
-    __shared__ __attribute__((aligned(16))) uint16_t lds[2 * kRowsB * kRowB];
-    uint16_t* Ph = lds;                       // bf16 hi plane [64][kRowB]
-    uint16_t* Pl = lds + kRowsB * kRowB;      // bf16 lo plane
-    float* F = reinterpret_cast<float*>(lds); // fp32 pre-LayerNorm tile [64][257] (aliases the planes)
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int rt = wave >> 2, cg = wave & 3;
-    const int t0 = 2 * cg, t1 = 2 * cg + 1;
-    const uint32_t ray0 = blockIdx.x * kRowsB;
-    for (int i = tid; i < kRowsB * kXkB; i += kThreadsB) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+    constexpr int kRows = RT * 32;
+    uint16_t* Ph = lds;                       // bf16 hi plane [kRows][kRowB]
+    uint16_t* Pl = lds + kRows * kRowB;       // bf16 lo plane
+    float* F = reinterpret_cast<float*>(lds); // fp32 pre-LayerNorm tile [kRows][257] (aliases the planes)
+    static_assert((size_t)kRows * kHStride * 4 <= head_lds_bytes<RT>(), "LN tile must fit the planes");
+    const int tid = threadIdx.x, ct = tid >> 6, lane = tid & 63;
+    const uint32_t ray0 = blockIdx.x * kRows;
+    for (int i = tid; i < kRows * kXkB; i += kThreadsB) {
         const int rr = i / kXkB, c = i % kXkB;
         const uint32_t ray = ray0 + rr;
         float v = 0.0f;
@@ -368,65 +370,84 @@ __global__ void __launch_bounds__(kThreadsB) k_sam_head_bf3(HeadArgsB a) {
         Pl[rr * kRowB + c] = (uint16_t)lo;
     }
     __syncthreads();
-    uint16_t* Ah = Ph + rt * 32 * kRowB;      // this wave's 32 rows
-    uint16_t* Al = Pl + rt * 32 * kRowB;
-    float* Fw = F + rt * 32 * kHStride;
 
-    floatx16 acc0 = {}, acc1 = {}, skip0 = {}, skip1 = {};
-    kloop_bf3<0>(a, Ah, Al, t0, t1, lane, acc0, acc1);       // layer 0: W0 . x
-    kloop_bf3<5>(a, Ah, Al, t0, t1, lane, skip0, skip1);     // layer 2's W2[:, 256:] . x
-    __syncthreads();
-    epilogue_bf3<false>(a.b[0], Ah, Al, Fw, t0, t1, lane, acc0, acc1);
-    __syncthreads();
-    acc0 = {}; acc1 = {};
-    kloop_bf3<1>(a, Ah, Al, t0, t1, lane, acc0, acc1);       // layer 1
-    __syncthreads();
-    epilogue_bf3<false>(a.b[1], Ah, Al, Fw, t0, t1, lane, acc0, acc1);
-    __syncthreads();
-    kloop_bf3<2>(a, Ah, Al, t0, t1, lane, skip0, skip1);     // layer 2: + W2[:, :256] . h
-    __syncthreads();
-    epilogue_bf3<false>(a.b[2], Ah, Al, Fw, t0, t1, lane, skip0, skip1);
-    __syncthreads();
-    acc0 = {}; acc1 = {};
-    kloop_bf3<3>(a, Ah, Al, t0, t1, lane, acc0, acc1);       // layer 3
-    __syncthreads();
-    epilogue_bf3<false>(a.b[3], Ah, Al, Fw, t0, t1, lane, acc0, acc1);
-    __syncthreads();
-    acc0 = {}; acc1 = {};
-    kloop_bf3<4>(a, Ah, Al, t0, t1, lane, acc0, acc1);       // layer 4 (no activation)
-    __syncthreads();
-    epilogue_bf3<true>(a.b[4], Ah, Al, Fw, t0, t1, lane, acc0, acc1);
-    __syncthreads();
-
-    // LayerNorm(256, eps=1e-5): 8 threads per row, 32 columns each
-    const int row = tid >> 3, q = tid & 7;
-    const float* hr = F + row * kHStride + q * 32;
-    double s = 0.0;
-    for (int c = 0; c < 32; ++c) s += (double)hr[c];
+    floatx16 acc[RT], skip[RT];
 #pragma unroll
-    for (int m = 1; m < 8; m <<= 1) s += __shfl_xor(s, m, 8);
+    for (int t = 0; t < RT; ++t) { acc[t] = floatx16{}; skip[t] = floatx16{}; }
+    kloop_bf3<0, RT>(a, Ph, Pl, ct, lane, acc);        // layer 0: W0 . x
+    kloop_bf3<5, RT>(a, Ph, Pl, ct, lane, skip);       // layer 2's W2[:, 256:] . x
+    __syncthreads();
+    epilogue_bf3<false, RT>(a.b[0], Ph, Pl, F, ct, lane, acc);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < RT; ++t) acc[t] = floatx16{};
+    kloop_bf3<1, RT>(a, Ph, Pl, ct, lane, acc);        // layer 1
+    __syncthreads();
+    epilogue_bf3<false, RT>(a.b[1], Ph, Pl, F, ct, lane, acc);
+    __syncthreads();
+    kloop_bf3<2, RT>(a, Ph, Pl, ct, lane, skip);       // layer 2: + W2[:, :256] . h
+    __syncthreads();
+    epilogue_bf3<false, RT>(a.b[2], Ph, Pl, F, ct, lane, skip);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < RT; ++t) acc[t] = floatx16{};
+    kloop_bf3<3, RT>(a, Ph, Pl, ct, lane, acc);        // layer 3
+    __syncthreads();
+    epilogue_bf3<false, RT>(a.b[3], Ph, Pl, F, ct, lane, acc);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < RT; ++t) acc[t] = floatx16{};
+    kloop_bf3<4, RT>(a, Ph, Pl, ct, lane, acc);        // layer 4 (no activation)
+    __syncthreads();
+    epilogue_bf3<true, RT>(a.b[4], Ph, Pl, F, ct, lane, acc);
+    __syncthreads();
+
+    // LayerNorm(256, eps=1e-5): TPR threads per row, in double
+    constexpr int TPR = kThreadsB / kRows, CPT = 256 / TPR;
+    const int row = tid / TPR, q = tid % TPR;
+    const float* hr = F + row * kHStride + q * CPT;
+    double s = 0.0;
+    for (int c = 0; c < CPT; ++c) s += (double)hr[c];
+#pragma unroll
+    for (int m = 1; m < TPR; m <<= 1) s += __shfl_xor(s, m, TPR);
     const double mean = s / 256.0;
     double v = 0.0;
-    for (int c = 0; c < 32; ++c) {
+    for (int c = 0; c < CPT; ++c) {
         const double dlt = (double)hr[c] - mean;
         v += dlt * dlt;
     }
 #pragma unroll
-    for (int m = 1; m < 8; m <<= 1) v += __shfl_xor(v, m, 8);
+    for (int m = 1; m < TPR; m <<= 1) v += __shfl_xor(v, m, TPR);
     const float rstd = (float)(1.0 / sqrt(v / 256.0 + 1e-5));
     const float mf = (float)mean;
     const uint32_t ray = ray0 + row;
     if (ray < a.N) {
-        float* o = a.out + (size_t)ray * 256 + q * 32;
-        for (int c = 0; c < 32; c += 4) {
+        float* o = a.out + (size_t)ray * 256 + q * CPT;
+        const float* lw = a.ln_w + q * CPT;
+        const float* lb = a.ln_b + q * CPT;
+        for (int c = 0; c < CPT; c += 4) {
             float4 y;
-            y.x = ((hr[c + 0] - mf) * rstd) * a.ln_w[q * 32 + c + 0] + a.ln_b[q * 32 + c + 0];
-            y.y = ((hr[c + 1] - mf) * rstd) * a.ln_w[q * 32 + c + 1] + a.ln_b[q * 32 + c + 1];
-            y.z = ((hr[c + 2] - mf) * rstd) * a.ln_w[q * 32 + c + 2] + a.ln_b[q * 32 + c + 2];
-            y.w = ((hr[c + 3] - mf) * rstd) * a.ln_w[q * 32 + c + 3] + a.ln_b[q * 32 + c + 3];
+            y.x = ((hr[c + 0] - mf) * rstd) * lw[c + 0] + lb[c + 0];
+            y.y = ((hr[c + 1] - mf) * rstd) * lw[c + 1] + lb[c + 1];
+            y.z = ((hr[c + 2] - mf) * rstd) * lw[c + 2] + lb[c + 2];
+            y.w = ((hr[c + 3] - mf) * rstd) * lw[c + 3] + lb[c + 3];
             *reinterpret_cast<float4*>(o + c) = y;
         }
     }
+}
+
+template <int RT>
+int launch_head_bf3(const HeadArgsB& a, hipStream_t s) {
+    static bool attr = false;                 // > 64 KB of dynamic LDS needs opting in once
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sam_head_bf3<RT>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)head_lds_bytes<RT>()) != hipSuccess)
+            return fail(SAMNERF_ELAUNCH, "sam_head: cannot reserve %zu B of LDS", head_lds_bytes<RT>());
+        attr = true;
+    }
+    k_sam_head_bf3<RT><<<div_up(a.N, RT * 32u), kThreadsB, head_lds_bytes<RT>(), s>>>(a);
+    return check_launch("sam_head_bf3");
 }
 
 }  // namespace
@@ -454,8 +475,8 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         a.ln_w = m->ln_w;
         a.ln_b = m->ln_b;
         a.out = samvit;
-        k_sam_head_bf3<<<div_up(N, kRowsB), kThreadsB, 0, s>>>(a);
-        return check_launch("sam_head_bf3");
+        // 128 rays per block when that still gives >= 2 blocks per CU, else 64
+        return N >= 128u * 512u ? launch_head_bf3<4>(a, s) : launch_head_bf3<2>(a, s);
     }
     const uint32_t nvec = 8u * kTotalGroups * 64u;
     k_pack<<<div_up(nvec, 256), 256, 0, s>>>(m->sam_w[0], m->sam_w[1], m->sam_w[2], m->sam_w[3],
