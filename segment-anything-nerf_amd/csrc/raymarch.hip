@@ -201,6 +201,7 @@ struct FinalArgs {
     uint32_t N;
     float bound, bg;
     const Tables* tab;
+    const float* grid_emb;  // == tab->grid.emb, as a kernel argument so gathers are global_load (not flat)
     const float* G0;   // grid_mlp [64,32]
     const float* G1;   // [64,64]
     const float* G2;   // [16,64]
@@ -230,39 +231,55 @@ __global__ void k_put_tables(Tables t, Tables* __restrict__ dst) {
     if (threadIdx.x == 0) *dst = t;
 }
 
-// ---- MFMA weight fragments (v_mfma_f32_32x32x2_f32, transposed orientation:
-// rows = hidden units, columns = 32 rays).  ρ(q) = (q&3) + 8(q>>2) is the row
-// that accumulator register q holds in the lower half-wave (+4 in the upper),
-// so a layer's accumulator is the next layer's B operand as it stands and the
-// weights (A operand) are stored permuted to match.
-constexpr int kW1 = 0;               // grid_mlp.0 [ob 2][level 16][lane]   W[64,32]
-constexpr int kW2 = 2048;            // grid_mlp.1 [ob 2][ob' 2][q 16][lane] W[64,64]
-constexpr int kW3 = 6144;            // grid_mlp.2 [ob' 2][q 16][lane]       W[16,64]
-constexpr int kV1 = 8192;            // view_mlp.0 [q 16][lane]  q<8: geo acc rows, q>=8: sh pairs
-constexpr int kV2 = 9216;            // view_mlp.1 [q 16][lane]              W[32,32]
-constexpr int kV3 = 10240;           // view_mlp.2 [q 16][lane]              W[3,32]
-constexpr int kWTotal = 11264;
+// ---- grid_mlp on bf16x3 MFMAs (v_mfma_f32_32x32x16_bf16, fp32 accumulate).
+// Transposed orientation: A = weights (rows = hidden units), B = activations
+// (columns = 32 rays), so a layer's accumulator is the next layer's B operand
+// as it stands.  Lane (j, h) of a 32x32 accumulator holds rows rho(q) + 4h,
+// rho(q) = (q&3) + 8(q>>2); k-block kb of a 64-wide input takes registers
+// 8(kb&1)..8(kb&1)+7 of tile kb>>1, and the weights are stored permuted to
+// match (hidden_unit).  Each product is split x = hi + lo (bf16 RNE) and
+// A.B ~= A_lo.B_hi + A_hi.B_lo + A_hi.B_hi: ~2^-16 relative error per product
+// against the 1e-3 output budget, at 3 MFMAs of 32 cycles per 16-deep k-block
+// instead of 8 fp32 MFMAs of 64.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+
+constexpr int kF1 = 0;               // grid_mlp.0: slot kb*2 + ob      (kb < 2)  W[64,32]
+constexpr int kF2 = 4;               // grid_mlp.1: slot 4 + kb*2 + ob  (kb < 4)  W[64,64]
+constexpr int kF3 = 12;              // grid_mlp.2: slot 12 + kb        (kb < 4)  W[16,64]
+constexpr int kFSlots = 16;          // x 64 lanes x (8 bf16 hi + 8 bf16 lo)
+// view_mlp on v_mfma_f32_32x32x2_f32 (once per ray): [q 16][lane] each
+constexpr int kV1 = 0;               // view_mlp.0  q<8: geo acc rows, q>=8: sh pairs
+constexpr int kV2 = 1024;            // view_mlp.1  W[32,32]
+constexpr int kV3 = 2048;            // view_mlp.2  W[3,32]
+constexpr int kVTotal = 3072;
 
 __device__ __forceinline__ int rho(int q) { return (q & 3) + 8 * (q >> 2); }
 
-__device__ float weight_fragment(const FinalArgs& a, int idx) {
+// input unit of a 64-wide layer fed by accumulator tiles (kb, half h, element m)
+__device__ __forceinline__ int hidden_unit(int kb, int h, int m) {
+    return (kb >> 1) * 32 + rho(8 * (kb & 1) + m) + 4 * h;
+}
+
+__device__ float grid_weight(const FinalArgs& a, int slot, int lane, int m) {
+    const int i = lane & 31, h = lane >> 5;
+    if (slot < kF2) {                          // input k = 2*level + channel = 16kb + 8h + m
+        const int kb = slot >> 1, ob = slot & 1;
+        return a.G0[(ob * 32 + i) * 32 + 16 * kb + 8 * h + m];
+    }
+    if (slot < kF3) {
+        const int t = slot - kF2, kb = t >> 1, ob = t & 1;
+        return a.G1[(ob * 32 + i) * 64 + hidden_unit(kb, h, m)];
+    }
+    const int kb = slot - kF3;
+    return i < 16 ? a.G2[i * 64 + hidden_unit(kb, h, m)] : 0.0f;
+}
+
+__device__ float view_weight(const FinalArgs& a, int idx) {
     const int lane = idx & 63, i = lane & 31, h = lane >> 5;
-    if (idx < kW2) {                           // k = 2*level + h
-        const int s = (idx >> 6) & 15, ob = idx >> 10;
-        return a.G0[(ob * 32 + i) * 32 + 2 * s + h];
-    }
-    if (idx < kW3) {
-        const int q = idx - kW2;
-        const int r = (q >> 6) & 15, obp = (q >> 10) & 1, ob = q >> 11;
-        return a.G1[(ob * 32 + i) * 64 + obp * 32 + rho(r) + 4 * h];
-    }
-    if (idx < kV1) {
-        const int q = idx - kW3;
-        const int r = (q >> 6) & 15, obp = q >> 10;
-        return i < 16 ? a.G2[i * 64 + obp * 32 + rho(r) + 4 * h] : 0.0f;
-    }
     if (idx < kV2) {                           // f_image = [geo (units 1..15), sh * wsum]
-        const int r = (idx - kV1) >> 6;
+        const int r = idx >> 6;
         if (r < 8) {
             const int unit = rho(r) + 4 * h;   // grid_mlp output row; unit 0 is sigma
             return unit >= 1 ? a.V0[i * 31 + unit - 1] : 0.0f;
@@ -277,19 +294,87 @@ __device__ float weight_fragment(const FinalArgs& a, int idx) {
     return i < 3 ? a.V2[i * 32 + rho(r) + 4 * h] : 0.0f;
 }
 
-#define MFMA32(A, B, C) __builtin_amdgcn_mfma_f32_32x32x2f32((A), (B), (C), 0, 0, 0)
+__device__ __forceinline__ void split_pair(float x, float y, uint32_t& hi, uint32_t& lo) {
+    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v){x, y}, bf16x2v));
+    const float hx = __uint_as_float(hi << 16), hy = __uint_as_float(hi & 0xffff0000u);
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v){x - hx, y - hy}, bf16x2v));
+}
 
-// One wave marches 32 rays.  Lane (h, j) owns ray j and feature channel h:
-// for level l it gathers channel h of the 8 corners of ray j -- which is
-// exactly the B operand of k-step l of the first layer -- so the hash-grid
-// gather feeds the matrix cores with no data movement.  grid_mlp
-// 32->64->64->16 and view_mlp 31->32->32->3 run as 32x32x2 f32 MFMAs
-// (exact fp32 fma chains); compositing runs in-lane (both half-waves hold
-// the same ray and compute the same weights).
+__device__ __forceinline__ void split8(const float* v, uint4& hi, uint4& lo) {
+    split_pair(v[0], v[1], hi.x, lo.x);
+    split_pair(v[2], v[3], hi.y, lo.y);
+    split_pair(v[4], v[5], hi.z, lo.z);
+    split_pair(v[6], v[7], hi.w, lo.w);
+}
+
+#define MFMA32(A, B, C) __builtin_amdgcn_mfma_f32_32x32x2f32((A), (B), (C), 0, 0, 0)
+#define MFMA_BF16(A, B, C) __builtin_amdgcn_mfma_f32_32x32x16_bf16((A), (B), (C), 0, 0, 0)
+
+__device__ __forceinline__ floatx16 mfma3(uint4 ah, uint4 al, uint4 bh, uint4 bl, floatx16 c) {
+    const bf16x8 Ah = __builtin_bit_cast(bf16x8, ah), Al = __builtin_bit_cast(bf16x8, al);
+    const bf16x8 Bh = __builtin_bit_cast(bf16x8, bh), Bl = __builtin_bit_cast(bf16x8, bl);
+    c = MFMA_BF16(Al, Bh, c);
+    c = MFMA_BF16(Ah, Bl, c);
+    return MFMA_BF16(Ah, Bh, c);
+}
+
+// Trilinear lookup of both channels of one L16C2 level whose descriptor
+// differs between the half-waves (lane-varying; no divergent branch): the
+// row of corner (x, y, z) is x + y*res + z*res^2 (dense) or
+// (x ^ y*P1 ^ z*P2) & (size-1) (hashed), built from per-axis terms.
+__device__ __forceinline__ void gather_level_c2(const float2* __restrict__ emb, const LevelDesc& d,
+                                                float ux, float uy, float uz, float& f0, float& f1) {
+    uint32_t cx, cy, cz;
+    float fx, fy, fz;
+    locate_axis(ux, d.res, cx, fx);
+    locate_axis(uy, d.res, cy, fy);
+    locate_axis(uz, d.res, cz, fz);
+    const uint32_t top = d.res - 1u;
+    const bool hashed = d.flags & kHashed;
+    const uint32_t my = hashed ? kPrime1 : d.res, mz = hashed ? kPrime2 : d.res * d.res;
+    const uint32_t mask = hashed ? d.size - 1u : 0xffffffffu;
+    const uint32_t X[2] = {cx, min(cx + 1u, top)};
+    const uint32_t Y[2] = {cy * my, min(cy + 1u, top) * my};
+    const uint32_t Z[2] = {cz * mz, min(cz + 1u, top) * mz};
+    const float2* base = emb + d.off;
+    f0 = 0.0f;
+    f1 = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const float wx = (c & 1) ? fx : 1.0f - fx;
+        const float wy = (c & 2) ? fy : 1.0f - fy;
+        const float wz = (c & 4) ? fz : 1.0f - fz;
+        const uint32_t xs = X[c & 1], ys = Y[(c >> 1) & 1], zs = Z[c >> 2];
+        const uint32_t row = hashed ? ((xs ^ ys ^ zs) & mask) : (xs + ys + zs);
+        const float w = (wx * wy) * wz;
+        const float2 e = base[row];
+        f0 = __builtin_fmaf(w, e.x, f0);
+        f1 = __builtin_fmaf(w, e.y, f1);
+    }
+}
+
+__device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const LevelDesc& q, bool hi) {
+    return LevelDesc{hi ? q.off : p.off, hi ? q.size : p.size, hi ? q.res : p.res, hi ? q.flags : p.flags};
+}
+
+// One wave marches 32 rays.  Lane (j, h) owns ray j; for k-block kb it
+// gathers both channels of levels 8kb + 4h .. 8kb + 4h + 3 -- exactly its B
+// operand of the first layer (input index 2*level + channel) -- so the hash
+// grid feeds the matrix cores with no data movement.  grid_mlp 32->64->64->16
+// runs on bf16x3 MFMAs, view_mlp 31->32->32->3 (once per ray) on fp32 MFMAs;
+// compositing runs in-lane (both half-waves hold the same ray and compute the
+// same weights).
 template <int T>
 __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
-    __shared__ float Wl[kWTotal];
-    for (int i = threadIdx.x; i < kWTotal; i += 256) Wl[i] = weight_fragment(a, i);
+    __shared__ uint4 Fh[kFSlots * 64], Fl[kFSlots * 64];
+    __shared__ float Vl[kVTotal];
+    for (int idx = threadIdx.x; idx < kFSlots * 64; idx += 256) {
+        float v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[m] = grid_weight(a, idx >> 6, idx & 63, m);
+        split8(v, Fh[idx], Fl[idx]);
+    }
+    for (int idx = threadIdx.x; idx < kVTotal; idx += 256) Vl[idx] = view_weight(a, idx);
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -302,7 +387,7 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
     const bool writer = live && hh == 0;
     const uint32_t N = a.N;
     const GridDesc<16>* __restrict__ G = &a.tab->grid;
-    const float* __restrict__ emb = a.tab->grid.emb;
+    const float2* __restrict__ emb = reinterpret_cast<const float2*>(a.grid_emb);
 
     float o[3], d[3];
 #pragma unroll
@@ -329,36 +414,27 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
             a.u_out[((size_t)k * 3 + 1) * N + r] = uy;
             a.u_out[((size_t)k * 3 + 2) * N + r] = uz;
         }
-        // weight fragments are re-read from LDS each sample (1 ds_read per
-        // 64-cycle MFMA) rather than hoisted into VGPRs for the whole loop
+        // weight fragments are re-read from LDS each sample rather than
+        // hoisted into VGPRs for the whole loop (opaque offset defeats LICM)
         int wo = lane;
         asm volatile("" : "+v"(wo));
-        const float* W = Wl + wo;
-        // gather + layer 1, level by level
+        const uint4* FH = Fh + wo;
+        const uint4* FL = Fl + wo;
+
         floatx16 h1a = {}, h1b = {};
-#pragma unroll 2
-        for (int l = 0; l < 16; ++l) {
-            const LevelDesc dl = G->lv[l];
-            uint32_t cx, cy, cz;
-            float fx, fy, fz;
-            locate_axis(ux, dl.res, cx, fx);
-            locate_axis(uy, dl.res, cy, fy);
-            locate_axis(uz, dl.res, cz, fz);
-            const uint32_t top = dl.res - 1u;
-            const uint32_t nx = min(cx + 1u, top), ny = min(cy + 1u, top), nz = min(cz + 1u, top);
-            const float* base = emb + dl.off * 2u + (uint32_t)hh;
-            float f = 0.0f;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const float wx = (c & 1) ? fx : 1.0f - fx;
-                const float wy = (c & 2) ? fy : 1.0f - fy;
-                const float wz = (c & 4) ? fz : 1.0f - fz;
-                const uint32_t row = dense_or_hash_row((c & 1) ? nx : cx, (c & 2) ? ny : cy,
-                                                       (c & 4) ? nz : cz, dl);
-                f = __builtin_fmaf((wx * wy) * wz, base[row * 2u], f);
+        for (int kb = 0; kb < 2; ++kb) {
+            float f[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const LevelDesc dl = select_level(G->lv[8 * kb + i], G->lv[8 * kb + 4 + i], hh != 0);
+                gather_level_c2(emb, dl, ux, uy, uz, f[2 * i], f[2 * i + 1]);
+                if (i & 1) __builtin_amdgcn_sched_barrier(0);   // <= 2 levels of gathers in flight
             }
-            h1a = MFMA32(W[kW1 + (0 * 16 + l) * 64], f, h1a);
-            h1b = MFMA32(W[kW1 + (1 * 16 + l) * 64], f, h1b);
+            uint4 bh, bl;
+            split8(f, bh, bl);
+            h1a = mfma3(FH[(kF1 + 2 * kb) * 64], FL[(kF1 + 2 * kb) * 64], bh, bl, h1a);
+            h1b = mfma3(FH[(kF1 + 2 * kb + 1) * 64], FL[(kF1 + 2 * kb + 1) * 64], bh, bl, h1b);
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -367,14 +443,15 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
         }
         floatx16 h2a = {}, h2b = {};
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            h2a = MFMA32(W[kW2 + ((0 * 2 + 0) * 16 + q) * 64], h1a[q], h2a);
-            h2b = MFMA32(W[kW2 + ((1 * 2 + 0) * 16 + q) * 64], h1a[q], h2b);
-        }
+        for (int kb = 0; kb < 4; ++kb) {
+            float v[8];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            h2a = MFMA32(W[kW2 + ((0 * 2 + 1) * 16 + q) * 64], h1b[q], h2a);
-            h2b = MFMA32(W[kW2 + ((1 * 2 + 1) * 16 + q) * 64], h1b[q], h2b);
+            for (int m = 0; m < 8; ++m) v[m] = (kb >> 1) ? h1b[8 * (kb & 1) + m] : h1a[8 * (kb & 1) + m];
+            uint4 bh, bl;
+            split8(v, bh, bl);
+            h2a = mfma3(FH[(kF2 + 2 * kb) * 64], FL[(kF2 + 2 * kb) * 64], bh, bl, h2a);
+            h2b = mfma3(FH[(kF2 + 2 * kb + 1) * 64], FL[(kF2 + 2 * kb + 1) * 64], bh, bl, h2b);
+            __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -383,9 +460,15 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
         }
         floatx16 o3 = {};
 #pragma unroll
-        for (int q = 0; q < 16; ++q) o3 = MFMA32(W[kW3 + (0 * 16 + q) * 64], h2a[q], o3);
+        for (int kb = 0; kb < 4; ++kb) {
+            float v[8];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) o3 = MFMA32(W[kW3 + (1 * 16 + q) * 64], h2b[q], o3);
+            for (int m = 0; m < 8; ++m) v[m] = (kb >> 1) ? h2b[8 * (kb & 1) + m] : h2a[8 * (kb & 1) + m];
+            uint4 bh, bl;
+            split8(v, bh, bl);
+            o3 = mfma3(FH[(kF3 + kb) * 64], FL[(kF3 + kb) * 64], bh, bl, o3);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 
         // sigma pre-activation = row 0, held by the lower half-wave
         const float s_lo = o3[0];
@@ -412,19 +495,19 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
     const float ws = (float)wsum, dp = (float)depth;
     floatx16 v1 = {};
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v1 = MFMA32(Wl[kV1 + q * 64 + lane], fg[q], v1);
+    for (int q = 0; q < 8; ++q) v1 = MFMA32(Vl[kV1 + q * 64 + lane], fg[q], v1);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) v1 = MFMA32(Wl[kV1 + (8 + s) * 64 + lane], sh[2 * s + hh] * ws, v1);
+    for (int s = 0; s < 8; ++s) v1 = MFMA32(Vl[kV1 + (8 + s) * 64 + lane], sh[2 * s + hh] * ws, v1);
 #pragma unroll
     for (int i = 0; i < 16; ++i) v1[i] = fmaxf(v1[i], 0.0f);
     floatx16 v2 = {};
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v2 = MFMA32(Wl[kV2 + q * 64 + lane], v1[q], v2);
+    for (int q = 0; q < 16; ++q) v2 = MFMA32(Vl[kV2 + q * 64 + lane], v1[q], v2);
 #pragma unroll
     for (int i = 0; i < 16; ++i) v2[i] = fmaxf(v2[i], 0.0f);
     floatx16 v3 = {};
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v3 = MFMA32(Wl[kV3 + q * 64 + lane], v2[q], v3);
+    for (int q = 0; q < 16; ++q) v3 = MFMA32(Vl[kV3 + q * 64 + lane], v2[q], v3);
 
     if (!live) return;
     float* row = a.rows ? a.rows + (size_t)r * kRow : nullptr;
@@ -834,6 +917,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.bound = m->grid_bound;
     fa.bg = bg_color;
     fa.tab = w.tables;
+    fa.grid_emb = gg.emb;
     fa.G0 = m->grid_mlp[0];
     fa.G1 = m->grid_mlp[1];
     fa.G2 = m->grid_mlp[2];
