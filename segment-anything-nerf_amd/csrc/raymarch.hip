@@ -139,10 +139,6 @@ __global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
         }
         sn = spacing(near);
         sf = spacing(far);
-        if (k == 0) {
-            a.snf[r] = sn;
-            a.snf[N + r] = sf;
-        }
         b0 = a.bins0(k);
         b1 = a.bins0(k + 1);
     } else {
@@ -162,6 +158,12 @@ __global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
     dense<16, 10, true>(a.W0, feat, h);
     dense<1, 16, false>(a.W1, h, &sv);
     a.wtmp[(size_t)k * N + r] = (rb_next - rb_prev) * expf(sv);          // trunc_exp forward
+    // stores last: an earlier store could alias W0/W1 and would force the
+    // uniform weight reads from scalar to per-lane vector loads
+    if (FIRST && k == 0) {
+        a.snf[r] = sn;
+        a.snf[N + r] = sf;
+    }
 }
 
 // Proposal stage, part 2: one thread per ray, in the reference's sequential
