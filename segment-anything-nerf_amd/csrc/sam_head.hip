@@ -207,71 +207,95 @@ __global__ void __launch_bounds__(256) k_sam_head(HeadArgs a) {
 
 
 // ===================================================================== bf16x3
-// Split-precision head: x = x_hi + x_lo with x_hi = bf16(x), x_lo =
+// Split-precision head (default): x = x_hi + x_lo with x_hi = bf16(x), x_lo =
 // bf16(x - x_hi); A.B ~= A_lo.B_hi + A_hi.B_lo + A_hi.B_hi on
 // v_mfma_f32_32x32x16_bf16 (fp32 accumulate).  Relative error per product
-// ~2^-16 (the dropped A_lo.B_lo term and the rounding of the lo parts),
-// i.e. ~1e-5 on the head output against the 1e-3 budget, at 3 bf16 MFMAs per
-// 16-deep k-block instead of 8 fp32 ones (5.3x fewer matrix cycles).
+// ~2^-16 (the dropped A_lo.B_lo term and the rounding of the lo parts), i.e.
+// ~1e-5 on the head output against the 1e-3 budget, at 3 bf16 MFMAs per
+// 16-deep k-block instead of 8 fp32 ones.
+//
+// Orientation: out^T[256 units x 32 rays] = W . act^T -- A = weights (rows =
+// output units, 8 tiles of 32), B = activations (columns = the wave's 32
+// rays).  A 32x32 accumulator holds, in lane (j, h) register q, unit
+// rho(q) + 4h of ray j, rho(q) = (q&3) + 8(q>>2); k-block kb of a 256-wide
+// input takes registers 8(kb&1)..+7 of tile kb>>1, so after bias/activation
+// and the hi/lo split a layer's accumulators ARE the next layer's B operands
+// (weights are packed permuted to match, hidden_unit()).  Activations never
+// leave the registers; the x input (needed again by the skip layer) stays
+// resident as bf16 hi/lo.  Weights stream through LDS: one "step" = one
+// k-block of one layer for all 8 output tiles = 16 KiB of hi/lo fragments,
+// double-buffered and shared by the block's 4 waves (one per SIMD).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
 
-constexpr int kXkB = 176;                 // head input padded to 11 k-blocks of 16
-constexpr int kRowB = 264;                // LDS row stride in bf16 (528 B = 16 mod 256: conflict-free b128 reads)
-constexpr int kThreadsB = 512;            // 8 waves = the 8 output column tiles
-// k-block segments: 0 = W0 (x, 11), 1 = W1 (16), 2 = W2[:, :256] (h, 16),
-// 3 = W3 (16), 4 = W4 (16), 5 = W2[:, 256:] (x part of the skip layer, 11)
-constexpr int kKbB[6] = {11, 16, 16, 16, 16, 11};
-constexpr int kbBase(int seg) {
+constexpr int kXkb = 11;                      // 163 inputs -> 11 k-blocks of 16
+constexpr int kHkb = 16;                      // 256 -> 16 k-blocks
+// step segments in consumption order: L0 (x) | L1 (h) | L2 x-part | L2 h-part | L3 | L4
+constexpr int kSegKb[6] = {kXkb, kHkb, kXkb, kHkb, kHkb, kHkb};
+constexpr int segBase(int seg) {
     int b = 0;
-    for (int i = 0; i < seg; ++i) b += kKbB[i];
+    for (int i = 0; i < seg; ++i) b += kSegKb[i];
     return b;
 }
-constexpr int kKbTotal = kbBase(6);       // 86
+constexpr int kSteps = segBase(6);            // 86
+constexpr int kStepVec = 2 * 8 * 64;          // uint4 per step: [hi/lo][tile][lane]
+constexpr int kRaysV5 = 128;                  // 4 waves x 32 rays
 
-__device__ __forceinline__ uint32_t bf16_rne(float x) {
-    uint32_t u = __float_as_uint(x);
-    u += 0x7FFFu + ((u >> 16) & 1u);
-    return u >> 16;
-}
-__device__ __forceinline__ void split_bf16(float x, uint32_t& hi, uint32_t& lo) {
-    hi = bf16_rne(x);
-    lo = bf16_rne(x - __uint_as_float(hi << 16));
+__device__ __forceinline__ int rho(int q) { return (q & 3) + 8 * (q >> 2); }
+__device__ __forceinline__ int hidden_unit(int kb, int h, int m) {
+    return 32 * (kb >> 1) + rho(8 * (kb & 1) + m) + 4 * h;
 }
 
-// packed_{hi,lo}[tile 8][global k-block 86][lane 64] : 8 bf16 (16 B) each
+__device__ __forceinline__ void split_pair(float x, float y, uint32_t& hi, uint32_t& lo) {
+    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v){x, y}, bf16x2v));
+    const float hx = __uint_as_float(hi << 16), hy = __uint_as_float(hi & 0xffff0000u);
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v){x - hx, y - hy}, bf16x2v));
+}
+__device__ __forceinline__ void split8(const float* v, uint4& hi, uint4& lo) {
+    split_pair(v[0], v[1], hi.x, lo.x);
+    split_pair(v[2], v[3], hi.y, lo.y);
+    split_pair(v[4], v[5], hi.z, lo.z);
+    split_pair(v[6], v[7], hi.w, lo.w);
+}
+
+// packed[step 86][hi/lo][tile 8][lane 64] : 8 bf16 (16 B) each
 __global__ void __launch_bounds__(256)
 k_pack_bf3(const float* __restrict__ w0, const float* __restrict__ w1, const float* __restrict__ w2,
-           const float* __restrict__ w3, const float* __restrict__ w4, uint4* __restrict__ phi,
-           uint4* __restrict__ plo) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 8u * kKbTotal * 64u) return;
-    const uint32_t lane = t & 63u, rest = t >> 6;
-    const uint32_t tile = rest / kKbTotal, gkb = rest % kKbTotal;
+           const float* __restrict__ w3, const float* __restrict__ w4, uint4* __restrict__ packed) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;   // one (step, tile, lane)
+    if (t >= (uint32_t)kSteps * 8u * 64u) return;
+    const int lane = (int)(t & 63u), tile = (int)((t >> 6) & 7u), step = (int)(t >> 9);
     int seg = 0;
-    while (seg < 5 && (int)gkb >= kbBase(seg + 1)) ++seg;
-    const int kb = (int)gkb - kbBase(seg);
-    const float* W = seg == 0 ? w0 : seg == 1 ? w1 : (seg == 2 || seg == 5) ? w2 : seg == 3 ? w3 : w4;
-    const int ldw = seg == 0 ? kIn : (seg == 2 || seg == 5) ? 256 + kIn : 256;
-    const int col = (int)(tile * 32u + (lane & 31u));
-    uint32_t hi[8], lo[8];
+    while (seg < 5 && step >= segBase(seg + 1)) ++seg;
+    const int kb = step - segBase(seg);
+    const int i = lane & 31, h = lane >> 5, unit = tile * 32 + i;
+    float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int kp = kb * 16 + 8 * (int)(lane >> 5) + j;
-        int k = kp;                                   // logical weight column
-        if (seg == 0) k = kp < kIn ? kp : -1;
-        if (seg == 5) k = kp < kIn ? 256 + kp : -1;
-        const float v = k >= 0 ? W[(size_t)col * ldw + k] : 0.0f;
-        split_bf16(v, hi[j], lo[j]);
+    for (int m = 0; m < 8; ++m) {
+        const int kx = 16 * kb + 8 * h + m;           // x input column (natural order)
+        const int kh = hidden_unit(kb, h, m);         // hidden input unit (accumulator order)
+        float w;
+        switch (seg) {
+            case 0: w = kx < kIn ? w0[unit * kIn + kx] : 0.0f; break;
+            case 1: w = w1[unit * 256 + kh]; break;
+            case 2: w = kx < kIn ? w2[unit * (256 + kIn) + 256 + kx] : 0.0f; break;
+            case 3: w = w2[unit * (256 + kIn) + kh]; break;
+            case 4: w = w3[unit * 256 + kh]; break;
+            default: w = w4[unit * 256 + kh]; break;
+        }
+        v[m] = w;
     }
-    phi[t] = make_uint4(hi[0] | hi[1] << 16, hi[2] | hi[3] << 16, hi[4] | hi[5] << 16, hi[6] | hi[7] << 16);
-    plo[t] = make_uint4(lo[0] | lo[1] << 16, lo[2] | lo[3] << 16, lo[4] | lo[5] << 16, lo[6] | lo[7] << 16);
+    uint4 hi, lo;
+    split8(v, hi, lo);
+    packed[(size_t)step * kStepVec + tile * 64 + lane] = hi;
+    packed[(size_t)step * kStepVec + 512 + tile * 64 + lane] = lo;
 }
 
 struct HeadArgsB {
     const float* rows;
     uint32_t N;
-    const uint4* phi;
-    const uint4* plo;
+    const uint4* packed;
     const float* b[5];
     const float* ln_w;
     const float* ln_b;
@@ -280,203 +304,234 @@ struct HeadArgsB {
 
 #define MFMA_BF16(A, B, C) __builtin_amdgcn_mfma_f32_32x32x16_bf16((A), (B), (C), 0, 0, 0)
 
-// One workgroup = RT row tiles of 32 rays, 8 waves; wave ct owns output
-// columns 32ct..32ct+31 of every layer for ALL the block's rows, so each
-// weight fragment it streams from L2 feeds 3 x RT MFMAs (the head is bound by
-// that stream: ~11 KB of fragments per ray at RT = 4).  The skip layer's input
-// half W2[:, 256:] . x is accumulated during layer 0 (while x is resident), so
-// the activations need one in-place hi/lo buffer.
-template <int SEG, int RT>
-__device__ __forceinline__ void kloop_bf3(const HeadArgsB& a, const uint16_t* Ph, const uint16_t* Pl,
-                                          int ct, int lane, floatx16 (&acc)[RT]) {
-    const int r = lane & 31, h = lane >> 5;
-    const uint4* ph = a.phi + ((size_t)ct * kKbTotal + kbBase(SEG)) * 64 + lane;
-    const uint4* pl = a.plo + ((size_t)ct * kKbTotal + kbBase(SEG)) * 64 + lane;
-    uint4 bh = ph[0], bl = pl[0];
-#pragma unroll 1
-    for (int kb = 0; kb < kKbB[SEG]; ++kb) {
-        uint4 nh = bh, nl = bl;
-        if (kb + 1 < kKbB[SEG]) {           // prefetch the next k-block's B fragments (L2)
-            nh = ph[(kb + 1) * 64];
-            nl = pl[(kb + 1) * 64];
+__device__ __forceinline__ floatx16 mfma3(uint4 ah, uint4 al, uint4 bh, uint4 bl, floatx16 c) {
+    const bf16x8 Ah = __builtin_bit_cast(bf16x8, ah), Al = __builtin_bit_cast(bf16x8, al);
+    const bf16x8 Bh = __builtin_bit_cast(bf16x8, bh), Bl = __builtin_bit_cast(bf16x8, bl);
+    c = MFMA_BF16(Al, Bh, c);
+    c = MFMA_BF16(Ah, Bl, c);
+    return MFMA_BF16(Ah, Bh, c);
+}
+
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// Weight stream: step s's 16 KiB of fragments go global -> LDS by direct DMA
+// (global_load_lds_dwordx4, no VGPRs), into one of 3 buffers, two steps
+// ahead; each wave moves 4 KiB (4 wave-instructions of 64 x 16 B).  The step
+// boundary waits only for the step about to be read (counted vmcnt, one step
+// stays in flight across the raw barrier), per cdna_hip_programming.md
+// "Pipelining across barriers".
+struct HeadStepper {
+    const uint4* __restrict__ packed;
+    uint4* Wb;            // LDS [3][kStepVec]
+    int wave, lane;
+    int step;
+
+    // The DMA is issued from inline asm so that the compiler does not see an
+    // LDS write of unknown extent in flight (it would drain vmcnt(0) before
+    // every ds_read); the waits are counted by hand in run().  No ordinary
+    // vector-memory load is issued inside the step loop.
+    __device__ __forceinline__ void issue(int s) {
+        const uint4* src = packed + (size_t)s * kStepVec + wave * 256 + lane;
+        const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(Wb + (s % 3) * kStepVec + wave * 256);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t d = __builtin_amdgcn_readfirstlane(dst + c * 1024u);
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(src + c * 64), "s"(d)
+                : "memory");
         }
-        const int kk = kb * 16 + 8 * h;
-        bf16x8 ah[RT], al[RT];
+    }
+
+    // one k-block of the current layer for all 8 output tiles
+    __device__ __forceinline__ void run(floatx16 (&acc)[8], const uint4& bh, const uint4& bl) {
+        const bool ahead = step + 2 < kSteps;
+        if (ahead) issue(step + 2);
+        const uint4* cur = Wb + (step % 3) * kStepVec + lane;
+        uint4 fh[8], fl[8];
 #pragma unroll
-        for (int t = 0; t < RT; ++t) {
-            ah[t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Ph + (t * 32 + r) * kRowB + kk));
-            al[t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Pl + (t * 32 + r) * kRowB + kk));
+        for (int t = 0; t < 8; ++t) {
+            fh[t] = cur[t * 64];
+            fl[t] = cur[512 + t * 64];
         }
-        const bf16x8 b_h = __builtin_bit_cast(bf16x8, bh), b_l = __builtin_bit_cast(bf16x8, bl);
-        // small terms first, RT independent accumulators between dependent MFMAs
 #pragma unroll
-        for (int t = 0; t < RT; ++t) acc[t] = MFMA_BF16(al[t], b_h, acc[t]);
+        for (int t = 0; t < 8; ++t) acc[t] = mfma3(fh[t], fl[t], bh, bl, acc[t]);
+        if (ahead) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // step + 1 landed
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        ++step;
+    }
+};
+
+__device__ __forceinline__ float leaky(float x, bool act) { return act && x < 0.0f ? x * 0.01f : x; }
+
+// bias (+ leaky_relu) on the accumulators, then the hi/lo split into the next
+// layer's B operands (k-block kb = 2t + s <- registers 8s..8s+7 of tile t)
+__device__ __forceinline__ void epilogue(const floatx16 (&acc)[8], const float* Bs, int h,
+                                         uint4 (&ah)[kHkb], uint4 (&al)[kHkb]) {
 #pragma unroll
-        for (int t = 0; t < RT; ++t) acc[t] = MFMA_BF16(ah[t], b_l, acc[t]);
+    for (int t = 0; t < 8; ++t) {
+        float v[16];
 #pragma unroll
-        for (int t = 0; t < RT; ++t) acc[t] = MFMA_BF16(ah[t], b_h, acc[t]);
-        bh = nh;
-        bl = nl;
+        for (int mm = 0; mm < 4; ++mm) {      // registers 4mm..4mm+3 = units 32t + 8mm + 4h + 0..3
+            const float4 bb = *reinterpret_cast<const float4*>(Bs + 32 * t + 8 * mm + 4 * h);
+            v[4 * mm + 0] = leaky(acc[t][4 * mm + 0] + bb.x, true);
+            v[4 * mm + 1] = leaky(acc[t][4 * mm + 1] + bb.y, true);
+            v[4 * mm + 2] = leaky(acc[t][4 * mm + 2] + bb.z, true);
+            v[4 * mm + 3] = leaky(acc[t][4 * mm + 3] + bb.w, true);
+        }
+        split8(v, ah[2 * t], al[2 * t]);
+        split8(v + 8, ah[2 * t + 1], al[2 * t + 1]);
     }
 }
 
-// bias + activation, written back in place as bf16 hi/lo planes (or fp32 for
-// the LayerNorm), after every wave has finished reading the planes.
-template <bool LAST, int RT>
-__device__ __forceinline__ void epilogue_bf3(const float* __restrict__ bias, uint16_t* Ph, uint16_t* Pl,
-                                             float* F, int ct, int lane, const floatx16 (&acc)[RT]) {
-    const int r = lane & 31, h = lane >> 5;
-    const int col = ct * 32 + r;
-    const float bc = bias[col];
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_sam_head_bf3(HeadArgsB a) {
+    // one LDS object (a second __shared__ object can de-pipeline the DMA
+    // waits): 3 x 16 KiB weight steps, then biases and LN weight/bias
+    __shared__ uint4 smem[3 * kStepVec + (7 * 256) / 4];
+    uint4* Wb = smem;
+    float* Bs = reinterpret_cast<float*>(smem + 3 * kStepVec);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int j = lane & 31, h = lane >> 5;
+    const uint32_t ray = blockIdx.x * kRaysV5 + wave * 32u + j;
+    const bool live = ray < a.N;
+
+    for (int i = tid; i < 5 * 256; i += 256) Bs[i] = a.b[i >> 8][i & 255];
+    Bs[5 * 256 + tid] = a.ln_w[tid];
+    Bs[6 * 256 + tid] = a.ln_b[tid];
+
+    // x (head input row) as B operands: k-block kb, lane half h -> columns
+    // 16kb + 8h .. +7; loaded again for the skip layer rather than held in
+    // 88 VGPRs through layer 1
+    const float* xr = a.rows + (size_t)(live ? ray : 0u) * kRowIn;
+    auto load_x = [&](int kb, uint4& xh, uint4& xl) {
+        float v[8];
+        const int c0 = 16 * kb + 8 * h;
+        if (c0 + 8 <= kRowIn) {
+            const float4 p = *reinterpret_cast<const float4*>(xr + c0);
+            const float4 q = *reinterpret_cast<const float4*>(xr + c0 + 4);
+            v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w;
+            v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
+        } else {
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int row = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-            const float v = acc[t][i] + bc;
-            if constexpr (!LAST) {
-                uint32_t hi, lo;
-                split_bf16(leaky(v), hi, lo);
-                Ph[row * kRowB + col] = (uint16_t)hi;
-                Pl[row * kRowB + col] = (uint16_t)lo;
-            } else {
-                F[row * kHStride + col] = v;
-            }
+            for (int m = 0; m < 8; ++m) v[m] = c0 + m < kRowIn ? xr[c0 + m] : 0.0f;
         }
-    }
-}
-
-template <int RT>
-constexpr size_t head_lds_bytes() { return (size_t)2 * RT * 32 * kRowB * sizeof(uint16_t); }
-
-template <int RT>
-__global__ void __launch_bounds__(kThreadsB) k_sam_head_bf3(HeadArgsB a) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
-    constexpr int kRows = RT * 32;
-    uint16_t* Ph = lds;                       // bf16 hi plane [kRows][kRowB]
-    uint16_t* Pl = lds + kRows * kRowB;       // bf16 lo plane
-    float* F = reinterpret_cast<float*>(lds); // fp32 pre-LayerNorm tile [kRows][257] (aliases the planes)
-    static_assert((size_t)kRows * kHStride * 4 <= head_lds_bytes<RT>(), "LN tile must fit the planes");
-    const int tid = threadIdx.x, ct = tid >> 6, lane = tid & 63;
-    const uint32_t ray0 = blockIdx.x * kRows;
-    for (int i = tid; i < kRows * kXkB; i += kThreadsB) {
-        const int rr = i / kXkB, c = i % kXkB;
-        const uint32_t ray = ray0 + rr;
-        float v = 0.0f;
-        if (ray < a.N && c < kIn) v = a.rows[(size_t)ray * kRowIn + c];
-        uint32_t hi, lo;
-        split_bf16(v, hi, lo);
-        Ph[rr * kRowB + c] = (uint16_t)hi;
-        Pl[rr * kRowB + c] = (uint16_t)lo;
-    }
-    __syncthreads();
-
-    floatx16 acc[RT], skip[RT];
 #pragma unroll
-    for (int t = 0; t < RT; ++t) { acc[t] = floatx16{}; skip[t] = floatx16{}; }
-    kloop_bf3<0, RT>(a, Ph, Pl, ct, lane, acc);        // layer 0: W0 . x
-    kloop_bf3<5, RT>(a, Ph, Pl, ct, lane, skip);       // layer 2's W2[:, 256:] . x
-    __syncthreads();
-    epilogue_bf3<false, RT>(a.b[0], Ph, Pl, F, ct, lane, acc);
-    __syncthreads();
+        for (int m = 0; m < 8; ++m)
+            if (!live || c0 + m >= kIn) v[m] = 0.0f;      // column 163 of a row is padding
+        split8(v, xh, xl);
+    };
+    uint4 xh[kXkb], xl[kXkb];
 #pragma unroll
-    for (int t = 0; t < RT; ++t) acc[t] = floatx16{};
-    kloop_bf3<1, RT>(a, Ph, Pl, ct, lane, acc);        // layer 1
+    for (int kb = 0; kb < kXkb; ++kb) load_x(kb, xh[kb], xl[kb]);
+    HeadStepper st{a.packed, Wb, wave, lane, 0};
+    st.issue(0);
+    st.issue(1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");          // step 0 landed
     __syncthreads();
-    epilogue_bf3<false, RT>(a.b[1], Ph, Pl, F, ct, lane, acc);
-    __syncthreads();
-    kloop_bf3<2, RT>(a, Ph, Pl, ct, lane, skip);       // layer 2: + W2[:, :256] . h
-    __syncthreads();
-    epilogue_bf3<false, RT>(a.b[2], Ph, Pl, F, ct, lane, skip);
-    __syncthreads();
+    floatx16 acc[8];
+    uint4 ah[kHkb], al[kHkb];
+    auto zero = [&]() {
 #pragma unroll
-    for (int t = 0; t < RT; ++t) acc[t] = floatx16{};
-    kloop_bf3<3, RT>(a, Ph, Pl, ct, lane, acc);        // layer 3
-    __syncthreads();
-    epilogue_bf3<false, RT>(a.b[3], Ph, Pl, F, ct, lane, acc);
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < RT; ++t) acc[t] = floatx16{};
-    kloop_bf3<4, RT>(a, Ph, Pl, ct, lane, acc);        // layer 4 (no activation)
-    __syncthreads();
-    epilogue_bf3<true, RT>(a.b[4], Ph, Pl, F, ct, lane, acc);
-    __syncthreads();
+        for (int t = 0; t < 8; ++t) acc[t] = floatx16{};
+    };
 
-    // LayerNorm(256, eps=1e-5): TPR threads per row, in double
-    constexpr int TPR = kThreadsB / kRows, CPT = 256 / TPR;
-    const int row = tid / TPR, q = tid % TPR;
-    const float* hr = F + row * kHStride + q * CPT;
+    zero();                                                   // layer 0: W0 . x
+#pragma unroll
+    for (int kb = 0; kb < kXkb; ++kb) st.run(acc, xh[kb], xl[kb]);
+    epilogue(acc, Bs + 0 * 256, h, ah, al);
+    zero();                                                   // layer 1
+#pragma unroll
+    for (int kb = 0; kb < kHkb; ++kb) st.run(acc, ah[kb], al[kb]);
+    epilogue(acc, Bs + 1 * 256, h, ah, al);
+    zero();                                                   // layer 2: W2 . cat(h, x)
+#pragma unroll
+    for (int kb = 0; kb < kXkb; ++kb) load_x(kb, xh[kb], xl[kb]);
+#pragma unroll
+    for (int kb = 0; kb < kXkb; ++kb) st.run(acc, xh[kb], xl[kb]);
+#pragma unroll
+    for (int kb = 0; kb < kHkb; ++kb) st.run(acc, ah[kb], al[kb]);
+    epilogue(acc, Bs + 2 * 256, h, ah, al);
+    zero();                                                   // layer 3
+#pragma unroll
+    for (int kb = 0; kb < kHkb; ++kb) st.run(acc, ah[kb], al[kb]);
+    epilogue(acc, Bs + 3 * 256, h, ah, al);
+    zero();                                                   // layer 4 (no activation)
+#pragma unroll
+    for (int kb = 0; kb < kHkb; ++kb) st.run(acc, ah[kb], al[kb]);
+
+    // + bias, LayerNorm(256, eps=1e-5) per ray: this lane holds 128 of the
+    // ray's units, the other half-wave (lane ^ 32) the rest; sums in double
     double s = 0.0;
-    for (int c = 0; c < CPT; ++c) s += (double)hr[c];
 #pragma unroll
-    for (int m = 1; m < TPR; m <<= 1) s += __shfl_xor(s, m, TPR);
-    const double mean = s / 256.0;
-    double v = 0.0;
-    for (int c = 0; c < CPT; ++c) {
-        const double dlt = (double)hr[c] - mean;
-        v += dlt * dlt;
-    }
+    for (int t = 0; t < 8; ++t)
 #pragma unroll
-    for (int m = 1; m < TPR; m <<= 1) v += __shfl_xor(v, m, TPR);
-    const float rstd = (float)(1.0 / sqrt(v / 256.0 + 1e-5));
-    const float mf = (float)mean;
-    const uint32_t ray = ray0 + row;
-    if (ray < a.N) {
-        float* o = a.out + (size_t)ray * 256 + q * CPT;
-        const float* lw = a.ln_w + q * CPT;
-        const float* lb = a.ln_b + q * CPT;
-        for (int c = 0; c < CPT; c += 4) {
-            float4 y;
-            y.x = ((hr[c + 0] - mf) * rstd) * lw[c + 0] + lb[c + 0];
-            y.y = ((hr[c + 1] - mf) * rstd) * lw[c + 1] + lb[c + 1];
-            y.z = ((hr[c + 2] - mf) * rstd) * lw[c + 2] + lb[c + 2];
-            y.w = ((hr[c + 3] - mf) * rstd) * lw[c + 3] + lb[c + 3];
-            *reinterpret_cast<float4*>(o + c) = y;
+        for (int q = 0; q < 16; ++q) {
+            acc[t][q] += Bs[4 * 256 + 32 * t + rho(q) + 4 * h];
+            s += (double)acc[t][q];
         }
-    }
-}
-
-template <int RT>
-int launch_head_bf3(const HeadArgsB& a, hipStream_t s) {
-    static bool attr = false;                 // > 64 KB of dynamic LDS needs opting in once
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sam_head_bf3<RT>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)head_lds_bytes<RT>()) != hipSuccess)
-            return fail(SAMNERF_ELAUNCH, "sam_head: cannot reserve %zu B of LDS", head_lds_bytes<RT>());
-        attr = true;
-    }
-    k_sam_head_bf3<RT><<<div_up(a.N, RT * 32u), kThreadsB, head_lds_bytes<RT>(), s>>>(a);
-    return check_launch("sam_head_bf3");
+    s += __shfl_xor(s, 32);
+    const double mean = s / 256.0;
+    double var = 0.0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const double dlt = (double)acc[t][q] - mean;
+            var += dlt * dlt;
+        }
+    var += __shfl_xor(var, 32);
+    const float rstd = (float)(1.0 / sqrt(var / 256.0 + 1e-5));
+    const float mf = (float)mean;
+    if (!live) return;
+    float* o = a.out + (size_t)ray * 256;
+    const float* lw = Bs + 5 * 256;
+    const float* lb = Bs + 6 * 256;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+            const int u = 32 * t + 8 * mm + 4 * h;
+            float4 y;
+            y.x = ((acc[t][4 * mm + 0] - mf) * rstd) * lw[u + 0] + lb[u + 0];
+            y.y = ((acc[t][4 * mm + 1] - mf) * rstd) * lw[u + 1] + lb[u + 1];
+            y.z = ((acc[t][4 * mm + 2] - mf) * rstd) * lw[u + 2] + lb[u + 2];
+            y.w = ((acc[t][4 * mm + 3] - mf) * rstd) * lw[u + 3] + lb[u + 3];
+            *reinterpret_cast<float4*>(o + u) = y;
+        }
 }
 
 }  // namespace
 
 size_t sam_head_packed_floats() {
     const size_t f32 = (size_t)8 * kTotalGroups * 64 * 4;
-    const size_t bf3 = (size_t)2 * 8 * kKbTotal * 64 * 4;      // hi + lo uint4 planes
+    const size_t bf3 = (size_t)kSteps * kStepVec * 4;        // uint4 fragments
     return f32 > bf3 ? f32 : bf3;
 }
 
 int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, float* samvit,
                      float* packed, hipStream_t s) {
     if (m->head_mode == 0) {                                     // bf16x3 (default)
-        const uint32_t nvec = 8u * kKbTotal * 64u;
-        uint4* phi = reinterpret_cast<uint4*>(packed);
-        uint4* plo = phi + nvec;
-        k_pack_bf3<<<div_up(nvec, 256), 256, 0, s>>>(m->sam_w[0], m->sam_w[1], m->sam_w[2],
-                                                     m->sam_w[3], m->sam_w[4], phi, plo);
+        uint4* pk = reinterpret_cast<uint4*>(packed);
+        const uint32_t nfrag = (uint32_t)kSteps * 8u * 64u;
+        k_pack_bf3<<<div_up(nfrag, 256), 256, 0, s>>>(m->sam_w[0], m->sam_w[1], m->sam_w[2],
+                                                      m->sam_w[3], m->sam_w[4], pk);
         HeadArgsB a;
         a.rows = rows;
         a.N = N;
-        a.phi = phi;
-        a.plo = plo;
+        a.packed = pk;
         for (int i = 0; i < 5; ++i) a.b[i] = m->sam_b[i];
         a.ln_w = m->ln_w;
         a.ln_b = m->ln_b;
         a.out = samvit;
-        // 128 rays per block when that still gives >= 2 blocks per CU, else 64
-        return N >= 128u * 512u ? launch_head_bf3<4>(a, s) : launch_head_bf3<2>(a, s);
+        k_sam_head_bf3<<<div_up(N, (uint32_t)kRaysV5), 256, 0, s>>>(a);
+        return check_launch("sam_head_bf3");
     }
     const uint32_t nvec = 8u * kTotalGroups * 64u;
     k_pack<<<div_up(nvec, 256), 256, 0, s>>>(m->sam_w[0], m->sam_w[1], m->sam_w[2], m->sam_w[3],
