@@ -359,15 +359,22 @@ __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const Leve
     return LevelDesc{hi ? q.off : p.off, hi ? q.size : p.size, hi ? q.res : p.res, hi ? q.flags : p.flags};
 }
 
-// One wave marches 32 rays.  Lane (j, h) owns ray j; for k-block kb it
-// gathers both channels of levels 8kb + 4h .. 8kb + 4h + 3 -- exactly its B
-// operand of the first layer (input index 2*level + channel) -- so the hash
-// grid feeds the matrix cores with no data movement.  grid_mlp 32->64->64->16
-// runs on bf16x3 MFMAs, view_mlp 31->32->32->3 (once per ray) on fp32 MFMAs;
-// compositing runs in-lane (both half-waves hold the same ray and compute the
-// same weights).
-template <int T>
+// One wave marches 32 (ray, segment) columns: with S segments per ray, lane
+// (j, h) owns segment j / R of ray j % R (R = 32 / S rays per wave), i.e. the
+// T/S samples seg*T/S .. (seg+1)*T/S - 1.  For k-block kb it gathers both
+// channels of levels 8kb + 4h .. 8kb + 4h + 3 -- exactly its B operand of the
+// first layer (input index 2*level + channel) -- so the hash grid feeds the
+// matrix cores with no data movement.  grid_mlp 32->64->64->16 runs on bf16x3
+// MFMAs, view_mlp 31->32->32->3 (once per ray) on fp32 MFMAs.  Compositing
+// runs in-lane with segment-local transmittance; compositing is associative
+// (C = C_0 + T_0 C_1 + T_0 T_1 C_2 ...), so the segments are combined by
+// shuffles at the end and the later segments' stored weights rescaled.  S > 1
+// only serves small N (one rank's share of a view), where S-times more waves
+// hide the gather latency.
+template <int T, int S>
 __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
+    static_assert(S == 1 || S == 2 || S == 4, "segments per ray");
+    constexpr int R = 32 / S, TS = T / S;
     __shared__ uint4 Fh[kFSlots * 64], Fl[kFSlots * 64];
     __shared__ float Vl[kVTotal];
     for (int idx = threadIdx.x; idx < kFSlots * 64; idx += 256) {
@@ -381,12 +388,14 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int hh = lane >> 5, jj = lane & 31;
-    const uint32_t ray0 = blockIdx.x * 128u + wave * 32u;
+    const int seg = jj / R;
+    const uint32_t ray0 = blockIdx.x * (4u * R) + wave * (uint32_t)R;
     if (ray0 >= a.N) return;                             // wave-uniform
-    const uint32_t r = ray0 + jj;
+    const uint32_t r = ray0 + (uint32_t)(jj % R);
     const bool live = r < a.N;
     const uint32_t rr = live ? r : a.N - 1;
-    const bool writer = live && hh == 0;
+    const bool sample_writer = live && hh == 0;          // u_out / w_out of this segment
+    const bool writer = sample_writer && seg == 0;       // per-ray outputs
     const uint32_t N = a.N;
     const GridDesc<16>* __restrict__ G = &a.tab->grid;
     const float2* __restrict__ emb = reinterpret_cast<const float2*>(a.grid_emb);
@@ -399,19 +408,20 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
     }
     const float sn = a.snf[rr], sf = a.snf[N + rr];
     const float b2 = 2.0f * a.bound;
-    float rb_prev = real_bin(sn, sf, a.bins_in[rr]);
+    const int k0 = seg * TS;
+    float rb_prev = real_bin(sn, sf, a.bins_in[(size_t)k0 * N + rr]);
     double cum = 0.0, wsum = 0.0, depth = 0.0;
     float fg[8];                                          // sum_k w_k * grid_mlp rows (acc layout)
 #pragma unroll
     for (int q = 0; q < 8; ++q) fg[q] = 0.0f;
 
-    for (int k = 0; k < T; ++k) {
+    for (int k = k0; k < k0 + TS; ++k) {
         const float rb_next = real_bin(sn, sf, a.bins_in[(size_t)(k + 1) * N + rr]);
         const float t = (rb_next + rb_prev) / 2.0f;
         float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
         contract3(x, y, z);
         const float ux = (x + a.bound) / b2, uy = (y + a.bound) / b2, uz = (z + a.bound) / b2;
-        if (writer) {
+        if (sample_writer) {
             a.u_out[((size_t)k * 3 + 0) * N + r] = ux;
             a.u_out[((size_t)k * 3 + 1) * N + r] = uy;
             a.u_out[((size_t)k * 3 + 2) * N + r] = uz;
@@ -477,12 +487,46 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
         const float s_hi = __shfl_xor(s_lo, 32);
         const float sigma = expf(hh == 0 ? s_lo : s_hi);
         const float w = composite_step((rb_next - rb_prev) * sigma, cum, k == T - 1);
-        if (writer) a.w_out[(size_t)k * N + r] = w;
+        if (sample_writer) a.w_out[(size_t)k * N + r] = w;
         wsum += (double)w;
         depth += (double)(w * t);
 #pragma unroll
         for (int q = 0; q < 8; ++q) fg[q] = fg[q] + w * o3[q];
         rb_prev = rb_next;
+    }
+
+    if constexpr (S > 1) {
+        // combine the segments of each ray (lanes jj % R + R*s, same half h):
+        // segment s is attenuated by exp(-sum of the earlier segments' optical
+        // depth); lanes of segment 0 end up with the ray's totals
+        double pre = 0.0;                                  // optical depth before this segment
+#pragma unroll
+        for (int s2 = 0; s2 < S - 1; ++s2) {
+            const double c2 = __shfl(cum, (jj % R) + R * s2 + 32 * hh);
+            if (s2 < seg) pre += c2;
+        }
+        if (seg > 0 && sample_writer) {                  // rescale this segment's weights
+            const float tr = expf(-(float)pre);
+            for (int k = k0; k < k0 + TS; ++k) a.w_out[(size_t)k * N + r] *= tr;
+        }
+        double pw = 0.0, pd = 0.0, acc_pre = 0.0;
+        float pf[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pf[q] = 0.0f;
+#pragma unroll
+        for (int s2 = 0; s2 < S; ++s2) {
+            const int src = (jj % R) + R * s2 + 32 * hh;
+            const float tr = expf(-(float)acc_pre);
+            pw += (double)tr * __shfl(wsum, src);
+            pd += (double)tr * __shfl(depth, src);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pf[q] += tr * __shfl(fg[q], src);
+            acc_pre += __shfl(cum, src);
+        }
+        wsum = pw;
+        depth = pd;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) fg[q] = pf[q];
     }
 
     // view MLP on the accumulated colour features: rows 1..15 of fg are
@@ -511,7 +555,7 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) v3 = MFMA32(Vl[kV3 + q * 64 + lane], v2[q], v3);
 
-    if (!live) return;
+    if (!live || seg != 0) return;
     float* row = a.rows ? a.rows + (size_t)r * kRow : nullptr;
     if (row) {                                 // geo units owned by this half-wave
 #pragma unroll
@@ -935,7 +979,10 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.wsum = weights_sum;
     fa.rows = m->with_sam || feature_rows ? rows : nullptr;
     mark_stage(2, s);
-    k_final<32><<<div_up(N, 128), 256, 0, s>>>(fa);
+    // segments per ray: enough waves to fill the resident slots (2 per SIMD)
+    if (N >= 65536u) k_final<32, 1><<<div_up(N, 128), 256, 0, s>>>(fa);
+    else if (N >= 32768u) k_final<32, 2><<<div_up(N, 64), 256, 0, s>>>(fa);
+    else k_final<32, 4><<<div_up(N, 32), 256, 0, s>>>(fa);
 
     if (m->with_sam) {
         SgridArgs sa{};

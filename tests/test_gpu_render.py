@@ -201,3 +201,31 @@ def test_sam_head_bf16x3_matches_exact_fp32(hip_lib, cuda):
     assert err < 2e-4, err
     ref = oracle_for(spec, params).run(ro[:256].cpu(), rd[:256].cpu(), return_feats=1)["samvit"]
     assert (exact[:256].cpu() - ref).abs().max().item() < 1e-4
+
+
+def test_ray_segment_paths_agree(hip_lib, cuda):
+    """k_final splits each ray into S = 1, 2 or 4 sample segments by N (more
+    waves for one rank's small share of a view) and recombines them
+    associatively: the same rays rendered at N >= 65536 (S = 1), 32768 <= N
+    < 65536 (S = 2) and N < 32768 (S = 4) must agree to fp32 rounding, and the
+    per-sample weights handed to the s_grid gather must too (f_sam rows)."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer, ROW
+    spec = synth.ModelSpec(with_sam=True)
+    params = synth.make_params(spec, seed=21, emb_scale=0.5, ln_jitter=0.1)
+    net = make_net(spec, params, cuda)
+    pose, intr = synth.gui_camera(512, 160, rot=synth.random_rotation(5))
+    ro, rd = ops.get_rays(pose, intr, 160, 512, device=cuda)          # 81920 rays
+    fr = FusedRenderer(net)
+    outs = {}
+    for n in (81920, 40000, 9000):
+        rows = torch.empty(n, ROW, device=cuda)
+        o = fr.render(ro[:n], rd[:n], rows=rows)
+        o["rows"] = rows
+        outs[n] = o
+    for n in (40000, 9000):
+        for k in ("image", "depth", "weights_sum", "samvit", "rows"):
+            a, b = outs[81920][k][:n], outs[n][k]
+            tol = 1e-4 * (1 + a.abs().max().item()) if k in ("depth", "rows") else 1e-4
+            err = (a - b).abs().max().item()
+            assert err < tol, (n, k, err)
