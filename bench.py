@@ -8,7 +8,9 @@ compositing + 256-d SAM head per ray) on synthetic random-init weights of the
 reference architecture.  With --gpus N > 1 (torchrun, one rank per GPU) the
 view's rows are split into N equal bands (strong scaling on a fixed view) and
 the packed per-ray outputs [rays/N, 3+1+1+256] are all-gathered over RCCL, as
-BASELINE config 4 / SURVEY.md 8e describe.
+BASELINE config 4 / SURVEY.md 8e describe.  Each step is one full view on every
+rank; view i's all-gather runs behind view i+1's kernels, and the last view's
+gather completes inside the timed region.
 
 Prints ONE JSON line (rank 0).  `value` = rays of the whole view x steps /
 (max over ranks of the timed region).  `roofline` prices the dominant kernel
@@ -59,7 +61,9 @@ def parse():
                     help="rays in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--head-mode", type=int, default=0, help="0 bf16x3 SAM head, 1 exact fp32")
     ap.add_argument("--chunks", type=int, default=0,
-                    help="row chunks per rank band for the pipelined all-gather (0 = auto)")
+                    help="N > 1: 0 = one launch per view with its all-gather pipelined behind "
+                         "the next view's rendering; k > 0 = k row chunks per view, each "
+                         "chunk's all-gather behind the next chunk")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -113,7 +117,7 @@ def main():
     rank, world, dev = setup_dist(args)
     from samnerf_amd import ops
     from samnerf_amd._lib import lib
-    from samnerf_amd.dist import render_view_sharded, shard_range
+    from samnerf_amd.dist import ShardedViewPipeline, render_view_sharded, shard_range
     from samnerf_amd.fused import FusedRenderer
     from oracle import synth
 
@@ -125,11 +129,7 @@ def main():
     r0, r1 = shard_range(H, rank, world)                      # row band of this rank
     n_total = H * W
     band_rays = (r1 - r0) * W
-    chunks = 1
-    if world > 1:
-        # enough chunks to hide the all-gather, each still large enough to
-        # fill the chip (>= 16384 rays)
-        chunks = args.chunks or max(1, min(4, band_rays // 16384))
+    chunks = max(1, args.chunks) if world > 1 else 1
 
     import ctypes
 
@@ -151,12 +151,19 @@ def main():
             lib().samnerf_set_stage_events(raw, 6 if raw is not None else 0)
             return renderer.render(ro, rd)
 
-        if world > 1:
+        if world > 1 and args.chunks > 0:
             return render_view_sharded(render_fn, ray_fn, H, W, chunks=chunks)
+        if world > 1:
+            pipe.submit(ray_fn, render_fn)   # this view's gather overlaps the next view
+            return pipe.collect_ready()
         return render_fn(*ray_fn(r0, r1 - r0))
+
+    pipe = ShardedViewPipeline(renderer.render, H, W) if world > 1 and args.chunks == 0 else None
 
     for _ in range(args.warmup):
         step()
+    if pipe is not None:
+        pipe.flush()
     sets = [[make_event_set() for _ in range(chunks)] for _ in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:
@@ -165,6 +172,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step([raw for _, raw in sets[i]])
+    if pipe is not None:
+        pipe.flush()                         # the last view's gather is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -201,8 +210,10 @@ def main():
             "config": {"workload": ("cfg3: 512x512 view, RGB + 256-d SAM feature per ray" if with_sam
                                     else "cfg2: 512x512 view, RGB only") if (H, W) == (512, 512)
                        else f"{H}x{W} view", "rays_per_step": n_total, "num_steps": [128, 64, 32],
-                       "parallelism": f"ray-sharded row bands x{world}, {chunks} chunk(s) per band, "
-                                      "async RCCL all-gather per chunk" if world > 1
+                       "parallelism": (f"ray-sharded row bands x{world}, RCCL all-gather of each view "
+                                       "overlapped with the next view's rendering" if args.chunks == 0 else
+                                       f"ray-sharded row bands x{world}, {chunks} chunks per band, "
+                                       "async RCCL all-gather per chunk") if world > 1
                        else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -7,8 +7,9 @@
 // ops per chunk):
 //   k_prop_sigma<128>       one thread per (ray, sample): near/far + uniform
 //                           bins + prop0 grid/MLP -> ds = delta * sigma
-//   k_prop_pdf<128, 65>     one thread per ray: compositing (double cumsum) +
-//                           torch-ordered normaliser + inverse-CDF -> 65 bins
+//   k_prop_pdf<128, 65>     per ray: compositing (double cumsum) + torch-
+//                           ordered normaliser + cdf (one thread), inverse-CDF
+//                           (four threads, quarter merge walks) -> 65 bins
 //   k_prop_sigma/pdf<64,33> the same for prop1 -> 33 bins
 //   k_final<32>             final samples: hash grid L16C2 + sigma/geo MLP +
 //                           SH(4) + compositing + view MLP -> image, depth,
@@ -58,6 +59,18 @@ Lin make_lin(float start, float end, uint32_t steps) {
     return l;
 }
 
+// XCD-aware block order.  Blocks are dispatched round-robin over the 8 XCDs
+// (block b runs on XCD b % 8), each with its own 4 MB L2.  A launch over n
+// ray chunks uses xcd_blocks(n) blocks and block b takes chunk xcd_chunk(b,
+// n): XCD x gets the contiguous chunks [x*per, (x+1)*per) -- a band of the
+// view -- so the grid cells that neighbouring rays share meet in one L2
+// instead of eight.  Chunks >= n are empty.
+__host__ __device__ constexpr uint32_t xcd_per(uint32_t n) { return (n + 7u) / 8u; }
+__host__ __device__ constexpr uint32_t xcd_blocks(uint32_t n) { return xcd_per(n) * 8u; }
+__device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t n) {
+    return (b & 7u) * xcd_per(n) + (b >> 3);
+}
+
 // MLP layer y = W x (torch layout W[out][in]), fma chain in input order.
 template <int OUT, int IN, bool RELU>
 __device__ __forceinline__ void dense(const float* __restrict__ W, const float* x, float* y) {
@@ -102,22 +115,22 @@ struct PropArgs {
 
 // Proposal stage, part 1: one thread per (ray, sample).  A wave is 64
 // neighbouring rays at one sample index (their corner gathers share cache
-// lines) and a block is 4 consecutive sample indices of those rays.  Blocks
-// are ordered so that all T/4 sample groups of a ray group are dispatched to
-// the same XCD (block b runs on XCD b % 8) and share its L2.  Writes ds_k =
+// lines) and a block is 4 consecutive sample indices of those rays.  XCD x
+// (blocks b with b % 8 == x) owns a contiguous band of ray groups, all T/4
+// sample groups of each, so they share its L2.  Writes ds_k =
 // (real_bin_{k+1} - real_bin_k) * trunc_exp(density) (renderer.py:282-300)
 // to wtmp[k][r]; the serial part of compositing is in k_prop_pdf.
 template <int T>
 constexpr uint32_t prop_sigma_blocks(uint32_t N) {
-    return ((N + 511u) / 512u) * 8u * (T / 4);
+    return xcd_blocks((N + 63u) / 64u) * (T / 4);
 }
 
 template <int T, bool FIRST>
 __global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
     static_assert(T % 4 == 0, "T must be a multiple of 4");
     constexpr uint32_t Q = T / 4;
-    const uint32_t b = blockIdx.x;
-    const uint32_t q = (b >> 3) % Q, g = ((b >> 3) / Q) * 8u + (b & 7u);
+    const uint32_t b = blockIdx.x, i = b >> 3;
+    const uint32_t q = i % Q, g = (b & 7u) * xcd_per((a.N + 63u) / 64u) + i / Q;
     const uint32_t r = g * 64u + (threadIdx.x & 63u), k = q * 4u + (threadIdx.x >> 6);
     if (r >= a.N) return;
     const uint32_t N = a.N;
@@ -166,34 +179,69 @@ __global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
     }
 }
 
-// Proposal stage, part 2: one thread per ray, in the reference's sequential
-// order -- composite weights with the double cumulative sum (renderer.py:
-// 300-307), the torch-ordered pdf normaliser and the sample_pdf merge walk
-// (renderer.py:84-119) -> TN new bins, sample-major [TN][N].
+// Proposal stage, part 2 (renderer.py:84-119 and 300-307), 64 rays per block.
+// Phase A, one thread per ray, in the reference's sequential order: composite
+// weights with the double cumulative sum, the torch-ordered pdf normaliser,
+// and cdf[i] = min(float(double cumsum of (w + 0.01) / sum), 1), written in
+// place over the ray's LDS row.  Phase B, 4 threads per ray: each takes a
+// contiguous quarter of the TN outputs, finds its first searchsorted(right)
+// position by binary search, and merge-walks its quarter -- the same cdf
+// values and the same interpolation as one walk over the whole ray, so the
+// indices and bins are identical, with a quarter of the dependent steps.
 template <int T, int TN, bool FIRST>
-__global__ void __launch_bounds__(64) k_prop_pdf(PropArgs a) {
-    // one wave = 64 rays; their ds rows are staged through LDS with coalesced
-    // loads from the sample-major wtmp (odd row stride: lane r at column k
-    // hits bank (r + k) % 64)
-    constexpr int SW = T + 1;
+__global__ void __launch_bounds__(256) k_prop_pdf(PropArgs a) {
+    constexpr int SW = T + 1;                 // T + 1 cdf entries per row (odd stride)
     __shared__ float sw[64 * SW];
-    const uint32_t lane = threadIdx.x, r0 = blockIdx.x * 64u;
-    const uint32_t nr = min(64u, a.N - r0);
-    if (lane < nr)
-        for (int k = 0; k < T; ++k) sw[lane * SW + k] = a.wtmp[(size_t)k * a.N + r0 + lane];
-    if (lane >= nr) return;
-    const uint32_t r = r0 + lane, N = a.N;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, part = tid >> 6;
+    const uint32_t r0 = xcd_chunk(blockIdx.x, (a.N + 63u) / 64u) * 64u, N = a.N;
+    if (r0 >= N) return;
+    const uint32_t nr = min(64u, N - r0);
     float* row = sw + lane * SW;
-    double cum = 0.0;
-    for (int k = 0; k < T; ++k) row[k] = composite_step(row[k], cum, k == T - 1);
+    if (part == 0 && lane < nr) {
+        // ds rows from the sample-major wtmp: coalesced across the wave
+        for (int k = 0; k < T; ++k) row[k] = a.wtmp[(size_t)k * N + r0 + lane];
+        double cum = 0.0;
+        for (int k = 0; k < T; ++k) row[k] = composite_step(row[k], cum, k == T - 1);
+        const float wsum = torch_row_sum(T, [&](int i) { return row[i] + 0.01f; });
+        double c = 0.0;
+        float wnext = row[0];
+        row[0] = 0.0f;
+        for (int i = 0; i < T; ++i) {
+            const float wi = wnext;
+            if (i + 1 < T) wnext = row[i + 1];
+            const float pdf = (wi + 0.01f) / wsum;
+            c += (double)pdf;
+            row[i + 1] = fminf((float)c, 1.0f);
+        }
+    }
+    __syncthreads();
+    if (lane >= nr) return;
+    const uint32_t r = r0 + lane;
     auto bin = [&](int i) -> float {
         if constexpr (FIRST) return a.bins0(i);
         else return a.bins_in[(size_t)i * N + r];
     };
-    const float wsum = torch_row_sum(T, [&](int i) { return row[i] + 0.01f; });
-    sample_pdf_walk(
-        T, TN, a.u, wsum, [&](int i) { return row[i]; }, bin,
-        [&](int j, float v, int) { a.bins_out[(size_t)j * N + r] = v; });
+    constexpr int QN = TN / 4;
+    const int j0 = (int)part * QN, j1 = part == 3 ? TN : j0 + QN;
+    // first index with cdf > u_j0 (cdf is nondecreasing, cdf[0] = 0 <= u)
+    const float u0 = a.u(j0);
+    int lo = 1, hi = T + 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (row[mid] <= u0) lo = mid + 1;
+        else hi = mid;
+    }
+    int i = lo;
+    for (int j = j0; j < j1; ++j) {
+        const float u = a.u(j);
+        while (i <= T && row[i] <= u) ++i;
+        const int below = i - 1, above = i <= T ? i : T;
+        const float g0 = row[below], g1 = row[above];
+        const float b0 = bin(below), b1 = bin(above);
+        float t = nan_to_num((u - g0) / (g1 - g0));
+        t = fminf(fmaxf(t, 0.0f), 1.0f);
+        a.bins_out[(size_t)j * N + r] = b0 + t * (b1 - b0);
+    }
 }
 
 struct Tables;
@@ -320,38 +368,57 @@ __device__ __forceinline__ floatx16 mfma3(uint4 ah, uint4 al, uint4 bh, uint4 bl
     return MFMA_BF16(Ah, Bh, c);
 }
 
-// Trilinear lookup of both channels of one L16C2 level whose descriptor
-// differs between the half-waves (lane-varying; no divergent branch): the
-// row of corner (x, y, z) is x + y*res + z*res^2 (dense) or
-// (x ^ y*P1 ^ z*P2) & (size-1) (hashed), built from per-axis terms.
-__device__ __forceinline__ void gather_level_c2(const float2* __restrict__ emb, const LevelDesc& d,
-                                                float ux, float uy, float uz, float& f0, float& f1) {
-    uint32_t cx, cy, cz;
-    float fx, fy, fz;
-    locate_axis(ux, d.res, cx, fx);
-    locate_axis(uy, d.res, cy, fy);
-    locate_axis(uz, d.res, cz, fz);
-    const uint32_t top = d.res - 1u;
-    const bool hashed = d.flags & kHashed;
-    const uint32_t my = hashed ? kPrime1 : d.res, mz = hashed ? kPrime2 : d.res * d.res;
-    const uint32_t mask = hashed ? d.size - 1u : 0xffffffffu;
-    const uint32_t X[2] = {cx, min(cx + 1u, top)};
-    const uint32_t Y[2] = {cy * my, min(cy + 1u, top) * my};
-    const uint32_t Z[2] = {cz * mz, min(cz + 1u, top) * mz};
-    const float2* base = emb + d.off;
-    f0 = 0.0f;
-    f1 = 0.0f;
+// Trilinear lookup of both channels of NL L16C2 levels whose descriptors
+// differ between the half-waves (lane-varying; no divergent branch): the row
+// of corner (x, y, z) is x + y*res + z*res^2 (dense) or (x ^ y*P1 ^ z*P2) &
+// (size-1) (hashed), built from per-axis terms.  All 8*NL corner loads are
+// issued before the first is consumed (one memory round trip per call; the
+// compiler otherwise waits for each level before issuing the next).
+template <int NL>
+__device__ __forceinline__ void gather_levels_c2(const float2* __restrict__ emb, const LevelDesc* d,
+                                                 float ux, float uy, float uz, float* f) {
+    uint32_t row[NL][8];
+    float fx[NL], fy[NL], fz[NL];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const float wx = (c & 1) ? fx : 1.0f - fx;
-        const float wy = (c & 2) ? fy : 1.0f - fy;
-        const float wz = (c & 4) ? fz : 1.0f - fz;
-        const uint32_t xs = X[c & 1], ys = Y[(c >> 1) & 1], zs = Z[c >> 2];
-        const uint32_t row = hashed ? ((xs ^ ys ^ zs) & mask) : (xs + ys + zs);
-        const float w = (wx * wy) * wz;
-        const float2 e = base[row];
-        f0 = __builtin_fmaf(w, e.x, f0);
-        f1 = __builtin_fmaf(w, e.y, f1);
+    for (int l = 0; l < NL; ++l) {
+        uint32_t cx, cy, cz;
+        locate_axis(ux, d[l].res, cx, fx[l]);
+        locate_axis(uy, d[l].res, cy, fy[l]);
+        locate_axis(uz, d[l].res, cz, fz[l]);
+        const uint32_t top = d[l].res - 1u;
+        const bool hashed = d[l].flags & kHashed;
+        const uint32_t my = hashed ? kPrime1 : d[l].res, mz = hashed ? kPrime2 : d[l].res * d[l].res;
+        const uint32_t mask = hashed ? d[l].size - 1u : 0xffffffffu;
+        const uint32_t X[2] = {cx, min(cx + 1u, top)};
+        const uint32_t Y[2] = {cy * my, min(cy + 1u, top) * my};
+        const uint32_t Z[2] = {cz * mz, min(cz + 1u, top) * mz};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t xs = X[c & 1], ys = Y[(c >> 1) & 1], zs = Z[c >> 2];
+            row[l][c] = (d[l].off + (hashed ? ((xs ^ ys ^ zs) & mask) : (xs + ys + zs))) << 3;
+        }
+    }
+    // 32-bit byte offsets from the uniform table base (saddr loads)
+    const char* base = reinterpret_cast<const char*>(emb);
+    float2 e[NL][8];
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) e[l][c] = *reinterpret_cast<const float2*>(base + row[l][c]);
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        float f0 = 0.0f, f1 = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const float wx = (c & 1) ? fx[l] : 1.0f - fx[l];
+            const float wy = (c & 2) ? fy[l] : 1.0f - fy[l];
+            const float wz = (c & 4) ? fz[l] : 1.0f - fz[l];
+            const float w = (wx * wy) * wz;
+            f0 = __builtin_fmaf(w, e[l][c].x, f0);
+            f1 = __builtin_fmaf(w, e[l][c].y, f1);
+        }
+        f[2 * l] = f0;
+        f[2 * l + 1] = f1;
     }
 }
 
@@ -359,20 +426,21 @@ __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const Leve
     return LevelDesc{hi ? q.off : p.off, hi ? q.size : p.size, hi ? q.res : p.res, hi ? q.flags : p.flags};
 }
 
-// One wave marches 32 (ray, segment) columns: with S segments per ray, lane
-// (j, h) owns segment j / R of ray j % R (R = 32 / S rays per wave), i.e. the
-// T/S samples seg*T/S .. (seg+1)*T/S - 1.  For k-block kb it gathers both
-// channels of levels 8kb + 4h .. 8kb + 4h + 3 -- exactly its B operand of the
-// first layer (input index 2*level + channel) -- so the hash grid feeds the
-// matrix cores with no data movement.  grid_mlp 32->64->64->16 runs on bf16x3
-// MFMAs, view_mlp 31->32->32->3 (once per ray) on fp32 MFMAs.  Compositing
-// runs in-lane with segment-local transmittance; compositing is associative
-// (C = C_0 + T_0 C_1 + T_0 T_1 C_2 ...), so the segments are combined by
-// shuffles at the end and the later segments' stored weights rescaled.  S > 1
-// only serves small N (one rank's share of a view), where S-times more waves
-// hide the gather latency.
+// One wave marches 32 (ray, slot) columns: with S slots per ray, lane (j, h)
+// owns slot j / R of ray j % R (R = 32 / S rays per wave), i.e. samples
+// slot, slot + S, slot + 2S, ...  For k-block kb it gathers both channels of
+// levels 8kb + 4h .. 8kb + 4h + 3 -- exactly its B operand of the first layer
+// (input index 2*level + channel) -- so the hash grid feeds the matrix cores
+// with no data movement.  grid_mlp 32->64->64->16 runs on bf16x3 MFMAs,
+// view_mlp 31->32->32->3 (once per ray) on fp32 MFMAs.  Compositing: each
+// step the S slots of a ray exchange their optical depths by shuffle and
+// every lane forms the ray's exclusive cumulative sum in sample order (the
+// reference's sequential double cumsum, exactly), so the stored weights are
+// final; per-slot partial sums of w, w*t and w*features are added at the end.
+// S > 1 only serves small N (one rank's share of a view): S-times more waves,
+// while a wave still gathers at adjacent samples of neighbouring rays.
 template <int T, int S>
-__global__ void __launch_bounds__(256) k_final(FinalArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_final(FinalArgs a) {
     static_assert(S == 1 || S == 2 || S == 4, "segments per ray");
     constexpr int R = 32 / S, TS = T / S;
     __shared__ uint4 Fh[kFSlots * 64], Fl[kFSlots * 64];
@@ -388,8 +456,9 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int hh = lane >> 5, jj = lane & 31;
-    const int seg = jj / R;
-    const uint32_t ray0 = blockIdx.x * (4u * R) + wave * (uint32_t)R;
+    const int seg = jj / R;                              // slot of this column
+    const uint32_t chunk = xcd_chunk(blockIdx.x, (a.N + 4u * R - 1u) / (4u * R));
+    const uint32_t ray0 = chunk * (4u * R) + wave * (uint32_t)R;
     if (ray0 >= a.N) return;                             // wave-uniform
     const uint32_t r = ray0 + (uint32_t)(jj % R);
     const bool live = r < a.N;
@@ -408,14 +477,15 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
     }
     const float sn = a.snf[rr], sf = a.snf[N + rr];
     const float b2 = 2.0f * a.bound;
-    const int k0 = seg * TS;
-    float rb_prev = real_bin(sn, sf, a.bins_in[(size_t)k0 * N + rr]);
-    double cum = 0.0, wsum = 0.0, depth = 0.0;
+    float rb_prev = real_bin(sn, sf, a.bins_in[(size_t)seg * N + rr]);
+    double cum = 0.0, wsum = 0.0, depth = 0.0;            // cum: optical depth before this step
     float fg[8];                                          // sum_k w_k * grid_mlp rows (acc layout)
 #pragma unroll
     for (int q = 0; q < 8; ++q) fg[q] = 0.0f;
 
-    for (int k = k0; k < k0 + TS; ++k) {
+    for (int i = 0; i < TS; ++i) {
+        const int k = i * S + seg;
+        if (S > 1 && i > 0) rb_prev = real_bin(sn, sf, a.bins_in[(size_t)k * N + rr]);
         const float rb_next = real_bin(sn, sf, a.bins_in[(size_t)(k + 1) * N + rr]);
         const float t = (rb_next + rb_prev) / 2.0f;
         float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
@@ -437,12 +507,10 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             float f[8];
+            LevelDesc dl[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const LevelDesc dl = select_level(G->lv[8 * kb + i], G->lv[8 * kb + 4 + i], hh != 0);
-                gather_level_c2(emb, dl, ux, uy, uz, f[2 * i], f[2 * i + 1]);
-                if (i & 1) __builtin_amdgcn_sched_barrier(0);   // <= 2 levels of gathers in flight
-            }
+            for (int i = 0; i < 4; ++i) dl[i] = select_level(G->lv[8 * kb + i], G->lv[8 * kb + 4 + i], hh != 0);
+            gather_levels_c2<4>(emb, dl, ux, uy, uz, f);
             uint4 bh, bl;
             split8(f, bh, bl);
             h1a = mfma3(FH[(kF1 + 2 * kb) * 64], FL[(kF1 + 2 * kb) * 64], bh, bl, h1a);
@@ -486,7 +554,17 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
         const float s_lo = o3[0];
         const float s_hi = __shfl_xor(s_lo, 32);
         const float sigma = expf(hh == 0 ? s_lo : s_hi);
-        const float w = composite_step((rb_next - rb_prev) * sigma, cum, k == T - 1);
+        // composite (renderer.py:300-307): w_k = alpha_k * exp(-sum_{j<k} ds_j),
+        // the sum in double and in sample order across the ray's S slots
+        const float ds = k == T - 1 ? INFINITY : (rb_next - rb_prev) * sigma;
+        double before = cum;
+#pragma unroll
+        for (int s2 = 0; s2 < S; ++s2) {
+            const float d2 = S > 1 ? __shfl(ds, (jj % R) + R * s2 + 32 * hh) : ds;
+            if (s2 < seg) before += (double)d2;
+            cum += (double)d2;
+        }
+        const float w = nan_to_num((1.0f - expf(-ds)) * expf(-(float)before));
         if (sample_writer) a.w_out[(size_t)k * N + r] = w;
         wsum += (double)w;
         depth += (double)(w * t);
@@ -495,33 +573,18 @@ __global__ void __launch_bounds__(256) k_final(FinalArgs a) {
         rb_prev = rb_next;
     }
 
-    if constexpr (S > 1) {
-        // combine the segments of each ray (lanes jj % R + R*s, same half h):
-        // segment s is attenuated by exp(-sum of the earlier segments' optical
-        // depth); lanes of segment 0 end up with the ray's totals
-        double pre = 0.0;                                  // optical depth before this segment
-#pragma unroll
-        for (int s2 = 0; s2 < S - 1; ++s2) {
-            const double c2 = __shfl(cum, (jj % R) + R * s2 + 32 * hh);
-            if (s2 < seg) pre += c2;
-        }
-        if (seg > 0 && sample_writer) {                  // rescale this segment's weights
-            const float tr = expf(-(float)pre);
-            for (int k = k0; k < k0 + TS; ++k) a.w_out[(size_t)k * N + r] *= tr;
-        }
-        double pw = 0.0, pd = 0.0, acc_pre = 0.0;
+    if constexpr (S > 1) {                               // add the slots' partial sums
+        double pw = 0.0, pd = 0.0;
         float pf[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) pf[q] = 0.0f;
 #pragma unroll
         for (int s2 = 0; s2 < S; ++s2) {
             const int src = (jj % R) + R * s2 + 32 * hh;
-            const float tr = expf(-(float)acc_pre);
-            pw += (double)tr * __shfl(wsum, src);
-            pd += (double)tr * __shfl(depth, src);
+            pw += __shfl(wsum, src);
+            pd += __shfl(depth, src);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) pf[q] += tr * __shfl(fg[q], src);
-            acc_pre += __shfl(cum, src);
+            for (int q = 0; q < 8; ++q) pf[q] += __shfl(fg[q], src);
         }
         wsum = pw;
         depth = pd;
@@ -592,28 +655,52 @@ struct SgridArgs {
     float* rows;         // [N, kRow]
 };
 
-// f_sam = sum_k w_k * s_grid(x_k): one thread per (ray, level); a wave holds
-// 64 neighbouring rays at one level, so corner rows are shared across lanes.
+// f_sam = sum_k w_k * s_grid(x_k).  A block is one level x 64 neighbouring
+// rays x 4 sample quarters: thread (q, ray) sums samples q*T/4 .. q*T/4 + T/4
+// - 1 (its next sample's position/weight prefetched behind the current
+// gather), and the quarters are added through LDS.  A wave is 64 rays at one
+// (level, sample), so corner rows are shared across lanes.
 template <int T>
 __global__ void __launch_bounds__(256) k_sgrid(SgridArgs a) {
-    const uint32_t r = blockIdx.x * 64u + (threadIdx.x & 63u);
-    const uint32_t level = blockIdx.y * 4u + (threadIdx.x >> 6);
-    if (r >= a.N) return;
-    const uint32_t N = a.N;
+    constexpr int TQ = T / 4;
+    __shared__ float part[3][8][64];
+    const uint32_t lane = threadIdx.x & 63u, q = threadIdx.x >> 6;
+    const uint32_t r = xcd_chunk(blockIdx.x, (a.N + 63u) / 64u) * 64u + lane;   // gridDim.x % 8 == 0
+    const uint32_t level = blockIdx.y;
+    const bool live = r < a.N;
+    const uint32_t N = a.N, rr = live ? r : N - 1;
     const LevelDesc lv = a.grid.lv[level];
     float acc[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) acc[c] = 0.0f;
-    for (int k = 0; k < T; ++k) {
-        const float ux = a.u_in[((size_t)k * 3 + 0) * N + r];
-        const float uy = a.u_in[((size_t)k * 3 + 1) * N + r];
-        const float uz = a.u_in[((size_t)k * 3 + 2) * N + r];
-        const float w = a.w_in[(size_t)k * N + r];
+    const int k0 = (int)q * TQ;
+    float ux = a.u_in[((size_t)k0 * 3 + 0) * N + rr];
+    float uy = a.u_in[((size_t)k0 * 3 + 1) * N + rr];
+    float uz = a.u_in[((size_t)k0 * 3 + 2) * N + rr];
+    float w = a.w_in[(size_t)k0 * N + rr];
+    for (int k = k0; k < k0 + TQ; ++k) {
+        const int kn = k + 1 < k0 + TQ ? k + 1 : k;          // prefetch (clamped)
+        const float nx = a.u_in[((size_t)kn * 3 + 0) * N + rr];
+        const float ny = a.u_in[((size_t)kn * 3 + 1) * N + rr];
+        const float nz = a.u_in[((size_t)kn * 3 + 2) * N + rr];
+        const float nw = a.w_in[(size_t)kn * N + rr];
         float f[8];
         lookup_level3<8>(a.grid.emb, lv, ux, uy, uz, f);
 #pragma unroll
         for (int c = 0; c < 8; ++c) acc[c] = acc[c] + w * f[c];
+        ux = nx;
+        uy = ny;
+        uz = nz;
+        w = nw;
     }
+    if (q > 0) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) part[q - 1][c][lane] = acc[c];
+    }
+    __syncthreads();
+    if (q > 0 || !live) return;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = ((acc[c] + part[0][c][lane]) + part[1][c][lane]) + part[2][c][lane];
     float4* dst = reinterpret_cast<float4*>(a.rows + (size_t)r * kRow + level * 8u);
     dst[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
     dst[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
@@ -813,8 +900,8 @@ int make_grid_desc(const samnerf_grid& g, uint32_t C, uint32_t L, GridDesc<16>& 
             if (hashed && (size & (size - 1u)))
                 return fail(SAMNERF_EINVAL, "render: %s level %u hashes into a non power-of-two table",
                             name, l);
-            if ((uint64_t)(off + size) * C >= (1ull << 32))
-                return fail(SAMNERF_EINVAL, "render: %s exceeds 2^32 elements", name);
+            if ((uint64_t)(off + size) * C * sizeof(float) > (1ull << 32))
+                return fail(SAMNERF_EINVAL, "render: %s exceeds 4 GiB (32-bit gather offsets)", name);
         } else {
             d.lv[l] = LevelDesc{0, 1, 1, 0};
         }
@@ -942,7 +1029,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.bins_out = w.bins1;
     mark_stage(0, s);
     k_prop_sigma<128, true><<<prop_sigma_blocks<128>(N), 256, 0, s>>>(pa);
-    k_prop_pdf<128, 65, true><<<div_up(N, 64), 64, 0, s>>>(pa);
+    k_prop_pdf<128, 65, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
 
     // stage 1: 64 samples -> 33 bins
     pa.grid = gp1;
@@ -953,7 +1040,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.bins_out = w.bins2;
     mark_stage(1, s);
     k_prop_sigma<64, false><<<prop_sigma_blocks<64>(N), 256, 0, s>>>(pa);
-    k_prop_pdf<64, 33, false><<<div_up(N, 64), 64, 0, s>>>(pa);
+    k_prop_pdf<64, 33, false><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
 
     // stage 2: 32 samples through the full network
     FinalArgs fa{};
@@ -980,9 +1067,9 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.rows = m->with_sam || feature_rows ? rows : nullptr;
     mark_stage(2, s);
     // segments per ray: enough waves to fill the resident slots (2 per SIMD)
-    if (N >= 65536u) k_final<32, 1><<<div_up(N, 128), 256, 0, s>>>(fa);
-    else if (N >= 32768u) k_final<32, 2><<<div_up(N, 64), 256, 0, s>>>(fa);
-    else k_final<32, 4><<<div_up(N, 32), 256, 0, s>>>(fa);
+    if (N >= 65536u) k_final<32, 1><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
+    else if (N >= 32768u) k_final<32, 2><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
+    else k_final<32, 4><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
 
     if (m->with_sam) {
         SgridArgs sa{};
@@ -992,7 +1079,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
         sa.w_in = w.w_f;
         sa.rows = rows;
         mark_stage(3, s);
-        k_sgrid<32><<<dim3(div_up(N, 64), 4), 256, 0, s>>>(sa);
+        k_sgrid<32><<<dim3(xcd_blocks(div_up(N, 64)), 16), 256, 0, s>>>(sa);
         if ((rc = check_launch("render"))) return rc;
         mark_stage(4, s);
         rc = sam_head_forward(m, rows, N, samvit, w.packed, s);

@@ -96,9 +96,31 @@ __device__ __forceinline__ void load_row(const float* __restrict__ p, float* out
     }
 }
 
+// Load C contiguous floats at a 32-bit byte offset from a uniform base: the
+// address is base (SGPRs) + zero-extended offset (one VGPR), i.e. the
+// global_load saddr form, with no per-lane 64-bit address arithmetic.  Only
+// for tables the host has checked to be < 4 GiB (make_grid_desc).
+template <int C>
+__device__ __forceinline__ void load_row_b(const char* __restrict__ base, uint32_t off, float* out) {
+    if constexpr (C == 2) {
+        const float2 v = *reinterpret_cast<const float2*>(base + off);
+        out[0] = v.x;
+        out[1] = v.y;
+    } else if constexpr (C == 8) {
+        const float4 a = *reinterpret_cast<const float4*>(base + off);
+        const float4 b = *reinterpret_cast<const float4*>(base + off + 16u);
+        out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
+        out[4] = b.x; out[5] = b.y; out[6] = b.z; out[7] = b.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < C; ++i) out[i] = *reinterpret_cast<const float*>(base + off + 4u * i);
+    }
+}
+
 // Trilinear lookup of one level (D = 3, linear interpolation, no
 // align_corners): the 8 corners in the reference's order (bit d <-> axis d,
-// gridencoder.cu:171-192), FMA accumulation into `acc`.
+// gridencoder.cu:171-192), FMA accumulation into `acc`.  Fused-path tables
+// only (32-bit byte offsets, see load_row_b).
 template <int C>
 __device__ __forceinline__ void lookup_level3(const float* __restrict__ emb, const LevelDesc& d,
                                               float ux, float uy, float uz, float* acc) {
@@ -109,7 +131,7 @@ __device__ __forceinline__ void lookup_level3(const float* __restrict__ emb, con
     locate_axis(uz, d.res, cz, fz);
     const uint32_t top = d.res - 1u;
     const uint32_t nx = min(cx + 1u, top), ny = min(cy + 1u, top), nz = min(cz + 1u, top);
-    const float* base = emb + d.off * (uint32_t)C;      // 32-bit element offsets
+    const char* base = reinterpret_cast<const char*>(emb);
 #pragma unroll
     for (int i = 0; i < C; ++i) acc[i] = 0.0f;
 #pragma unroll
@@ -121,7 +143,7 @@ __device__ __forceinline__ void lookup_level3(const float* __restrict__ emb, con
         const uint32_t row = dense_or_hash_row((c & 1) ? nx : cx, (c & 2) ? ny : cy,
                                                (c & 4) ? nz : cz, d);
         float e[C];
-        load_row<C>(base + row * (uint32_t)C, e);
+        load_row_b<C>(base, (d.off + row) * (uint32_t)(C * 4), e);
 #pragma unroll
         for (int i = 0; i < C; ++i) acc[i] = __builtin_fmaf(w, e[i], acc[i]);
     }

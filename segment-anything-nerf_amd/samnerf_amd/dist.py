@@ -116,3 +116,56 @@ def render_view_sharded(render_fn, ray_fn, H, W, keys=("image", "depth", "weight
     # bufs[c] = [world, n_c, C] (rank-major); image order is (rank, chunk, ray)
     full = torch.stack([b.view(world, n_c, C) for b in bufs], dim=1).reshape(world * chunks * n_c, C)
     return unpack_outputs(full, keys, widths)
+
+
+class ShardedViewPipeline:
+    """Strong-scaled rendering of a stream of views with the all-gather of
+    view i running behind the rendering of view i+1.
+
+        pipe = ShardedViewPipeline(render_fn, H, W)
+        for view in views:
+            pipe.submit(ray_fn_for(view))     # render this rank's band, start the gather
+            done = pipe.collect_ready()       # outputs of the previous view, or None
+        last = pipe.flush()
+
+    submit() only enqueues GPU work (kernels on the current stream, the
+    collective on RCCL's stream); collect_ready()/flush() make the current
+    stream wait for the oldest gather and return its outputs in image order.
+    One full-size launch per view and rank (no chunking): the communication
+    hides behind the next view's kernels instead of shrinking them."""
+
+    def __init__(self, render_fn, H, W, keys=("image", "depth", "weights_sum", "samvit"),
+                 group=None, depth=1):
+        self.render_fn, self.H, self.W = render_fn, H, W
+        self.keys, self.group, self.depth = keys, group, depth
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if H % self.world:
+            raise ValueError(f"H={H} must be divisible by the world size {self.world}")
+        self.band = H // self.world
+        self.inflight = []
+
+    def submit(self, ray_fn, render_fn=None):
+        ro, rd = ray_fn(self.rank * self.band, self.band)
+        out = (render_fn or self.render_fn)(ro, rd)
+        keys = [k for k in self.keys if k in out]
+        widths = [out[k].reshape(out[k].shape[0], -1).shape[1] for k in keys]
+        tile = pack_outputs(out, keys)
+        buf = tile.new_empty(self.world * tile.shape[0], tile.shape[1])
+        work = _all_gather(buf, tile, self.group, async_op=True)
+        self.inflight.append((work, buf, tile, keys, widths))
+
+    def _pop(self):
+        work, buf, _tile, keys, widths = self.inflight.pop(0)
+        work.wait()
+        return unpack_outputs(buf, keys, widths)          # rank-major bands = image order
+
+    def collect_ready(self):
+        """Outputs of the oldest view once more than `depth` views are in flight."""
+        return self._pop() if len(self.inflight) > self.depth else None
+
+    def flush(self):
+        outs = []
+        while self.inflight:
+            outs.append(self._pop())
+        return outs

@@ -41,6 +41,22 @@ def _worker(rank, world, port, n, q):
         view = render_view_sharded(_fake_render, ray_fn, H, W, chunks=4)
         ok = ok and all(torch.equal(view[k], ref[k][:H * W]) for k in ref)
         ok = ok and len(calls) == 4 and all(r == 2 for _, r in calls)
+        # the cross-view pipeline: 3 views (shifted inputs), one gather in flight
+        from samnerf_amd.dist import ShardedViewPipeline
+        pipe = ShardedViewPipeline(_fake_render, H, W)
+        got = []
+        for v in range(3):
+            def ray_fn_v(row0, rows, v=v):
+                return (o[row0 * W:(row0 + rows) * W] + v, d[row0 * W:(row0 + rows) * W])
+            pipe.submit(ray_fn_v)
+            r_ = pipe.collect_ready()
+            if r_ is not None:
+                got.append(r_)
+        got += pipe.flush()
+        ok = ok and len(got) == 3
+        for v, g in enumerate(got):
+            refv = _fake_render(o[:H * W] + v, d[:H * W])
+            ok = ok and all(torch.equal(g[k], refv[k]) for k in refv)
         q.put((rank, ok, {k: tuple(v.shape) for k, v in out.items()}))
     finally:
         dist.destroy_process_group()

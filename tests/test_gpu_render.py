@@ -204,11 +204,12 @@ def test_sam_head_bf16x3_matches_exact_fp32(hip_lib, cuda):
 
 
 def test_ray_segment_paths_agree(hip_lib, cuda):
-    """k_final splits each ray into S = 1, 2 or 4 sample segments by N (more
-    waves for one rank's small share of a view) and recombines them
-    associatively: the same rays rendered at N >= 65536 (S = 1), 32768 <= N
-    < 65536 (S = 2) and N < 32768 (S = 4) must agree to fp32 rounding, and the
-    per-sample weights handed to the s_grid gather must too (f_sam rows)."""
+    """k_final spreads each ray's samples over S = 1, 2 or 4 interleaved slots
+    by N (more waves for one rank's small share of a view), exchanging optical
+    depths by shuffle: the same rays rendered at N >= 65536 (S = 1), 32768 <=
+    N < 65536 (S = 2) and N < 32768 (S = 4) must agree to fp32 rounding, and
+    the per-sample weights handed to the s_grid gather must too (f_sam
+    rows)."""
     from samnerf_amd import ops
     from samnerf_amd.fused import FusedRenderer, ROW
     spec = synth.ModelSpec(with_sam=True)
