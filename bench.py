@@ -92,8 +92,10 @@ def build_net(with_sam, device):
     return net.to(device).eval(), spec, params
 
 
-def cpu_baseline(spec, params, pose, intr, H, W, n_rays):
-    """Time the CPU oracle on the first n_rays rays of the same view."""
+def cpu_baseline(spec, params, pose, intr, H, W, n_rays, gpu_out=None):
+    """Time the CPU oracle on n_rays rays spread over the same view; with the
+    GPU outputs of that view, also return PSNR / max error of the GPU render
+    against it (the metric's "PSNR vs ref"; psnr formula of utils.py:347-357)."""
     from oracle import renderer as orc
     # the box exposes every host CPU but grants this job a share of them
     # (OMP_NUM_THREADS, 16 per GPU); use the share, not the machine
@@ -104,12 +106,25 @@ def cpu_baseline(spec, params, pose, intr, H, W, n_rays):
     model = orc.OracleNeRF(spec, params)
     model.run(ro[idx[:64]], rd[idx[:64]], return_feats=1)      # warm-up
     t0 = time.perf_counter()
-    model.render(ro[idx], rd[idx], return_feats=1)
+    ref = model.render(ro[idx], rd[idx], return_feats=1)
     dt = time.perf_counter() - t0
-    return {"value": n_rays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
-            "sample": f"{n_rays} rays of the {H}x{W} view (same weights, chunks of 16384 as renderer.py:195); torch-CPU "
-                      f"restatement of nerf/renderer.py+network.py, encoders in C "
-                      f"(OpenMP over points); {dt:.1f} s"}
+    res = {"value": n_rays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
+           "sample": f"{n_rays} rays of the {H}x{W} view (same weights, chunks of 16384 as renderer.py:195); torch-CPU "
+                     f"restatement of nerf/renderer.py+network.py, encoders in C "
+                     f"(OpenMP over points); {dt:.1f} s"}
+    parity = None
+    if gpu_out is not None:
+        g = {k: v.detach().float().cpu() for k, v in gpu_out.items()}
+        img_g, img_r = g["image"][idx], ref["image"].reshape(-1, 3)
+        mse = float(((img_g - img_r) ** 2).mean())
+        parity = {"rays": n_rays, "weights": "the bench's default-init weights (see tests/ for parity weights)",
+                  "psnr_image_db": float("inf") if mse == 0 else -10.0 * float(np.log10(mse)),
+                  "max_abs_image": float((img_g - img_r).abs().max()),
+                  "max_abs_depth_rel": float(((g["depth"][idx] - ref["depth"].reshape(-1)).abs()
+                                              / ref["depth"].reshape(-1).abs().clamp_min(1.0)).max())}
+        if "samvit" in g and "samvit" in ref:
+            parity["max_abs_samvit"] = float((g["samvit"][idx] - ref["samvit"].reshape(n_rays, -1)).abs().max())
+    return res, parity
 
 
 def main():
@@ -170,8 +185,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    last = None
     for i in range(args.steps):
-        step([raw for _, raw in sets[i]])
+        last = step([raw for _, raw in sets[i]])
     if pipe is not None:
         pipe.flush()                         # the last view's gather is inside the timed region
     torch.cuda.synchronize()
@@ -222,7 +238,8 @@ def main():
             "stage_ms": stage_avg,
         }
         if world == 1 and args.cpu_rays > 0:
-            rec["cpu_baseline"] = cpu_baseline(spec, params, pose, intr, H, W, args.cpu_rays)
+            rec["cpu_baseline"], rec["parity_vs_ref"] = cpu_baseline(
+                spec, params, pose, intr, H, W, args.cpu_rays, gpu_out=last)
         else:
             rec["cpu_baseline"] = None
         print(json.dumps(rec), flush=True)
