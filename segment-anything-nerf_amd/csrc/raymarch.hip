@@ -21,6 +21,7 @@
 // proposal gathers run one thread per sample (enough waves to hide gather
 // latency even at the 32K rays of one rank of an 8-GPU view).
 #include <algorithm>
+#include <cmath>
 #include <type_traits>
 
 #include "raymarch_device.h"
@@ -71,6 +72,27 @@ __device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t n) {
     return (b & 7u) * xcd_per(n) + (b >> 3);
 }
 
+// Grid-space coordinate u = (x + bound) / (2 bound) (grid.py:156) with the
+// reference's rounding.  When 2*bound is a power of two the host passes its
+// exact reciprocal (inv_b2 != 0) and the division becomes a multiplication
+// with the identical result; otherwise it is an IEEE division.
+struct GridScale {
+    float bound, b2, inv_b2;
+    __device__ __forceinline__ float operator()(float x) const {
+        return inv_b2 != 0.0f ? (x + bound) * inv_b2 : (x + bound) / b2;
+    }
+};
+
+GridScale make_grid_scale(float bound) {
+    GridScale g;
+    g.bound = bound;
+    g.b2 = 2.0f * bound;
+    int e = 0;
+    const float m = std::frexp(g.b2, &e);                 // b2 = m * 2^e, m in [0.5, 1)
+    g.inv_b2 = (m == 0.5f && std::isfinite(g.b2)) ? std::ldexp(1.0f, 1 - e) : 0.0f;
+    return g;
+}
+
 // MLP layer y = W x (torch layout W[out][in]), fma chain in input order.
 template <int OUT, int IN, bool RELU>
 __device__ __forceinline__ void dense(const float* __restrict__ W, const float* x, float* y) {
@@ -101,7 +123,8 @@ struct PropArgs {
     const float* cnf;
     uint32_t N, n_cnf;
     float aabb[6];
-    float min_near, bound;
+    float min_near;
+    GridScale gs;
     GridDesc<16> grid;
     const float* W0;       // [16, 10]
     const float* W1;       // [1, 16]
@@ -140,43 +163,50 @@ __global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
         o[c] = a.rays_o[(size_t)r * 3 + c];
         d[c] = a.rays_d[(size_t)r * 3 + c];
     }
-    float sn, sf, b0, b1;
+    const float sn = a.snf[r], sf = a.snf[N + r];           // k_snf (stage 0) / stage 0 (stage 1)
+    float b0, b1;
     if constexpr (FIRST) {
-        float near, far;
-        near_far_aabb(o, d, a.aabb, a.min_near, near, far);
-        if (a.cnf) {  // renderer.py:234-236
-            const uint32_t q = a.n_cnf == 1 ? 0u : r;
-            const float cn = a.cnf[q * 2], cf = a.cnf[q * 2 + 1];
-            near = (isnan(near) || isnan(cn)) ? NAN : fmaxf(near, cn);
-            far = (isnan(far) || isnan(cf)) ? NAN : fminf(far, cf);
-        }
-        sn = spacing(near);
-        sf = spacing(far);
         b0 = a.bins0(k);
         b1 = a.bins0(k + 1);
     } else {
-        sn = a.snf[r];
-        sf = a.snf[N + r];
         b0 = a.bins_in[(size_t)k * N + r];
         b1 = a.bins_in[(size_t)(k + 1) * N + r];
     }
-    const float b2 = 2.0f * a.bound;
     const float rb_prev = real_bin(sn, sf, b0), rb_next = real_bin(sn, sf, b1);
     const float t = (rb_next + rb_prev) / 2.0f;
     float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
     contract3(x, y, z);
     float feat[10];
-    grid_features<5, 2>(a.grid, (x + a.bound) / b2, (y + a.bound) / b2, (z + a.bound) / b2, feat);
+    grid_features<5, 2>(a.grid, a.gs(x), a.gs(y), a.gs(z), feat);
     float h[16], sv;
     dense<16, 10, true>(a.W0, feat, h);
     dense<1, 16, false>(a.W1, h, &sv);
+    // the only store, after the weight reads: an earlier store could alias
+    // W0/W1 and would demote the uniform weight reads to per-lane vector loads
     a.wtmp[(size_t)k * N + r] = (rb_next - rb_prev) * expf(sv);          // trunc_exp forward
-    // stores last: an earlier store could alias W0/W1 and would force the
-    // uniform weight reads from scalar to per-lane vector loads
-    if (FIRST && k == 0) {
-        a.snf[r] = sn;
-        a.snf[N + r] = sf;
+}
+
+// Stage 0 ray setup, one thread per ray: near/far from the AABB slab test
+// (renderer.py:122-139, 229-236) and their spacing (renderer.py:250-253).
+__global__ void __launch_bounds__(256) k_snf(PropArgs a) {
+    const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+    if (r >= a.N) return;
+    float o[3], d[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        o[c] = a.rays_o[(size_t)r * 3 + c];
+        d[c] = a.rays_d[(size_t)r * 3 + c];
     }
+    float near, far;
+    near_far_aabb(o, d, a.aabb, a.min_near, near, far);
+    if (a.cnf) {  // renderer.py:234-236
+        const uint32_t q = a.n_cnf == 1 ? 0u : r;
+        const float cn = a.cnf[q * 2], cf = a.cnf[q * 2 + 1];
+        near = (isnan(near) || isnan(cn)) ? NAN : fmaxf(near, cn);
+        far = (isnan(far) || isnan(cf)) ? NAN : fminf(far, cf);
+    }
+    a.snf[r] = spacing(near);
+    a.snf[a.N + r] = spacing(far);
 }
 
 // Proposal stage, part 2 (renderer.py:84-119 and 300-307), 64 rays per block.
@@ -249,7 +279,8 @@ struct FinalArgs {
     const float* rays_o;
     const float* rays_d;
     uint32_t N;
-    float bound, bg;
+    GridScale gs;
+    float bg;
     const Tables* tab;
     const float* grid_emb;  // == tab->grid.emb, as a kernel argument so gathers are global_load (not flat)
     const float* G0;   // grid_mlp [64,32]
@@ -476,7 +507,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         d[c] = a.rays_d[(size_t)rr * 3 + c];
     }
     const float sn = a.snf[rr], sf = a.snf[N + rr];
-    const float b2 = 2.0f * a.bound;
     float rb_prev = real_bin(sn, sf, a.bins_in[(size_t)seg * N + rr]);
     double cum = 0.0, wsum = 0.0, depth = 0.0;            // cum: optical depth before this step
     float fg[8];                                          // sum_k w_k * grid_mlp rows (acc layout)
@@ -490,7 +520,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         const float t = (rb_next + rb_prev) / 2.0f;
         float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
         contract3(x, y, z);
-        const float ux = (x + a.bound) / b2, uy = (y + a.bound) / b2, uz = (z + a.bound) / b2;
+        const float ux = a.gs(x), uy = a.gs(y), uz = a.gs(z);
         if (sample_writer) {
             a.u_out[((size_t)k * 3 + 0) * N + r] = ux;
             a.u_out[((size_t)k * 3 + 1) * N + r] = uy;
@@ -1015,7 +1045,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.n_cnf = n_cnf;
     for (int i = 0; i < 6; ++i) pa.aabb[i] = m->aabb[i];
     pa.min_near = m->min_near;
-    pa.bound = m->grid_bound;
+    pa.gs = make_grid_scale(m->grid_bound);
     pa.snf = w.snf;
     pa.wtmp = w.wtmp;
 
@@ -1028,6 +1058,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.bins_in = nullptr;
     pa.bins_out = w.bins1;
     mark_stage(0, s);
+    k_snf<<<div_up(N, 256), 256, 0, s>>>(pa);
     k_prop_sigma<128, true><<<prop_sigma_blocks<128>(N), 256, 0, s>>>(pa);
     k_prop_pdf<128, 65, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
 
@@ -1047,7 +1078,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.rays_o = rays_o;
     fa.rays_d = rays_d;
     fa.N = N;
-    fa.bound = m->grid_bound;
+    fa.gs = make_grid_scale(m->grid_bound);
     fa.bg = bg_color;
     fa.tab = w.tables;
     fa.grid_emb = gg.emb;
