@@ -7,10 +7,11 @@
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC EA requests).  Per
 MI355X_MICROARCH.md (HBM section) FETCH_SIZE reads 1/2 of the bytes of a WIDE
-(16 B/lane) coalesced stream; the gathers here are 4-8 B per lane, a width the
-guide lists as uncalibrated, so the raw (uncorrected) value is reported and
-`fetch_x2` gives the corrected upper bound.  Passes are separate runs
-(FETCH_SIZE needs 3 TCC slots, WRITE_SIZE 2).
+(16 B/lane) coalesced stream and WRITE_SIZE is exact for 16-B stores; the
+gathers here are 8-32 B per lane, a width the guide lists as uncalibrated.
+`hbm_bytes` applies the guide's correction (2 * FETCH + WRITE); the raw fetch
+is kept beside it.  Passes are separate runs (FETCH_SIZE needs 3 TCC slots,
+WRITE_SIZE 2).
 usage: python tools/summarize_prof.py --tag r1
 """
 import argparse
@@ -24,8 +25,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out")
 PROF = os.path.join(REPO, "profiles")
 
-STAGE_OF = {"k_prop<128": "prop0", "k_prop<64": "prop1", "k_final": "final",
-            "k_sgrid<": "s_grid", "k_sam_head": "sam_head", "k_pack": "sam_pack",
+STAGE_OF = {"k_snf": "prop0", "k_prop_sigma<128": "prop0", "k_prop_pdf<128": "prop0",
+            "k_prop_sigma<64": "prop1", "k_prop_pdf<64": "prop1", "k_final": "final",
+            "k_sgrid<": "s_grid", "k_sam_head": "sam_head", "k_pack": "sam_head",
             "k_get_rays": "get_rays", "k_put_tables": "tables"}
 
 
@@ -60,10 +62,17 @@ def main():
         f, w = fetch.get(k, 0.0) * 1024, write.get(k, 0.0) * 1024
         rows.append({"kernel": k[:90], "stage": s or "", "fetch_bytes": int(f),
                      "write_bytes": int(w), "fetch_x2_bytes": int(2 * f)})
-        if s:
-            traffic[s] = {"hbm_bytes": int(f + w), "fetch_bytes": int(f), "write_bytes": int(w),
-                          "fetch_x2_bytes": int(2 * f),
-                          "note": "per launch; FETCH_SIZE uncorrected (gather width uncalibrated)"}
+        if s:                                   # a stage may be several kernels: sum them
+            t = traffic.setdefault(s, {"hbm_bytes": 0, "fetch_bytes": 0, "write_bytes": 0,
+                                       "fetch_x2_bytes": 0, "kernels": [],
+                                       "note": "per launch; hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE "
+                                               "(MI355X_MICROARCH.md: FETCH_SIZE is half the bytes of "
+                                               "16-B/lane streams; 8-B gathers uncalibrated)"})
+            t["hbm_bytes"] += int(2 * f + w)                 # guide-corrected (see header)
+            t["fetch_bytes"] += int(f)
+            t["write_bytes"] += int(w)
+            t["fetch_x2_bytes"] += int(2 * f)
+            t["kernels"].append(k[:60])
     with open(os.path.join(PROF, f"{a.tag}_pmc.csv"), "w", newline="") as fh:
         w = csv.DictWriter(fh, fieldnames=list(rows[0]))
         w.writeheader()
