@@ -64,6 +64,9 @@ def parse():
                     help="N > 1: 0 = one launch per view with its all-gather pipelined behind "
                          "the next view's rendering; k > 0 = k row chunks per view, each "
                          "chunk's all-gather behind the next chunk")
+    ap.add_argument("--mode", choices=["render", "train"], default="render",
+                    help="render: cfg 3 view throughput (the headline metric); train: cfg 5 "
+                         "SAM-feature distillation step (4096 rays, forward + backward + Adam)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -127,8 +130,62 @@ def cpu_baseline(spec, params, pose, intr, H, W, n_rays, gpu_out=None):
     return res, parity
 
 
+def train_main(args, dev):
+    """BASELINE config 5: one step = fused forward of 4096 rays
+    (64x64, fovy 60) with grad, MSE vs a N(0,1) [1,256,64,64] target (seed 1)
+    after the reference's bilinear resize, backward (HIP s_grid scatter +
+    torch head), Adam(lr 1e-2, eps 1e-15) over get_params-style groups with
+    the RGB parameters frozen (main.py:255-262, 296; utils.py:1072-1106)."""
+    import torch.nn.functional as F
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer, render_sam_train
+    from oracle import synth
+    net, spec, params = build_net(True, dev)
+    net.train()
+    for k, p in net.named_parameters():
+        p.requires_grad = k.startswith("s_grid") or k.startswith("samvit_mlp")
+    opt = torch.optim.Adam([p for p in net.parameters()], lr=1e-2, eps=1e-15)
+    renderer = FusedRenderer(net)
+    h = w = 64
+    pose, intr = synth.gui_camera(w, h)
+    ro, rd = ops.get_rays(pose, intr, h, w, device=dev)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    gt = torch.randn(1, 256, 64, 64, generator=g).to(dev)
+
+    def step():
+        out = render_sam_train(renderer, ro, rd)
+        pred = out["samvit"].reshape(1, h, w, 256).permute(0, 3, 1, 2).contiguous()
+        pred = F.interpolate(pred, gt.shape[2:], mode="bilinear")
+        loss = F.mse_loss(pred, gt)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    rec = {"metric": "cfg5 SAM distillation train steps/s (4096 rays, fwd+bwd+Adam)",
+           "value": args.steps / dt, "unit": "steps/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True,
+           "rays_per_s": 4096 * args.steps / dt, "final_loss": float(loss),
+           "dtype": "fp32 (SAM head bf16x3 in the fused forward; head backward torch fp32)",
+           "data": "synthetic (default-init weights, N(0,1) target)",
+           "config": {"workload": "cfg5: 64x64 rays, with_sam, RGB frozen", "optimizer": "Adam lr 1e-2 eps 1e-15"},
+           "vs_baseline": None}
+    print(json.dumps(rec), flush=True)
+
+
 def main():
     args = parse()
+    if args.mode == "train":
+        torch.cuda.set_device(0)
+        return train_main(args, torch.device("cuda", 0))
     rank, world, dev = setup_dist(args)
     from samnerf_amd import ops
     from samnerf_amd._lib import lib

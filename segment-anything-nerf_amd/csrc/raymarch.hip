@@ -745,17 +745,19 @@ k_sgrid_backward(uint32_t N, GridDesc<16> g, const float* __restrict__ u_in,
                  const float* __restrict__ w_in, const float* __restrict__ grad, uint32_t gstride,
                  float* __restrict__ gemb) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t r = (uint32_t)(t >> 3), ch = (uint32_t)(t & 7u);
+    const uint32_t r = (uint32_t)(t >> 3), ch = (uint32_t)(t & 7u), lane = threadIdx.x & 63u;
     const uint32_t level = blockIdx.y;
-    if (r >= N) return;
+    if (((t & ~(uint64_t)63) >> 3) >= N) return;          // whole wave past the end
+    const bool live = r < N;                                // lanes stay for the shuffles
+    const uint32_t rr = live ? r : N - 1;
     const LevelDesc d = g.lv[level];
-    const float gv = grad[(size_t)r * gstride + level * 8u + ch];
+    const float gv = live ? grad[(size_t)rr * gstride + level * 8u + ch] : 0.0f;
     float* base = gemb + (size_t)d.off * 8u + ch;
     for (int k = 0; k < T; ++k) {
-        const float ux = u_in[((size_t)k * 3 + 0) * N + r];
-        const float uy = u_in[((size_t)k * 3 + 1) * N + r];
-        const float uz = u_in[((size_t)k * 3 + 2) * N + r];
-        const float wg = w_in[(size_t)k * N + r] * gv;
+        const float ux = u_in[((size_t)k * 3 + 0) * N + rr];
+        const float uy = u_in[((size_t)k * 3 + 1) * N + rr];
+        const float uz = u_in[((size_t)k * 3 + 2) * N + rr];
+        const float wg = w_in[(size_t)k * N + rr] * gv;
         uint32_t cx, cy, cz;
         float fx, fy, fz;
         locate_axis(ux, d.res, cx, fx);
@@ -770,7 +772,23 @@ k_sgrid_backward(uint32_t N, GridDesc<16> g, const float* __restrict__ u_in,
             const float wz = (c & 4) ? fz : 1.0f - fz;
             const uint32_t row = dense_or_hash_row((c & 1) ? nx : cx, (c & 2) ? ny : cy,
                                                    (c & 4) ? nz : cz, d);
-            atomicAdd(base + (size_t)row * 8u, ((wx * wy) * wz) * wg);
+            float val = ((wx * wy) * wz) * wg;
+            // The wave's 8 rays (neighbouring pixels) often hit the same corner
+            // row: merge equal rows over a 3-level butterfly so one lane per
+            // row and channel issues the atomic (the atomics run at the memory
+            // side, so fewer and fuller requests are what pays).
+            bool alive = live;
+#pragma unroll
+            for (int sd = 8; sd < 64; sd <<= 1) {
+                const uint32_t orow = __shfl_xor(row, sd);
+                const float oval = __shfl_xor(val, sd);
+                const int oalive = __shfl_xor((int)alive, sd);
+                if (alive && oalive && orow == row) {
+                    if (lane & sd) alive = false;
+                    else val += oval;
+                }
+            }
+            if (alive) atomicAdd(base + (size_t)row * 8u, val);
         }
     }
 }
