@@ -210,7 +210,10 @@ k_grid_forward(const float* __restrict__ inputs, const float* __restrict__ emb,
 
 // --------------------------------------------------------------- backward --
 // One thread per (point, level, channel): lanes c = 0..C-1 of a point update
-// the C contiguous floats of the same corner row together.
+// the C contiguous floats of the same corner row together, and equal rows of
+// the wave's other points are merged before the atomic (fewer memory-side
+// requests; the sum is reassociated, within the backward's float-atomic
+// tolerance).
 template <uint32_t D, uint32_t C>
 __global__ void __launch_bounds__(256)
 k_grid_backward(const float* __restrict__ grad, const float* __restrict__ inputs,
@@ -219,24 +222,41 @@ k_grid_backward(const float* __restrict__ grad, const float* __restrict__ inputs
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t level = blockIdx.y;
     const uint32_t b = (uint32_t)(t / C), ch = (uint32_t)(t % C);
-    if (b >= B) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    if ((t & ~(uint64_t)63) / C >= B) return;              // whole wave past the end
+    const uint32_t bb = b < B ? b : B - 1;                  // lanes stay for the shuffles
     float x[D];
 #pragma unroll
-    for (uint32_t d = 0; d < D; ++d) x[d] = inputs[(size_t)b * D + d];
-    if (outside<D>(x)) return;
+    for (uint32_t d = 0; d < D; ++d) x[d] = inputs[(size_t)bb * D + d];
+    const bool live = b < B && !outside<D>(x);
     const uint32_t base = (uint32_t)offsets[level];
     const uint32_t size = (uint32_t)offsets[level + 1] - base;
     const uint32_t res = rt.res[level];
     float frac[D], dfrac[D];
     uint32_t cell[D], cc[D];
     place<D>(x, res, align_corners, interp, frac, dfrac, cell);
-    const float g = grad[((size_t)level * B + b) * C + ch];
+    const float g = live ? grad[((size_t)level * B + bb) * C + ch] : 0.0f;
     float* gtab = grad_emb + (size_t)base * C + ch;
 #pragma unroll
     for (uint32_t c = 0; c < (1u << D); ++c) {
         const float w = corner_weight<D>(c, res, frac, cell, cc);
         const uint32_t row = grid_row<D>(gridtype, size, res, cc);
-        atomicAdd(gtab + (size_t)row * C, w * g);
+        float val = w * g;
+        // neighbouring points of a wave often hit the same corner row: merge
+        // equal rows (same channel = lanes C apart) over a butterfly so one
+        // lane per row issues the memory-side atomic
+        bool alive = live;
+#pragma unroll
+        for (uint32_t sd = C; sd < 64u; sd <<= 1) {
+            const uint32_t orow = __shfl_xor(row, (int)sd);
+            const float oval = __shfl_xor(val, (int)sd);
+            const int oalive = __shfl_xor((int)alive, (int)sd);
+            if (alive && oalive && orow == row) {
+                if (lane & sd) alive = false;
+                else val += oval;
+            }
+        }
+        if (alive) atomicAdd(gtab + (size_t)row * C, val);
     }
 }
 
