@@ -135,6 +135,10 @@ def default_opt(with_sam=True, **kw):
     import types
     o = dict(bound=128.0, contract=True, min_near=0.2, density_thresh=10, with_sam=with_sam,
              sum_after_mlp=False, sam_use_view_direction=True, with_mask=False,
-             num_steps=[128, 64, 32], background="last_sample", max_ray_batch=4096 * 4, fp16=False)
+             num_steps=[128, 64, 32], background="last_sample", max_ray_batch=4096 * 4, fp16=False,
+             # training (main.py:75-110, 226)
+             lr=1e-2, num_rays=4096, adaptive_num_rays=True, num_points=2 ** 18,
+             lambda_entropy=0.0, lambda_tv=0.0, lambda_wd=0.0, lambda_proposal=1.0,
+             lambda_distort=0.02)
     o.update(kw)
     return types.SimpleNamespace(**o)

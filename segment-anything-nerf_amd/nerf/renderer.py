@@ -59,6 +59,51 @@ def sample_pdf(bins, weights, T, perturb=False):
     return b0 + t * (b1 - b0)
 
 
+def eff_distloss(w, m, interval):
+    """Distortion loss sum_ij w_i w_j |m_i - m_j| + 1/3 sum_i w_i^2 s_i, mean over
+    rays, in its O(T) cumulative-sum form.  Restates the third-party
+    `torch_efficient_distloss.eff_distloss` the reference calls
+    (renderer.py:14, 25; requirements.txt:22, un-pinned, absent here): parity
+    unpinned, tests/test_losses.py checks it against the double sum."""
+    loss_uni = (1 / 3) * (interval * w.pow(2)).sum(dim=-1).mean()
+    wm = w * m
+    w_cumsum = w.cumsum(dim=-1)
+    wm_cumsum = wm.cumsum(dim=-1)
+    loss_bi_0 = wm[..., 1:] * w_cumsum[..., :-1]
+    loss_bi_1 = w[..., 1:] * wm_cumsum[..., :-1]
+    loss_bi = 2 * (loss_bi_0 - loss_bi_1).sum(dim=-1).mean()
+    return loss_bi + loss_uni
+
+
+def distort_loss(bins, weights):
+    """renderer.py:17-27: bins [N, T+1], weights [N, T]."""
+    intervals = bins[..., 1:] - bins[..., :-1]
+    mid_points = bins[..., :-1] + intervals / 2
+    return eff_distloss(weights, mid_points, intervals)
+
+
+def proposal_loss(all_bins, all_weights):
+    """renderer.py:30-57 (mip-NeRF 360 inter-level loss): the final stage's
+    (detached) weights must be bounded by each proposal stage's."""
+    def loss_interlevel(t0, w0, t1, w1):
+        cw1 = torch.cat([torch.zeros_like(w1[..., :1]), torch.cumsum(w1, dim=-1)], dim=-1)
+        inds_lo = (torch.searchsorted(t1[..., :-1].contiguous(), t0[..., :-1].contiguous(),
+                                      right=True) - 1).clamp(0, w1.shape[-1] - 1)
+        inds_hi = torch.searchsorted(t1[..., 1:].contiguous(), t0[..., 1:].contiguous(),
+                                     right=True).clamp(0, w1.shape[-1] - 1)
+        cw1_lo = torch.take_along_dim(cw1[..., :-1], inds_lo, dim=-1)
+        cw1_hi = torch.take_along_dim(cw1[..., 1:], inds_hi, dim=-1)
+        w = cw1_hi - cw1_lo
+        return (w0 - w).clamp(min=0) ** 2 / (w0 + 1e-8)
+
+    bins_ref = all_bins[-1].detach()
+    weights_ref = all_weights[-1].detach()
+    loss = 0
+    for bins, weights in zip(all_bins[:-1], all_weights[:-1]):
+        loss += loss_interlevel(bins_ref, weights_ref, bins, weights).mean()
+    return loss
+
+
 def _spacing(x):
     return torch.where(x < 1, x / 2, 1 - 1 / (2 * x))
 
@@ -166,6 +211,7 @@ class NeRFRenderer(nn.Module):
         results = {}
         s_n, s_f = _spacing(nears), _spacing(fars)
         bins = weights = None
+        all_bins, all_weights = [], []
         for it, T in enumerate(opt.num_steps):
             if it == 0:
                 bins = torch.linspace(0, 1, T + 1, device=dev).unsqueeze(0).expand(N, -1)
@@ -196,10 +242,20 @@ class NeRFRenderer(nn.Module):
             trans = torch.exp(-torch.cat([torch.zeros_like(trans[..., :1]), trans], dim=-1))
             weights = alphas * trans
             weights.nan_to_num_(0)
+            if self.training:
+                all_bins.append(bins)
+                all_weights.append(weights)
         weights_sum = weights.sum(-1)
         depth = (weights * rays_t).sum(-1)
         f_image = (weights.unsqueeze(-1) * colors).sum(-2)
         image = torch.sigmoid(self.view_mlp(f_image))
+        if self.training and not opt.with_sam:              # renderer.py:348-356
+            results["num_points"] = xyzs.shape[0] * xyzs.shape[1]
+            results["weights"] = weights
+            if getattr(opt, "lambda_proposal", 0) > 0 and update_proposal:
+                results["proposal_loss"] = proposal_loss(all_bins, all_weights)
+            if getattr(opt, "lambda_distort", 0) > 0:
+                results["distort_loss"] = distort_loss(bins, weights)
         image = image + (1 - weights_sum).unsqueeze(-1) * bg_color
         results.update(weights_sum=weights_sum, depth=depth, image=image)
         if opt.with_sam:

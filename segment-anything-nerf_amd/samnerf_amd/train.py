@@ -1,0 +1,58 @@
+"""Training steps of the reference's Trainer on this package's kernels.
+
+`rgb_train_step` is Trainer.train_step's RGB branch (nerf/utils.py:897-937):
+render with perturbed sampling through the reference's op sequence with the
+HIP drop-in encoders (forward and backward kernels: grid, SH), MSE + the
+proposal (mip-NeRF 360 inter-level) and distortion losses, optional entropy
+regulariser, and the adaptive ray-count update.  `sam_train_step` is its
+SAM-distillation branch (utils.py:1072-1106) on the fused forward and the HIP
+s_grid scatter (BASELINE config 5).  Optimisation (Adam over
+NeRFNetwork.get_params-style groups, main.py:296) is the caller's.
+"""
+import torch
+import torch.nn.functional as F
+
+
+def update_proposal_now(global_step, with_sam=False):
+    """utils.py:912-913: proposal nets train every step for the first 3000,
+    then every 5th."""
+    return (not with_sam) and (global_step <= 3000 or global_step % 5 == 0)
+
+
+def rgb_train_step(model, rays_o, rays_d, gt_rgb, global_step, bg_color=None,
+                   cam_near_far=None, perturb=True):
+    """Returns (pred_rgb, loss, outputs).  gt_rgb [N,3] (or [N,4] with alpha,
+    composited on bg as utils.py:903-906).  Updates model.opt.num_rays like
+    the reference when adaptive_num_rays is on."""
+    opt = model.opt
+    if bg_color is None:
+        bg_color = 1
+    if gt_rgb.shape[-1] == 4:
+        gt_rgb = gt_rgb[..., :3] * gt_rgb[..., 3:] + bg_color * (1 - gt_rgb[..., 3:])
+    update_proposal = update_proposal_now(global_step, opt.with_sam)
+    outputs = model.render(rays_o, rays_d, staged=False, bg_color=bg_color, perturb=perturb,
+                           cam_near_far=cam_near_far, update_proposal=update_proposal,
+                           return_feats=0)
+    pred_rgb = outputs["image"]
+    loss = F.mse_loss(pred_rgb, gt_rgb, reduction="none").mean()
+    if "proposal_loss" in outputs and opt.lambda_proposal > 0:
+        loss = loss + opt.lambda_proposal * outputs["proposal_loss"]
+    if "distort_loss" in outputs and opt.lambda_distort > 0:
+        loss = loss + opt.lambda_distort * outputs["distort_loss"]
+    if opt.lambda_entropy > 0:
+        w = outputs["weights_sum"].clamp(1e-5, 1 - 1e-5)
+        entropy = -w * torch.log2(w) - (1 - w) * torch.log2(1 - w)
+        loss = loss + opt.lambda_entropy * entropy.mean()
+    if opt.adaptive_num_rays and "num_points" in outputs:
+        opt.num_rays = int(round((opt.num_points / outputs["num_points"]) * opt.num_rays))
+    return pred_rgb, loss, outputs
+
+
+def sam_train_step(renderer, rays_o_lr, rays_d_lr, h, w, gt_samvit, cam_near_far=None):
+    """utils.py:1091-1106 on the fused path: 64x64 feature rays, bilinear
+    resize to the target, MSE.  Returns (pred [1,256,h',w'], loss)."""
+    from .fused import render_sam_train
+    out = render_sam_train(renderer, rays_o_lr, rays_d_lr, cam_near_far=cam_near_far)
+    pred = out["samvit"].reshape(1, h, w, 256).permute(0, 3, 1, 2).contiguous()
+    pred = F.interpolate(pred, gt_samvit.shape[2:], mode="bilinear")
+    return pred, F.mse_loss(pred, gt_samvit, reduction="none").mean()
