@@ -22,11 +22,14 @@
 // latency even at the 32K rays of one rank of an 8-GPU view).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "raymarch_device.h"
 #include "samnerf_common.h"
 #include "sh_device.h"
+#include "wave_box.h"
 
 using namespace samnerf;
 
@@ -105,14 +108,31 @@ __device__ __forceinline__ void dense(const float* __restrict__ W, const float* 
     }
 }
 
+// The same layer with two output units per v_pk_fma_f32 (each lane of it is
+// the scalar fma chain of dense(), so the bits are unchanged).
+template <int OUT, int IN, bool RELU>
+__device__ __forceinline__ void dense_pk(const float* __restrict__ W, const float* x, float* y) {
+    static_assert(OUT % 2 == 0, "output pairs");
+#pragma unroll
+    for (int o = 0; o < OUT; o += 2) {
+        f2v a = {0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < IN; ++i)
+            a = __builtin_elementwise_fma(f2v{W[o * IN + i], W[(o + 1) * IN + i]}, f2v{x[i], x[i]}, a);
+        y[o] = RELU ? fmaxf(a.x, 0.0f) : a.x;
+        y[o + 1] = RELU ? fmaxf(a.y, 0.0f) : a.y;
+    }
+}
+
 // Levels are issued in groups of GROUP (8 corner loads each) separated by a
 // scheduling barrier, bounding the loads in flight (and their VGPRs) per lane.
-template <int L, int C, int GROUP = 4>
+template <int L, int C, bool REF, int GROUP = 4>
 __device__ __forceinline__ void grid_features(const GridDesc<16>& g, float ux, float uy, float uz,
                                               float* feat) {
 #pragma unroll
     for (int l = 0; l < L; ++l) {
-        lookup_level3<C>(g.emb, g.lv[l], ux, uy, uz, feat + l * C);
+        if constexpr (REF) lookup_level3_ref<C>(g.emb, g.lv[l], ux, uy, uz, feat + l * C);
+        else lookup_level3<C>(g.emb, g.lv[l], ux, uy, uz, feat + l * C);
         if ((l + 1) % GROUP == 0 && l + 1 < L) __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -148,7 +168,7 @@ constexpr uint32_t prop_sigma_blocks(uint32_t N) {
     return xcd_blocks((N + 63u) / 64u) * (T / 4);
 }
 
-template <int T, bool FIRST>
+template <int T, bool FIRST, bool REF>
 __global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
     static_assert(T % 4 == 0, "T must be a multiple of 4");
     constexpr uint32_t Q = T / 4;
@@ -177,9 +197,10 @@ __global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
     float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
     contract3(x, y, z);
     float feat[10];
-    grid_features<5, 2>(a.grid, a.gs(x), a.gs(y), a.gs(z), feat);
+    grid_features<5, 2, REF>(a.grid, a.gs(x), a.gs(y), a.gs(z), feat);
     float h[16], sv;
-    dense<16, 10, true>(a.W0, feat, h);
+    if constexpr (REF) dense<16, 10, true>(a.W0, feat, h);
+    else dense_pk<16, 10, true>(a.W0, feat, h);
     dense<1, 16, false>(a.W1, h, &sv);
     // the only store, after the weight reads: an earlier store could alias
     // W0/W1 and would demote the uniform weight reads to per-lane vector loads
@@ -690,10 +711,17 @@ struct SgridArgs {
 // - 1 (its next sample's position/weight prefetched behind the current
 // gather), and the quarters are added through LDS.  A wave is 64 rays at one
 // (level, sample), so corner rows are shared across lanes.
-template <int T>
+// MODE: kLookPacked (lookup_level3), kLookRef (lookup_level3_ref, scalar
+// accumulation), kLookBox (wave_box.h: each distinct corner row of the wave
+// read once through LDS).  All three give identical bits.
+constexpr int kLookPacked = 0, kLookRef = 1, kLookBox = 2;
+constexpr uint32_t kSgridBoxCap = 256;      // rows of 32 B per wave (8 KiB)
+
+template <int T, int MODE>
 __global__ void __launch_bounds__(256) k_sgrid(SgridArgs a) {
     constexpr int TQ = T / 4;
     __shared__ float part[3][8][64];
+    __shared__ float4 boxes[MODE == kLookBox ? 4 : 1][MODE == kLookBox ? kSgridBoxCap * 2 : 1];
     const uint32_t lane = threadIdx.x & 63u, q = threadIdx.x >> 6;
     const uint32_t r = xcd_chunk(blockIdx.x, (a.N + 63u) / 64u) * 64u + lane;   // gridDim.x % 8 == 0
     const uint32_t level = blockIdx.y;
@@ -715,9 +743,31 @@ __global__ void __launch_bounds__(256) k_sgrid(SgridArgs a) {
         const float nz = a.u_in[((size_t)kn * 3 + 2) * N + rr];
         const float nw = a.w_in[(size_t)kn * N + rr];
         float f[8];
-        lookup_level3<8>(a.grid.emb, lv, ux, uy, uz, f);
+        if constexpr (MODE == kLookRef) {
+            lookup_level3_ref<8>(a.grid.emb, lv, ux, uy, uz, f);
 #pragma unroll
-        for (int c = 0; c < 8; ++c) acc[c] = acc[c] + w * f[c];
+            for (int c = 0; c < 8; ++c) acc[c] = acc[c] + w * f[c];
+        } else {
+            if constexpr (MODE == kLookBox) {
+                float* slice = reinterpret_cast<float*>(boxes[q]);
+                const Box b = level_box(lv, wave_urange(ux, uy, uz));
+                if (b.n <= kSgridBoxCap) {
+                    stage_box<8>(reinterpret_cast<const char*>(a.grid.emb), lv, b, slice, lane);
+                    lookup_level3_box<8>(a.grid.emb, lv, b, slice, ux, uy, uz, f);
+                } else {
+                    lookup_level3<8>(a.grid.emb, lv, ux, uy, uz, f);
+                }
+            } else {
+                lookup_level3<8>(a.grid.emb, lv, ux, uy, uz, f);
+            }
+            const f2v wv = {w, w};            // acc + w * f, two channels per packed mul / add
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+                const f2v s = f2v{acc[c], acc[c + 1]} + wv * f2v{f[c], f[c + 1]};
+                acc[c] = s.x;
+                acc[c + 1] = s.y;
+            }
+        }
         ux = nx;
         uy = ny;
         uz = nz;
@@ -898,6 +948,17 @@ struct Workspace {
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
+// Gather variants, for A/B measurement and the bit-identity tests:
+// SAMNERF_LOOKUP = packed (default) | ref | box (k_sgrid only; the proposal
+// stages use packed).  Read per call (getenv is cheap next to a launch).
+int lookup_mode() {
+    const char* v = getenv("SAMNERF_LOOKUP");
+    if (!v || !*v) return kLookPacked;
+    if (!strcmp(v, "ref")) return kLookRef;
+    if (!strcmp(v, "box")) return kLookBox;
+    return kLookPacked;
+}
+
 thread_local hipEvent_t g_stage_events[8];
 thread_local uint32_t g_n_stage_events = 0;
 
@@ -1075,9 +1136,11 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.u = make_lin((float)(0.5 / 65), (float)(1.0 - 0.5 / 65), 65);
     pa.bins_in = nullptr;
     pa.bins_out = w.bins1;
+    const int look = lookup_mode();
     mark_stage(0, s);
     k_snf<<<div_up(N, 256), 256, 0, s>>>(pa);
-    k_prop_sigma<128, true><<<prop_sigma_blocks<128>(N), 256, 0, s>>>(pa);
+    if (look == kLookRef) k_prop_sigma<128, true, true><<<prop_sigma_blocks<128>(N), 256, 0, s>>>(pa);
+    else k_prop_sigma<128, true, false><<<prop_sigma_blocks<128>(N), 256, 0, s>>>(pa);
     k_prop_pdf<128, 65, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
 
     // stage 1: 64 samples -> 33 bins
@@ -1088,7 +1151,8 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.bins_in = w.bins1;
     pa.bins_out = w.bins2;
     mark_stage(1, s);
-    k_prop_sigma<64, false><<<prop_sigma_blocks<64>(N), 256, 0, s>>>(pa);
+    if (look == kLookRef) k_prop_sigma<64, false, true><<<prop_sigma_blocks<64>(N), 256, 0, s>>>(pa);
+    else k_prop_sigma<64, false, false><<<prop_sigma_blocks<64>(N), 256, 0, s>>>(pa);
     k_prop_pdf<64, 33, false><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
 
     // stage 2: 32 samples through the full network
@@ -1128,7 +1192,10 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
         sa.w_in = w.w_f;
         sa.rows = rows;
         mark_stage(3, s);
-        k_sgrid<32><<<dim3(xcd_blocks(div_up(N, 64)), 16), 256, 0, s>>>(sa);
+        const dim3 sg(xcd_blocks(div_up(N, 64)), 16);
+        if (look == kLookRef) k_sgrid<32, kLookRef><<<sg, 256, 0, s>>>(sa);
+        else if (look == kLookBox) k_sgrid<32, kLookBox><<<sg, 256, 0, s>>>(sa);
+        else k_sgrid<32, kLookPacked><<<sg, 256, 0, s>>>(sa);
         if ((rc = check_launch("render"))) return rc;
         mark_stage(4, s);
         rc = sam_head_forward(m, rows, N, samvit, w.packed, s);

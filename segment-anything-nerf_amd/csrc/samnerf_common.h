@@ -117,13 +117,85 @@ __device__ __forceinline__ void load_row_b(const char* __restrict__ base, uint32
     }
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// Byte offsets (from the table base) of the 8 corner rows of the cell holding
+// (ux, uy, uz) and their trilinear weights, corner c = bit d <-> axis d
+// (gridencoder.cu:168-201).  Built from per-axis terms: 4 multiplies per
+// level instead of 2 per corner, 24-bit multiplies for dense levels (res^3 <=
+// size < 2^30 keeps every factor below 2^24), the level's first row folded
+// into the x terms.  Same rows as dense_or_hash_row (uint32 wrap-around sums
+// are associative) and the same weights ((wx * wy) * wz) as the reference.
+template <int C>
+__device__ __forceinline__ void corner_rows(const LevelDesc& d, float ux, float uy, float uz,
+                                            uint32_t* off, float* w) {
+    uint32_t cx, cy, cz;
+    float fx, fy, fz;
+    locate_axis(ux, d.res, cx, fx);
+    locate_axis(uy, d.res, cy, fy);
+    locate_axis(uz, d.res, cz, fz);
+    const uint32_t top = d.res - 1u;
+    const uint32_t nx = min(cx + 1u, top), ny = min(cy + 1u, top), nz = min(cz + 1u, top);
+    constexpr uint32_t RB = C * 4u;
+    if (d.flags & kHashed) {
+        const uint32_t m = d.size - 1u;
+        const uint32_t y0 = cy * kPrime1, y1 = ny * kPrime1, z0 = cz * kPrime2, z1 = nz * kPrime2;
+        const uint32_t xy[4] = {cx ^ y0, nx ^ y0, cx ^ y1, nx ^ y1};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) off[c] = (d.off + ((xy[c & 3] ^ ((c & 4) ? z1 : z0)) & m)) * RB;
+    } else {
+        const uint32_t r2 = d.res * d.res;
+        const uint32_t y0 = __umul24(cy, d.res), y1 = __umul24(ny, d.res);
+        const uint32_t z0 = __umul24(cz, r2), z1 = __umul24(nz, r2);
+        const uint32_t x0 = d.off + cx, x1 = d.off + nx;
+        const uint32_t xy[4] = {x0 + y0, x1 + y0, x0 + y1, x1 + y1};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) off[c] = (xy[c & 3] + ((c & 4) ? z1 : z0)) * RB;
+    }
+    const float wx0 = 1.0f - fx, wy0 = 1.0f - fy, wz0 = 1.0f - fz;
+    const float wxy[4] = {wx0 * wy0, fx * wy0, wx0 * fy, fx * fy};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) w[c] = wxy[c & 3] * ((c & 4) ? fz : wz0);
+}
+
 // Trilinear lookup of one level (D = 3, linear interpolation, no
-// align_corners): the 8 corners in the reference's order (bit d <-> axis d,
-// gridencoder.cu:171-192), FMA accumulation into `acc`.  Fused-path tables
-// only (32-bit byte offsets, see load_row_b).
+// align_corners): the 8 corners in the reference's order, FMA accumulation
+// into `acc` on packed-fp32 FMAs (two channels per v_pk_fma_f32; each lane
+// of it is the same IEEE fma as the scalar form, so the bits are unchanged).
+// Fused-path tables only (32-bit byte offsets, see load_row_b).
 template <int C>
 __device__ __forceinline__ void lookup_level3(const float* __restrict__ emb, const LevelDesc& d,
                                               float ux, float uy, float uz, float* acc) {
+    static_assert(C % 2 == 0, "packed accumulation needs an even channel count");
+    uint32_t off[8];
+    float w[8];
+    corner_rows<C>(d, ux, uy, uz, off, w);
+    const char* base = reinterpret_cast<const char*>(emb);
+    f2v a[C / 2];
+#pragma unroll
+    for (int i = 0; i < C / 2; ++i) a[i] = f2v{0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        float e[C];
+        load_row_b<C>(base, off[c], e);
+        const f2v wc = {w[c], w[c]};
+#pragma unroll
+        for (int i = 0; i < C / 2; ++i)
+            a[i] = __builtin_elementwise_fma(wc, f2v{e[2 * i], e[2 * i + 1]}, a[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < C / 2; ++i) {
+        acc[2 * i] = a[i].x;
+        acc[2 * i + 1] = a[i].y;
+    }
+}
+
+// The per-corner form (one row computation and one scalar FMA per corner and
+// channel): kept as the reference variant of lookup_level3 for the A/B
+// parity test (SAMNERF_LOOKUP=ref).
+template <int C>
+__device__ __forceinline__ void lookup_level3_ref(const float* __restrict__ emb, const LevelDesc& d,
+                                                  float ux, float uy, float uz, float* acc) {
     uint32_t cx, cy, cz;
     float fx, fy, fz;
     locate_axis(ux, d.res, cx, fx);

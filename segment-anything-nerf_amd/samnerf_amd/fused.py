@@ -32,6 +32,8 @@ class FusedRenderer:
         self.net = net
         self._ws = None
         self._keep = []
+        self._model = None
+        self._model_key_cached = None
         self.head_mode = int(os.environ.get("SAMNERF_HEAD_MODE", "0")) if head_mode is None else head_mode
 
     # --------------------------------------------------------------- model --
@@ -47,7 +49,28 @@ class FusedRenderer:
         g.base_resolution = enc.base_resolution
         return g
 
+    def _model_key(self):
+        """What the samnerf_model struct depends on: parameter addresses (the
+        struct holds pointers, values may change freely, e.g. under Adam) and
+        the by-value fields (aabb, bounds, steps)."""
+        n = self.net
+        aabb = n.aabb_train if n.training else n.aabb_infer
+        return (n.training, self.head_mode, aabb.data_ptr(), aabb._version,
+                tuple(p.data_ptr() for p in n.parameters()), tuple(n.opt.num_steps),
+                float(n.opt.min_near), float(n.bound), bool(n.opt.with_sam))
+
     def model(self):
+        """The samnerf_model struct of the wrapped network, rebuilt only when
+        _model_key changes: reading the aabb back to the host would otherwise
+        synchronise the stream on every call and stall the launch queue."""
+        key = self._model_key()
+        if self._model is not None and key == self._model_key_cached:
+            return self._model
+        self._model = self._build_model()
+        self._model_key_cached = key
+        return self._model
+
+    def _build_model(self):
         n = self.net
         opt = n.opt
         self._keep = []

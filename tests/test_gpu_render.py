@@ -203,6 +203,38 @@ def test_sam_head_bf16x3_matches_exact_fp32(hip_lib, cuda):
     assert (exact[:256].cpu() - ref).abs().max().item() < 1e-4
 
 
+@pytest.mark.parametrize("mode", ["ref", "box"])
+def test_gather_variants_bit_identical(hip_lib, cuda, monkeypatch, mode):
+    """The packed-FMA gathers (default), the per-corner scalar form (ref) and
+    the LDS box gathers of k_sgrid (box) read the same rows with the same
+    weights in the same FMA order: every output bit must agree, including
+    for scattered rays (boxes too big for LDS -> direct gathers) and a NaN
+    ray (its lanes fall outside the box -> per-lane direct gathers)."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer, ROW
+    spec = synth.ModelSpec(with_sam=True)
+    params = synth.make_params(spec, seed=21, emb_scale=0.5, ln_jitter=0.1)
+    net = make_net(spec, params, cuda)
+    pose, intr = synth.gui_camera(512, 96, rot=synth.random_rotation(5))
+    ro, rd = ops.get_rays(pose, intr, 96, 512, device=cuda)               # 49152 rays
+    perm = torch.randperm(ro.shape[0], generator=torch.Generator().manual_seed(0)).to(cuda)
+    ro = torch.cat([ro, ro[perm[:8192]]]).contiguous()
+    rd = torch.cat([rd, rd[perm[:8192]]]).contiguous()
+    rd[-5] = float("nan")
+    fr = FusedRenderer(net)
+    outs = {}
+    for m in ("packed", mode):
+        monkeypatch.setenv("SAMNERF_LOOKUP", m)
+        rows = torch.empty(ro.shape[0], ROW, device=cuda)
+        o = fr.render(ro, rd, rows=rows)
+        o["rows"] = rows
+        outs[m] = o
+    for k in outs["packed"]:
+        a = torch.nan_to_num(outs["packed"][k], nan=7.0)
+        b = torch.nan_to_num(outs[mode][k], nan=7.0)
+        assert torch.equal(a, b), (k, (a - b).abs().max().item())
+
+
 def test_ray_segment_paths_agree(hip_lib, cuda):
     """k_final spreads each ray's samples over S = 1, 2 or 4 interleaved slots
     by N (more waves for one rank's small share of a view), exchanging optical

@@ -92,18 +92,47 @@ def test_rgb_train_step_gradients_match_cpu_twin(hip_lib, cuda):
     pose, intr = synth.gui_camera(16, 16, rot=synth.random_rotation(6))
     ro, rd = orc.get_rays(pose, intr, 16, 16)
     gt = torch.rand(256, 3, generator=torch.Generator().manual_seed(2))
+    # the hash grid's input and upstream gradient on the GPU (its one call,
+    # the final stage), to check the drop-in backward kernel in isolation
+    seen = {}
+
+    def grab(mod, args, out):
+        seen["x"] = args[0].detach()
+        out.register_hook(lambda g: seen.__setitem__("g", g.detach()))
+    h = gpu.grid.register_forward_hook(grab)
     _, lg, _ = rgb_train_step(gpu, ro.to(cuda), rd.to(cuda), gt.to(cuda), global_step=1, perturb=False)
     lg.backward()
+    h.remove()
     with oracle_encoders():
         _, lc, _ = rgb_train_step(cpu, ro, rd, gt, global_step=1, perturb=False)
         lc.backward()
+        # (1) the kernel: oracle backward on the GPU's own (x, upstream grad)
+        emb = cpu.grid.embeddings
+        emb.grad = None
+        cpu.grid(seen["x"].cpu(), bound=cpu.bound).backward(seen["g"].cpu())
+        k_ref = emb.grad.clone()
+    k_err = (gpu.grid.embeddings.grad.cpu() - k_ref).norm() / k_ref.norm()
+    assert k_err < 1e-4, float(k_err)
+    # (2) end to end: forward loss to fp32 rounding
     assert abs(float(lg) - float(lc)) <= 1e-4 * abs(float(lc)) + 1e-7, (float(lg), float(lc))
+    # (3) end to end gradients.  The density path's parameter gradients are
+    # small sums of cancelling terms (sigma feeds the MSE, distortion and
+    # proposal losses; measured max |g| ~1e-6 for grid.embeddings against
+    # ~1e-3 for view_mlp), so fp32 reassociation (GPU vs CPU cumsum / sum /
+    # GEMM order) moves them by ~1e-2 relative while every other gradient
+    # agrees to <= 2e-4: per-tensor bound 2e-3, or 2e-2 with cosine > 0.9999
+    # for the grid / grid_mlp tensors behind the cancellation.
     for (k, pg), (_, pc) in zip(gpu.named_parameters(), cpu.named_parameters()):
         if pc.grad is None:
             assert pg.grad is None or pg.grad.abs().sum() == 0, k
             continue
-        err = (pg.grad.cpu() - pc.grad).norm() / pc.grad.norm().clamp_min(1e-12)
-        assert err < 2e-3, (k, float(err))
+        a = pg.grad.cpu()
+        err = (a - pc.grad).norm() / pc.grad.norm().clamp_min(1e-12)
+        if k.startswith("grid.") or k.startswith("grid_mlp."):
+            cos = F.cosine_similarity(a.flatten(), pc.grad.flatten(), dim=0)
+            assert err < 2e-2 and cos > 0.9999, (k, float(err), float(cos))
+        else:
+            assert err < 2e-3, (k, float(err))
 
 
 def test_rgb_training_reduces_loss(hip_lib, cuda):
