@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--no-sam", action="store_true", help="config 2 (RGB only)")
     ap.add_argument("--cpu-rays", type=int, default=262144,
                     help="rays in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--ref-gpu-rays", type=int, default=262144,
+                    help="rays of the view rendered by run_torch, the reference's unfused op "
+                         "sequence on the same GPU (0 = skip)")
     ap.add_argument("--head-mode", type=int, default=0, help="0 bf16x3 SAM head, 1 exact fp32")
     ap.add_argument("--chunks", type=int, default=0,
                     help="N > 1: 0 = one launch per view with its all-gather pipelined behind "
@@ -128,6 +131,27 @@ def cpu_baseline(spec, params, pose, intr, H, W, n_rays, gpu_out=None):
         if "samvit" in g and "samvit" in ref:
             parity["max_abs_samvit"] = float((g["samvit"][idx] - ref["samvit"].reshape(n_rays, -1)).abs().max())
     return res, parity
+
+
+def reference_equivalent_gpu(net, ro, rd, n_rays, chunk=16384):
+    """The reference's own op sequence on the same GPU: NeRFRenderer.run_torch
+    (renderer.py:221-390 as ~350 torch ops per chunk, hash/SH encoders = the
+    drop-in HIP kernels with the reference's one-thread-per-(point, level)
+    design), staged in max_ray_batch = 16384 chunks like renderer.py:195.
+    This is BASELINE.md's "reference-equivalent single-GPU" denominator of the
+    >= 10x target (the reference's CUDA extensions cannot run here)."""
+    n = min(n_rays, ro.shape[0])
+    with torch.no_grad():
+        net.run_torch(ro[:chunk], rd[:chunk], return_feats=1)          # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for h in range(0, n, chunk):
+            net.run_torch(ro[h:h + chunk], rd[h:h + chunk], return_feats=1)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "rays/s", "rays": n,
+            "what": "NeRFRenderer.run_torch (the reference's unfused torch op sequence, drop-in HIP "
+                    "encoders), chunks of 16384 rays, same view and weights"}
 
 
 def train_main(args, dev):
@@ -294,6 +318,11 @@ def main():
                          "avg_launch_ms": stage_avg[dom]},
             "stage_ms": stage_avg,
         }
+        if world == 1 and args.ref_gpu_rays > 0:
+            ro_all, rd_all = ops.get_rays(pose, intr, H, W, device=dev)
+            ref = reference_equivalent_gpu(net, ro_all, rd_all, args.ref_gpu_rays)
+            ref["speedup"] = value / ref["value"]
+            rec["reference_equivalent_gpu"] = ref
         if world == 1 and args.cpu_rays > 0:
             rec["cpu_baseline"], rec["parity_vs_ref"] = cpu_baseline(
                 spec, params, pose, intr, H, W, args.cpu_rays, gpu_out=last)

@@ -30,10 +30,10 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
 fi
 
 for m in ${MODES:-packed ref box}; do
-  SAMNERF_LOOKUP=$m timeout -k 10 300 python bench.py --cpu-rays 0 --steps 20 > "$OUT/bench_$m.log" 2>&1
+  SAMNERF_LOOKUP=$m timeout -k 10 300 python bench.py --cpu-rays 0 --ref-gpu-rays 0 --steps 20 > "$OUT/bench_$m.log" 2>&1
   rc=$?; echo "bench $m rc=$rc"; summ "$OUT/bench_$m.log"; fatal $rc && exit $rc
   for h in ${SWEEP_H:-}; do
-    SAMNERF_LOOKUP=$m timeout -k 10 200 python bench.py --H $h --cpu-rays 0 --steps 30 > "$OUT/bench_${m}_h$h.log" 2>&1
+    SAMNERF_LOOKUP=$m timeout -k 10 200 python bench.py --H $h --cpu-rays 0 --ref-gpu-rays 0 --steps 30 > "$OUT/bench_${m}_h$h.log" 2>&1
     rc=$?; echo "bench $m H=$h rc=$rc"; summ "$OUT/bench_${m}_h$h.log"; fatal $rc && exit $rc
   done
 done
@@ -42,7 +42,7 @@ done
 export SAMNERF_LOOKUP=${PROF_MODE:-packed}
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_trace" -o trace \
-  -- python "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --cpu-rays 0 > "$OUT/prof_trace.log" 2>&1
+  -- python "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --cpu-rays 0 --ref-gpu-rays 0 > "$OUT/prof_trace.log" 2>&1
 rc=$?; echo "prof trace rc=$rc"; fatal $rc && exit $rc
 [ "${SKIP_PMC:-0}" = "1" ] && exit 0
 timeout -s KILL 60 rocprofv3 --list-avail > "$OUT/pmc_avail.txt" 2>&1; echo "list-avail rc=$?"
@@ -55,7 +55,7 @@ GROUPS_=(
 i=0
 for g in "${GROUPS_[@]}"; do
   timeout -s KILL 120 rocprofv3 --pmc $g --output-format csv -d "$OUT/pmc/p$i" -o p$i \
-    -- python "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --cpu-rays 0 > "$OUT/pmc_p$i.log" 2>&1
+    -- python "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --cpu-rays 0 --ref-gpu-rays 0 > "$OUT/pmc_p$i.log" 2>&1
   rc=$?; echo "pmc pass $i rc=$rc ($g)"
   if fatal $rc; then break; fi
   i=$((i+1))
