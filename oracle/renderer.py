@@ -158,12 +158,16 @@ def sh_encode(d, degree=4):
 
 # ---------------------------------------------------------------- model --
 
-def mlp(x, weights):
-    """MLP.forward (nerf/network.py:23-34), bias-free, ReLU between layers."""
+def mlp(x, weights, ir=None):
+    """MLP.forward (nerf/network.py:23-34), bias-free, ReLU between layers;
+    `ir` (a list) receives each layer's output after its activation, as
+    save_intermedian_results stores them (network.py:32-33)."""
     for l, W in enumerate(weights):
         x = F.linear(x, W)
         if l != len(weights) - 1:
             x = F.relu(x, inplace=True)
+        if ir is not None:
+            ir.append(x.detach())
     return x
 
 
@@ -200,20 +204,25 @@ class OracleNeRF:
                                for i in range(5)]
             self.ln_w = t("samvit_mlp.1.weight")
             self.ln_b = t("samvit_mlp.1.bias")
+        if spec.with_mask:
+            if spec.m_grid is not None:
+                self.m_grid = OracleGrid(spec.m_grid, params["m_grid.embeddings"],
+                                         params["m_grid.offsets"])
+            self.mask_w = [t(name + ".weight") for name, _, _, _ in spec.mask_shapes()]
         self.aabb = t("aabb_infer")
         self.bound = spec.grid_bound
 
     # network.py:221-229
-    def common_forward(self, x):
+    def common_forward(self, x, ir=None):
         grid_output = self.grid(x, bound=self.bound)
-        f = mlp(grid_output, self.grid_mlp)
+        f = mlp(grid_output, self.grid_mlp, ir)
         sigma = torch.exp(f[..., 0])              # trunc_exp forward, activation.py:15-18
         feat = f[..., 1:]
         return sigma, feat, grid_output
 
     # network.py:231-246
-    def forward(self, x, d):
-        sigma, feat, grid_output = self.common_forward(x)
+    def forward(self, x, d, ir=None):
+        sigma, feat, grid_output = self.common_forward(x, ir)
         d = sh_encode(d, self.spec.sh_degree)
         f_color = torch.cat([feat, d], dim=-1)
         return {"sigma": sigma, "geo_feat": feat, "color": f_color, "grid_output": grid_output}
@@ -232,12 +241,43 @@ class OracleNeRF:
         x = skip_mlp(f, self.sam_layers)
         return F.layer_norm(x, (256,), self.ln_w, self.ln_b, 1e-5)
 
+    def mask_head(self, masks, outputs, colors, grid_ir, view_ir):
+        """Per-sample instance logits, renderer.py:392-452."""
+        spec, M = self.spec, self.mask_w
+        if spec.mask_type == "default":
+            return skip_mlp(torch.cat([masks, outputs["geo_feat"].detach()], dim=-1),
+                            [(W, None) for W in M], skip_layers=())
+        if spec.mask_type == "lightweight_mask":       # 63 inputs into a 35-input MLP: raises, as the reference
+            return mlp(torch.cat([masks, colors.detach()], dim=-1), M)
+        g = grid_ir
+        if spec.adaptive_type == "rgb":
+            v = view_ir
+            m = F.linear(outputs["grid_output"].detach(), M[0])
+            m = F.linear(torch.cat([g[0], m], dim=-1), M[1])
+            m = F.linear(torch.cat([g[1], m], dim=-1), M[2])
+            m = F.linear(torch.cat([g[2], m], dim=-1), M[3])
+            m = F.linear(torch.cat([v[0], m], dim=-1), M[4])
+            m = F.linear(torch.cat([v[1], m], dim=-1), M[5])
+            m = F.linear(m, M[6])
+            return F.linear(m, M[7])
+        if spec.adaptive_type == "density":
+            m = F.linear(outputs["grid_output"].detach(), M[0])
+            m = F.linear(torch.cat([g[0], m], dim=-1), M[1])
+            m = F.linear(torch.cat([g[1], m], dim=-1), M[2])
+            m = F.linear(torch.cat([g[2], m], dim=-1), M[3])
+            m = F.linear(m, M[4])
+            return F.linear(m, M[5])
+        raise AttributeError("'Sequential' object has no attribute 'intermedian_reuslts' "
+                             "(renderer.py:448: the reference's adaptive 'sam' head reads "
+                             "intermediates its samvit_mlp never stores)")
+
     @torch.no_grad()
-    def run(self, rays_o, rays_d, bg_color=None, return_feats=0, H=None, W=None,
+    def run(self, rays_o, rays_d, bg_color=None, return_feats=0, return_mask=0, H=None, W=None,
             keep=None):
-        """nerf/renderer.py:221-390 in eval mode (perturb=False, contract=True,
-        background='last_sample', sum_after_mlp=False, sam_use_view_direction).
-        `keep` (a dict) receives per-stage intermediates for finer checks."""
+        """nerf/renderer.py:221-464 in eval mode (perturb=False, contract=True,
+        background='last_sample', sam_use_view_direction; sum_after_mlp for
+        the RGB + mask configurations).  `keep` (a dict) receives per-stage
+        intermediates for finer checks."""
         rays_o = rays_o.contiguous()
         rays_d = rays_d.contiguous()
         N = rays_o.shape[0]
@@ -264,11 +304,14 @@ class OracleNeRF:
             else:
                 dirs = rays_d.view(-1, 1, 3).expand_as(xyzs)
                 dirs = dirs / torch.norm(dirs, dim=-1, keepdim=True)
-                outputs = self.forward(xyzs, dirs)
+                grid_ir = []
+                outputs = self.forward(xyzs, dirs, grid_ir)
                 sigmas = outputs["sigma"]
                 colors = outputs["color"]
                 if self.spec.with_sam:
                     features = self.s_grid(xyzs, bound=self.bound)
+                if return_mask > 0 and self.spec.mask_type in ("default", "lightweight_mask"):
+                    masks = self.m_grid(xyzs, bound=self.bound)
             weights = composite_weights(real_bins, sigmas)
             if keep is not None:
                 keep[f"bins{prop_iter}"] = bins.clone()
@@ -277,12 +320,20 @@ class OracleNeRF:
         weights_sum = torch.sum(weights, dim=-1)
         depth = torch.sum(weights * rays_t, dim=-1)
         f_image = torch.sum(weights.unsqueeze(-1) * colors, dim=-2)
-        image = torch.sigmoid(mlp(f_image, self.view_mlp))
+        view_ir = []
+        if self.spec.sum_after_mlp:                      # renderer.py:339-342
+            f_colors = mlp(colors, self.view_mlp, view_ir)
+            image = torch.sigmoid(torch.sum(weights.unsqueeze(-1) * f_colors, dim=-2))
+        else:
+            image = torch.sigmoid(mlp(f_image, self.view_mlp, view_ir))
         image = image + (1 - weights_sum).unsqueeze(-1) * bg_color
         results["weights_sum"] = weights_sum
         results["depth"] = depth
         results["image"] = image
         if self.spec.with_sam:
+            if self.spec.sum_after_mlp:
+                raise NotImplementedError("with_sam + sum_after_mlp: the reference's branch "
+                                          "crashes (renderer.py:371-372, SURVEY.md 0.2)")
             f_sam = torch.sum(weights.unsqueeze(-1) * features, dim=-2)
             f = torch.cat([f_sam, f_image, image, depth.unsqueeze(-1)], dim=-1)
             samvit = self.sam_head(f)
@@ -291,6 +342,11 @@ class OracleNeRF:
                 keep["f_image"] = f_image
             if return_feats > 0:
                 results["samvit"] = samvit.view(H, W, -1) if H is not None else samvit
+        if return_mask > 0:                              # renderer.py:392-454
+            point_masks = self.mask_head(masks if self.spec.mask_type in ("default", "lightweight_mask")
+                                         else None, outputs, colors, grid_ir, view_ir)
+            results["instance_mask_logits"] = torch.sum(weights.detach().unsqueeze(-1) * point_masks,
+                                                        dim=-2)
         return results
 
     def render(self, rays_o, rays_d, max_ray_batch=4096 * 4, **kw):

@@ -74,6 +74,14 @@ class ModelSpec:
     prop_log2: int = 17
     geo_feat_dim: int = 15
     sh_degree: int = 4
+    # --with_mask heads (nerf/network.py:125-203; main.py:112-148 defaults)
+    with_mask: bool = False
+    mask_type: str = "default"          # default | lightweight_mask | adaptive
+    adaptive_type: str = "density"      # rgb | density | sam (adaptive only)
+    n_inst: int = 2
+    redundant_instance: int = 0
+    m_grid_log2: int = 19
+    sum_after_mlp: bool = False
     extras: dict = field(default_factory=dict)
 
     @property
@@ -87,6 +95,37 @@ class ModelSpec:
     @property
     def prop(self):
         return [GridSpec(5, 2, self.prop_log2, 128), GridSpec(5, 2, self.prop_log2, 256)]
+
+    @property
+    def m_grid(self):
+        """network.py:127-128 (default) / :138-139 (lightweight_mask); the
+        lightweight table size is hard-coded to 2^10 in the reference."""
+        if not self.with_mask or self.mask_type == "adaptive":
+            return None
+        if self.mask_type == "default":
+            return GridSpec(16, 8, self.m_grid_log2, 512)
+        return GridSpec(16, 2, 10, 256)
+
+    def mask_shapes(self):
+        """(name, out, in, bias) of the mask head's Linears (network.py:125-203)."""
+        if not self.with_mask:
+            return []
+        g, sh = self.geo_feat_dim, self.sh_degree ** 2
+        n_out = self.n_inst + self.redundant_instance
+        if self.mask_type == "default":                  # SkipConnMLP(143, n_out, 256, 3), bias off
+            m = self.m_grid.output_dim + g
+            return [("mask_mlp.0.net.0", 256, m, False), ("mask_mlp.0.net.1", 256, 256, False),
+                    ("mask_mlp.0.net.2", n_out, 256, False)]
+        if self.mask_type == "lightweight_mask":         # MLP(15 + 16 + 4, n_out, 64, 3)
+            return [("mask_mlp.net.0", 64, g + sh + 4, False), ("mask_mlp.net.1", 64, 64, False),
+                    ("mask_mlp.net.2", n_out, 64, False)]
+        d = 96                                           # adaptive: bias-free Linears
+        ins = {"rgb": [(d, 32), (d, 64 + d), (d, 64 + d), (d, 16 + d), (d, 32 + d), (d, 32 + d),
+                       (d, d), (self.n_inst, d)],
+               "density": [(d, 32), (d, 64 + d), (d, 64 + d), (d, 16 + d), (d, d), (self.n_inst, d)],
+               "sam": [(32, 64), (32, 64 + 32), (64, 16 + 32), (256, 256 + 64), (256, 512),
+                       (256, 512), (self.n_inst, 512)]}[self.adaptive_type]
+        return [(f"mask_mlp.{i}", o, i_, False) for i, (o, i_) in enumerate(ins)]
 
     def linear_shapes(self):
         """(name, out, in, bias) in state_dict order of the reference modules."""
@@ -109,6 +148,7 @@ class ModelSpec:
                 ("samvit_mlp.0.net.3", 256, 256, True),
                 ("samvit_mlp.0.net.4", 256, 256, True),
             ]
+        shapes += self.mask_shapes()
         for i, p in enumerate(self.prop):
             shapes += [(f"prop_mlp.{i}.net.0", 16, p.output_dim, False),
                        (f"prop_mlp.{i}.net.1", 1, 16, False)]
@@ -130,6 +170,8 @@ def make_params(spec: ModelSpec, seed=0, emb_scale=1e-4, ln_jitter=0.0):
     grids = [("grid", spec.grid)]
     if spec.with_sam:
         grids.append(("s_grid", spec.s_grid))
+    if spec.m_grid is not None:
+        grids.append(("m_grid", spec.m_grid))
     grids += [(f"prop_encoders.{i}", g) for i, g in enumerate(spec.prop)]
     for name, g in grids:
         offs = g.offsets()

@@ -1,8 +1,9 @@
 """NeRFNetwork on gfx950 -- interface of nerf/network.py:9-308.
 
 Same submodules, parameter names and shapes as the reference (checkpoint
-state_dicts load with strict=True for the RGB + SAM configuration).  The
-mask heads (--with_mask, network.py:125-203) are out of scope.
+state_dicts load with strict=True), including the --with_mask instance heads
+(network.py:125-203: 'default', 'lightweight_mask', 'adaptive' with
+'rgb' / 'density' / 'sam').
 """
 import torch
 import torch.nn as nn
@@ -25,11 +26,18 @@ class MLP(nn.Module):
                       dim_out if l == num_layers - 1 else dim_hidden, bias=bias)
             for l in range(num_layers)])
 
-    def forward(self, x, save_intermedian_results=False):
+    def forward(self, x, save_intermedian_results=True):
+        """network.py:23-34: `intermedian_reuslts` (the reference's attribute
+        name) keeps each layer's detached output after its activation; the
+        adaptive mask heads read them (renderer.py:403-451)."""
+        if save_intermedian_results:
+            self.intermedian_reuslts = []
         for l, layer in enumerate(self.net):
             x = layer(x)
             if l != self.num_layers - 1:
                 x = F.relu(x, inplace=True)
+            if save_intermedian_results:
+                self.intermedian_reuslts.append(x.detach())
         return x
 
 
@@ -50,20 +58,22 @@ class SkipConnMLP(nn.Module):
 
     def forward(self, x, save_intermedian_results=False):
         x_in = x
+        if save_intermedian_results:
+            self.intermedian_reuslts = []
         for l, layer in enumerate(self.net):
             if l in self.skip_layers:
                 x = torch.cat([x, x_in], dim=-1)
             x = layer(x)
             if l != self.num_layers - 1:
                 x = F.leaky_relu(x, inplace=True)
+            if save_intermedian_results:
+                self.intermedian_reuslts.append(x.detach())
         return x
 
 
 class NeRFNetwork(NeRFRenderer):
     def __init__(self, opt):
         super().__init__(opt)
-        if getattr(opt, "with_mask", False):
-            raise NotImplementedError("--with_mask heads are out of scope (SURVEY.md 8f)")
         self.geom_feat_dim = 15
         # table sizes are hard-coded in the reference (19 / 19 / 17); the
         # optional opt.*_log2 overrides exist for small-table test fixtures
@@ -84,6 +94,8 @@ class NeRFNetwork(NeRFRenderer):
                 SkipConnMLP(self.s_dim + self.geom_feat_dim + self.view_in_dim + 4, 256, 256, 5,
                             skip_layers=[2], bias=True),
                 nn.LayerNorm(256))
+        if getattr(opt, "with_mask", False):
+            self._build_mask_head(opt)
         self.prop_encoders = nn.ModuleList()
         self.prop_mlp = nn.ModuleList()
         for desired in (128, 256):
@@ -92,13 +104,74 @@ class NeRFNetwork(NeRFRenderer):
             self.prop_encoders.append(enc)
             self.prop_mlp.append(MLP(dim, 1, 16, 2, bias=False))
 
+    def _build_mask_head(self, opt):
+        """network.py:125-203."""
+        n_out = opt.n_inst + getattr(opt, "redundant_instance", 0)
+        mtype = opt.mask_mlp_type
+        if mtype == "default":
+            self.m_grid, self.m_dim = get_encoder(
+                "hashgrid", input_dim=3, num_levels=16, level_dim=8, base_resolution=16,
+                log2_hashmap_size=getattr(opt, "m_grid_log2", 19), desired_resolution=512)
+            self.mask_mlp = nn.Sequential(SkipConnMLP(self.m_dim + self.geom_feat_dim, n_out, 256, 3,
+                                                      skip_layers=[], bias=False))
+        elif mtype == "lightweight_mask":
+            self.m_grid, self.m_dim = get_encoder(
+                "hashgrid", input_dim=3, num_levels=16, level_dim=2, base_resolution=16,
+                log2_hashmap_size=10, desired_resolution=256)
+            self.mask_mlp = MLP(self.geom_feat_dim + self.view_in_dim + 4, n_out, 64, 3, bias=False)
+        elif mtype == "adaptive":
+            d = self.mask_mlp_dim = 96
+            at = opt.adaptive_mlp_type
+            shapes = {"rgb": [(self.grid_in_dim, d), (64 + d, d), (64 + d, d), (16 + d, d),
+                              (32 + d, d), (32 + d, d), (d, d), (d, opt.n_inst)],
+                      "density": [(self.grid_in_dim, d), (64 + d, d), (64 + d, d), (16 + d, d),
+                                  (d, d), (d, opt.n_inst)],
+                      "sam": [(64, 32), (64 + 32, 32), (16 + 32, 64), (256 + 64, 256), (256 + 256, 256),
+                              (256 + 256, 256), (256 + 256, opt.n_inst)]}[at]
+            self.mask_mlp = nn.ModuleList([nn.Linear(i, o, bias=False) for i, o in shapes])
+        else:
+            raise ValueError(f"unknown mask_mlp_type {mtype!r}")
+
+    def mask_logits(self, masks, outputs, colors):
+        """Per-sample instance logits (renderer.py:392-452)."""
+        mtype = self.opt.mask_mlp_type
+        if mtype == "default":
+            return self.mask_mlp(torch.cat([masks, outputs["geo_feat"].detach()], dim=-1))
+        if mtype == "lightweight_mask":     # 63 inputs into a 35-input MLP: raises, like the reference
+            return self.mask_mlp(torch.cat([masks, colors.detach()], dim=-1))
+        M, g = self.mask_mlp, self.grid_mlp.intermedian_reuslts
+        at = self.opt.adaptive_mlp_type
+        if at == "rgb":
+            v = self.view_mlp.intermedian_reuslts
+            m = M[0](outputs["grid_output"].detach())
+            m = M[1](torch.cat([g[0], m], dim=-1))
+            m = M[2](torch.cat([g[1], m], dim=-1))
+            m = M[3](torch.cat([g[2], m], dim=-1))
+            m = M[4](torch.cat([v[0], m], dim=-1))
+            m = M[5](torch.cat([v[1], m], dim=-1))
+            return M[7](M[6](m))
+        if at == "density":
+            m = M[0](outputs["grid_output"].detach())
+            m = M[1](torch.cat([g[0], m], dim=-1))
+            m = M[2](torch.cat([g[1], m], dim=-1))
+            m = M[3](torch.cat([g[2], m], dim=-1))
+            return M[5](M[4](m))
+        s = self.samvit_mlp.intermedian_reuslts      # AttributeError, as in the reference
+        m = M[0](g[0])
+        m = M[1](torch.cat([g[1], m], dim=-1))
+        m = M[2](torch.cat([g[2], m], dim=-1))
+        m = M[3](torch.cat([s[0], m], dim=-1))
+        m = M[4](torch.cat([s[1], m], dim=-1))
+        m = M[5](torch.cat([s[2], m], dim=-1))
+        return M[6](torch.cat([s[3], m], dim=-1))
+
     def common_forward(self, x, save_intermedian_results=False):
         grid_output = self.grid(x, bound=self.bound)
-        f = self.grid_mlp(grid_output)
+        f = self.grid_mlp(grid_output, save_intermedian_results)
         return trunc_exp(f[..., 0]), f[..., 1:], grid_output
 
     def forward(self, x, d, save_intermedian_results=False, **kwargs):
-        sigma, feat, grid_output = self.common_forward(x)
+        sigma, feat, grid_output = self.common_forward(x, save_intermedian_results)
         d = self.view_encoder(d)
         return {"sigma": sigma, "geo_feat": feat, "color": torch.cat([feat, d], dim=-1),
                 "grid_output": grid_output}
@@ -111,11 +184,19 @@ class NeRFNetwork(NeRFRenderer):
             sigma, _, _ = self.common_forward(x)
         return {"sigma": sigma}
 
+    def _reg_grid(self):
+        """network.py:261-275: the grid the TV / weight-decay regularisers act on."""
+        if self.opt.with_sam:
+            return self.s_grid
+        if getattr(self.opt, "with_mask", False):
+            return self.m_grid
+        return self.grid
+
     def apply_total_variation(self, w):
-        (self.s_grid if self.opt.with_sam else self.grid).grad_total_variation(w)
+        self._reg_grid().grad_total_variation(w)
 
     def apply_weight_decay(self, w):
-        (self.s_grid if self.opt.with_sam else self.grid).grad_weight_decay(w)
+        self._reg_grid().grad_weight_decay(w)
 
     def get_params(self, lr):
         params = [{"params": self.grid.parameters(), "lr": lr},
@@ -126,6 +207,10 @@ class NeRFNetwork(NeRFRenderer):
         if self.opt.with_sam:
             params += [{"params": self.s_grid.parameters(), "lr": lr},
                        {"params": self.samvit_mlp.parameters(), "lr": lr}]
+        if getattr(self.opt, "with_mask", False):
+            if self.opt.mask_mlp_type in ("default", "lightweight_mask"):
+                params.append({"params": self.m_grid.parameters(), "lr": lr})
+            params.append({"params": self.mask_mlp.parameters(), "lr": lr})
         return params
 
 
@@ -135,6 +220,8 @@ def default_opt(with_sam=True, **kw):
     import types
     o = dict(bound=128.0, contract=True, min_near=0.2, density_thresh=10, with_sam=with_sam,
              sum_after_mlp=False, sam_use_view_direction=True, with_mask=False,
+             mask_mlp_type="default", adaptive_mlp_type="density", n_inst=2, redundant_instance=0,
+             epsilon=1e-6,
              num_steps=[128, 64, 32], background="last_sample", max_ray_batch=4096 * 4, fp16=False,
              # training (main.py:75-110, 226)
              lr=1e-2, num_rays=4096, adaptive_num_rays=True, num_points=2 ** 18,

@@ -191,11 +191,15 @@ class NeRFRenderer(nn.Module):
 
     def run_torch(self, rays_o, rays_d, bg_color=None, perturb=False, cam_near_far=None,
                   update_proposal=True, return_feats=0, return_mask=0, H=None, W=None, **kwargs):
-        """The reference's unfused op sequence (renderer.py:221-390) with the
-        HIP drop-in encoders: ~350 small kernels per call."""
-        if return_mask:
-            raise NotImplementedError("--with_mask heads are out of scope (SURVEY.md 8f)")
+        """The reference's unfused op sequence (renderer.py:221-464) with the
+        HIP drop-in encoders: ~350 small kernels per call.  Covers what the
+        fused kernels do not: perturbed sampling, training-mode extras,
+        sum_after_mlp and the --with_mask instance heads."""
         opt = self.opt
+        with_mask = getattr(opt, "with_mask", False)
+        mask_type = getattr(opt, "mask_mlp_type", "default")
+        sum_after = getattr(opt, "sum_after_mlp", False)
+        save_ir = with_mask and mask_type == "adaptive"
         rays_o = rays_o.contiguous()
         rays_d = rays_d.contiguous()
         N = rays_o.shape[0]
@@ -230,10 +234,12 @@ class NeRFRenderer(nn.Module):
             else:
                 dirs = rays_d.view(-1, 1, 3).expand_as(xyzs)
                 dirs = dirs / torch.norm(dirs, dim=-1, keepdim=True)
-                outputs = self(xyzs, dirs)
+                outputs = self(xyzs, dirs, save_intermedian_results=save_ir)
                 sigmas, colors = outputs["sigma"], outputs["color"]
                 if opt.with_sam:
                     features = self.s_grid(xyzs, bound=self.bound)
+                if return_mask > 0 and mask_type in ("default", "lightweight_mask"):
+                    masks = self.m_grid(xyzs, bound=self.bound)
             ds = (real_bins[..., 1:] - real_bins[..., :-1]) * sigmas
             if opt.background == "last_sample":
                 ds = torch.cat([ds[..., :-1], torch.full_like(ds[..., -1:], torch.inf)], dim=-1)
@@ -248,8 +254,12 @@ class NeRFRenderer(nn.Module):
         weights_sum = weights.sum(-1)
         depth = (weights * rays_t).sum(-1)
         f_image = (weights.unsqueeze(-1) * colors).sum(-2)
-        image = torch.sigmoid(self.view_mlp(f_image))
-        if self.training and not opt.with_sam:              # renderer.py:348-356
+        if sum_after:                                        # renderer.py:339-342
+            f_colors = self.view_mlp(colors, save_intermedian_results=save_ir)
+            image = torch.sigmoid((weights.unsqueeze(-1) * f_colors).sum(-2))
+        else:
+            image = torch.sigmoid(self.view_mlp(f_image, save_intermedian_results=save_ir))
+        if self.training and not with_mask and not opt.with_sam:       # renderer.py:348-356
             results["num_points"] = xyzs.shape[0] * xyzs.shape[1]
             results["weights"] = weights
             if getattr(opt, "lambda_proposal", 0) > 0 and update_proposal:
@@ -259,9 +269,16 @@ class NeRFRenderer(nn.Module):
         image = image + (1 - weights_sum).unsqueeze(-1) * bg_color
         results.update(weights_sum=weights_sum, depth=depth, image=image)
         if opt.with_sam:
+            if sum_after:
+                raise NotImplementedError("with_sam + sum_after_mlp: the reference's branch crashes "
+                                          "(renderer.py:371-372, SURVEY.md 0.2)")
             f_sam = (weights.unsqueeze(-1) * features).sum(-2)
             f = torch.cat([f_sam, f_image, image, depth.unsqueeze(-1)], dim=-1)
             samvit = self.samvit_mlp(f)
             if return_feats > 0:
                 results["samvit"] = samvit.view(H, W, -1) if H is not None else samvit
+        if return_mask > 0:                                  # renderer.py:392-454
+            point_masks = self.mask_logits(masks if mask_type in ("default", "lightweight_mask")
+                                           else None, outputs, colors)
+            results["instance_mask_logits"] = (weights.detach().unsqueeze(-1) * point_masks).sum(-2)
         return results

@@ -56,3 +56,35 @@ def sam_train_step(renderer, rays_o_lr, rays_d_lr, h, w, gt_samvit, cam_near_far
     pred = out["samvit"].reshape(1, h, w, 256).permute(0, 3, 1, 2).contiguous()
     pred = F.interpolate(pred, gt_samvit.shape[2:], mode="bilinear")
     return pred, F.mse_loss(pred, gt_samvit, reduction="none").mean()
+
+
+def mask_train_step(model, rays_o, rays_d, gt_mask, num_rays=None, cam_near_far=None):
+    """Trainer.train_step's --with_mask branch (nerf/utils.py:941-977, 1026):
+    render the instance logits (perturb off, proposal nets frozen, white
+    background), softmax over instances, clamp to [epsilon, 1 - epsilon], and
+    the mean negative log-likelihood of the labels of the first `num_rays`
+    rays (the global rays of mixed sampling; no loss if no pixel is labelled,
+    label -1 = unlabelled; like the reference, a -1 among the rays that enter
+    the gather is an error -- raised here before it can become a device-side
+    assert).  The error-map EMA, incoherent-region
+    re-weighting, label regularisation and RGB-similarity terms
+    (utils.py:978-1065) are options of the data pipeline and are not
+    reproduced.  gt_mask: int64 [N] (or [B, N]).  Returns (pred_ids, loss)."""
+    opt = model.opt
+    gt = gt_mask.reshape(-1).long()
+    n = gt.shape[0] if num_rays is None else num_rays
+    outputs = model.render(rays_o, rays_d, staged=False, bg_color=1, perturb=False,
+                           cam_near_far=cam_near_far, update_proposal=False, return_feats=0,
+                           return_mask=1)
+    inst = torch.softmax(outputs["instance_mask_logits"], dim=-1)
+    pred = inst.view(-1, opt.n_inst)
+    pred = torch.clamp(pred, min=opt.epsilon, max=1 - opt.epsilon)
+    labeled = gt != -1
+    if labeled.sum() > 0:
+        if bool((gt[:n] < 0).any()):
+            raise RuntimeError("mask_train_step: label -1 inside the gathered rays "
+                               "(utils.py:973 gathers with it: index out of bounds)")
+        loss = -torch.log(torch.gather(pred[:n], -1, gt[:n, None]))
+    else:
+        loss = torch.zeros((), dtype=pred.dtype, device=pred.device)
+    return pred.argmax(dim=-1), loss.mean()

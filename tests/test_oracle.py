@@ -20,13 +20,11 @@ from oracle import renderer as orc
 from oracle import synth
 
 
-def _spec_from(fx):
-    with_sam, g, s, p = [int(v) for v in fx["spec"]]
-    return synth.ModelSpec(with_sam=bool(with_sam), grid_log2=g, s_grid_log2=s, prop_log2=p)
-
+from helpers import spec_from_fixture as _spec_from  # noqa: E402
 
 RENDER_FIXTURES = ["render_small_rgb", "render_small_sam", "render_small_sam_default_init",
-                   "render_full_sam"]
+                   "render_full_sam", "render_mask_default", "render_mask_default_nosum",
+                   "render_mask_adaptive_density", "render_mask_adaptive_rgb"]
 
 
 @pytest.mark.parametrize("name", RENDER_FIXTURES)
@@ -38,11 +36,14 @@ def test_oracle_render_matches_reference_golden(oracle_lib, name):
     H, W = int(fx["H"]), int(fx["W"])
     ro, rd = orc.get_rays(fx["pose"], fx["intrinsics"], H, W)
     assert np.array_equal(ro.numpy(), fx["rays_o"]) and np.array_equal(rd.numpy(), fx["rays_d"])
-    out = orc.OracleNeRF(spec, params).run(ro, rd, return_feats=1, H=H, W=W)
+    out = orc.OracleNeRF(spec, params).run(ro, rd, return_feats=1, return_mask=int(spec.with_mask),
+                                           H=H, W=W)
     for k in ("image", "depth", "weights_sum"):
         assert np.array_equal(out[k].numpy(), fx[k]), k
     if spec.with_sam:
         assert np.array_equal(out["samvit"].reshape(H * W, -1).numpy(), fx["samvit"])
+    if spec.with_mask:
+        assert np.array_equal(out["instance_mask_logits"].numpy(), fx["instance_mask_logits"])
 
 
 def test_oracle_steps_match_reference_golden():

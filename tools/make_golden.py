@@ -135,10 +135,12 @@ def install_reference():
 def make_opt(spec: synth.ModelSpec):
     return types.SimpleNamespace(
         bound=spec.bound, contract=True, min_near=spec.min_near, density_thresh=10,
-        with_sam=spec.with_sam, sum_after_mlp=False, sam_use_view_direction=True,
-        with_mask=False, mask_mlp_type="default", num_steps=list(spec.num_steps),
+        with_sam=spec.with_sam, sum_after_mlp=spec.sum_after_mlp, sam_use_view_direction=True,
+        with_mask=spec.with_mask, mask_mlp_type=spec.mask_type,
+        adaptive_mlp_type=spec.adaptive_type, num_steps=list(spec.num_steps),
         background="last_sample", max_ray_batch=4096 * 4, lambda_proposal=1,
-        lambda_distort=0.02, fp16=False, n_inst=2, redundant_instance=0)
+        lambda_distort=0.02, fp16=False, n_inst=spec.n_inst,
+        redundant_instance=spec.redundant_instance)
 
 
 # -------------------------------------------------------------- fixtures --
@@ -146,7 +148,8 @@ def make_opt(spec: synth.ModelSpec):
 def render_fixture(network, name, spec, seed, emb_scale, H, W, rot_seed, ln_jitter=0.1):
     TABLE_LOG2.clear()
     TABLE_LOG2[(16, 2, int(2048 * spec.grid_bound))] = spec.grid_log2
-    TABLE_LOG2[(16, 8, 512)] = spec.s_grid_log2
+    assert not (spec.with_sam and spec.with_mask and spec.s_grid_log2 != spec.m_grid_log2)
+    TABLE_LOG2[(16, 8, 512)] = spec.m_grid_log2 if spec.with_mask else spec.s_grid_log2
     TABLE_LOG2[(5, 2, 128)] = spec.prop_log2
     TABLE_LOG2[(5, 2, 256)] = spec.prop_log2
     params = synth.make_params(spec, seed=seed, emb_scale=emb_scale, ln_jitter=ln_jitter)
@@ -160,15 +163,19 @@ def render_fixture(network, name, spec, seed, emb_scale, H, W, rot_seed, ln_jitt
     rot = synth.random_rotation(rot_seed) if rot_seed is not None else None
     pose, intr = synth.gui_camera(W, H, rot=rot)
     rays_o, rays_d = orc.get_rays(pose, intr, H, W)
+    rm = int(spec.with_mask)
     with torch.no_grad():
-        ref = model.run(rays_o, rays_d, return_feats=1, H=H, W=W)
-    mine = orc.OracleNeRF(spec, params).run(rays_o, rays_d, return_feats=1, H=H, W=W)
+        ref = model.run(rays_o, rays_d, return_feats=1, return_mask=rm, H=H, W=W)
+    mine = orc.OracleNeRF(spec, params).run(rays_o, rays_d, return_feats=1, return_mask=rm, H=H, W=W)
     for k, v in ref.items():
         d = (v - mine[k]).abs().max().item()
         print(f"  {name}: {k:12s} max|ref-oracle| = {d:.3e}")
         assert d == 0.0, f"oracle restatement diverges from reference on {k}"
     out = dict(
         spec=np.array([spec.with_sam, spec.grid_log2, spec.s_grid_log2, spec.prop_log2], np.int64),
+        mask_spec=np.array([spec.with_mask, spec.n_inst, spec.redundant_instance, spec.m_grid_log2,
+                            spec.sum_after_mlp], np.int64),
+        mask_types=np.array([spec.mask_type, spec.adaptive_type]),
         seed=np.int64(seed), emb_scale=np.float64(emb_scale), ln_jitter=np.float64(ln_jitter),
         pose=pose, intrinsics=intr, H=np.int64(H), W=np.int64(W),
         rays_o=rays_o.numpy(), rays_d=rays_d.numpy(),
@@ -176,7 +183,53 @@ def render_fixture(network, name, spec, seed, emb_scale, H, W, rot_seed, ln_jitt
         weights_sum=ref["weights_sum"].numpy())
     if spec.with_sam:
         out["samvit"] = ref["samvit"].reshape(H * W, -1).numpy()
+    if spec.with_mask:
+        out["instance_mask_logits"] = ref["instance_mask_logits"].numpy()
     np.savez_compressed(os.path.join(GOLDEN, name + ".npz"), **out)
+
+
+def mask_fixtures(network):
+    """--with_mask heads (network.py:125-203, renderer.py:392-454) in the
+    configurations the reference's scripts run (scripts/train_mask.sh:
+    adaptive + density + sum_after_mlp; scripts/test_mask_gui.sh: default +
+    sum_after_mlp), plus the two head types whose reference forward raises:
+    their exception types and messages are stored so the tests can require
+    the same behaviour."""
+    small = dict(grid_log2=12, s_grid_log2=11, prop_log2=10, m_grid_log2=11, with_sam=False)
+    render_fixture(network, "render_mask_default",
+                   synth.ModelSpec(with_mask=True, mask_type="default", sum_after_mlp=True, **small),
+                   seed=7, emb_scale=0.5, H=16, W=16, rot_seed=6)
+    render_fixture(network, "render_mask_default_nosum",
+                   synth.ModelSpec(with_mask=True, mask_type="default", n_inst=3, redundant_instance=1,
+                                   **small), seed=8, emb_scale=0.5, H=12, W=12, rot_seed=7)
+    for at in ("density", "rgb"):
+        render_fixture(network, f"render_mask_adaptive_{at}",
+                       synth.ModelSpec(with_mask=True, mask_type="adaptive", adaptive_type=at,
+                                       sum_after_mlp=True, **small),
+                       seed=9, emb_scale=0.5, H=12, W=12, rot_seed=8)
+    errs = {}
+    for mt, at in (("lightweight_mask", "density"), ("adaptive", "sam")):
+        spec = synth.ModelSpec(with_mask=True, mask_type=mt, adaptive_type=at, **small)
+        TABLE_LOG2.clear()
+        TABLE_LOG2[(16, 2, int(2048 * spec.grid_bound))] = spec.grid_log2
+        TABLE_LOG2[(5, 2, 128)] = spec.prop_log2
+        TABLE_LOG2[(5, 2, 256)] = spec.prop_log2
+        params = synth.make_params(spec, seed=3, emb_scale=0.5)
+        model = network.NeRFNetwork(make_opt(spec))
+        model.load_state_dict({k: torch.from_numpy(np.asarray(params[k])) for k in model.state_dict()},
+                              strict=True)
+        model.eval()
+        rays_o, rays_d = orc.get_rays(*synth.gui_camera(4, 4), 4, 4)
+        try:
+            with torch.no_grad():
+                model.run(rays_o, rays_d, return_mask=1)
+            raise AssertionError(f"{mt}/{at}: the reference did not raise")
+        except (RuntimeError, AttributeError, TypeError) as e:
+            errs[f"{mt}_{at}"] = (type(e).__name__, str(e).splitlines()[0][:200])
+            print(f"  {mt}/{at}: reference raises {type(e).__name__}: {errs[f'{mt}_{at}'][1]}")
+    np.savez_compressed(os.path.join(GOLDEN, "mask_errors.npz"),
+                        **{k + "_type": np.array(v[0]) for k, v in errs.items()},
+                        **{k + "_msg": np.array(v[1]) for k, v in errs.items()})
 
 
 def units_fixture(renderer, utils):
@@ -236,6 +289,7 @@ def main():
     render_fixture(network, "render_small_sam_default_init",
                    synth.ModelSpec(with_sam=True, **small),
                    seed=5, emb_scale=1e-4, H=8, W=8, rot_seed=None, ln_jitter=0.0)
+    mask_fixtures(network)
     if not args.skip_full:
         render_fixture(network, "render_full_sam", synth.ModelSpec(with_sam=True),
                        seed=3, emb_scale=0.5, H=8, W=8, rot_seed=5)
