@@ -168,8 +168,8 @@ constexpr uint32_t prop_sigma_blocks(uint32_t N) {
     return xcd_blocks((N + 63u) / 64u) * (T / 4);
 }
 
-template <int T, bool FIRST, bool REF>
-__global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
+template <int T, bool FIRST, bool REF, int OCC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) k_prop_sigma(PropArgs a) {
     static_assert(T % 4 == 0, "T must be a multiple of 4");
     constexpr uint32_t Q = T / 4;
     const uint32_t b = blockIdx.x, i = b >> 3;
@@ -966,6 +966,24 @@ void mark_stage(uint32_t i, hipStream_t s) {
     if (i < g_n_stage_events && g_stage_events[i]) (void)hipEventRecord(g_stage_events[i], s);
 }
 
+// Minimum waves per SIMD the proposal-sigma kernel is compiled for
+// (SAMNERF_PROP_OCC = 1 (no bound, the compiler's choice) | 5 | 6): fewer
+// registers per wave, more waves to hide the gather latency.
+int prop_occ() {
+    const char* v = getenv("SAMNERF_PROP_OCC");
+    const int o = v ? atoi(v) : 1;
+    return (o == 5 || o == 6) ? o : 1;
+}
+
+template <int T, bool FIRST>
+void launch_prop_sigma(int look, int occ, uint32_t N, hipStream_t s, const PropArgs& pa) {
+    const uint32_t nb = prop_sigma_blocks<T>(N);
+    if (look == kLookRef) k_prop_sigma<T, FIRST, true, 1><<<nb, 256, 0, s>>>(pa);
+    else if (occ == 5) k_prop_sigma<T, FIRST, false, 5><<<nb, 256, 0, s>>>(pa);
+    else if (occ == 6) k_prop_sigma<T, FIRST, false, 6><<<nb, 256, 0, s>>>(pa);
+    else k_prop_sigma<T, FIRST, false, 1><<<nb, 256, 0, s>>>(pa);
+}
+
 Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
     Workspace w;
     char* p = static_cast<char*>(base);
@@ -1139,8 +1157,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     const int look = lookup_mode();
     mark_stage(0, s);
     k_snf<<<div_up(N, 256), 256, 0, s>>>(pa);
-    if (look == kLookRef) k_prop_sigma<128, true, true><<<prop_sigma_blocks<128>(N), 256, 0, s>>>(pa);
-    else k_prop_sigma<128, true, false><<<prop_sigma_blocks<128>(N), 256, 0, s>>>(pa);
+    launch_prop_sigma<128, true>(look, prop_occ(), N, s, pa);
     k_prop_pdf<128, 65, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
 
     // stage 1: 64 samples -> 33 bins
@@ -1151,8 +1168,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.bins_in = w.bins1;
     pa.bins_out = w.bins2;
     mark_stage(1, s);
-    if (look == kLookRef) k_prop_sigma<64, false, true><<<prop_sigma_blocks<64>(N), 256, 0, s>>>(pa);
-    else k_prop_sigma<64, false, false><<<prop_sigma_blocks<64>(N), 256, 0, s>>>(pa);
+    launch_prop_sigma<64, false>(look, prop_occ(), N, s, pa);
     k_prop_pdf<64, 33, false><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
 
     // stage 2: 32 samples through the full network
