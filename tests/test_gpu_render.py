@@ -262,3 +262,22 @@ def test_ray_segment_paths_agree(hip_lib, cuda):
             tol = 1e-4 * (1 + a.abs().max().item()) if k in ("depth", "rows") else 1e-4
             err = (a - b).abs().max().item()
             assert err < tol, (n, k, err)
+
+
+def test_sam_feature_handoff_stays_on_device(hip_lib, cuda):
+    """the fused render's 64x64 feature map goes to the SAM
+    decoder interface without leaving the device (nerf/gui.py:143-161 loop)."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer
+    from samnerf_amd.sam_bridge import prepare_sam_features, render_and_predict
+    from test_sam_bridge import Recorder
+    spec = synth.ModelSpec(with_sam=True, grid_log2=12, s_grid_log2=11, prop_log2=10)
+    net = make_net(spec, synth.make_params(spec, seed=4, emb_scale=0.5, ln_jitter=0.1), cuda)
+    pose, intr = synth.gui_camera(64, 64)
+    ro, rd = ops.get_rays(pose, intr, 64, 64, device=cuda)
+    rec = Recorder()
+    (masks, orig, low), out = render_and_predict(FusedRenderer(net), rec, ro, rd, 64, 64, 512, 512,
+                                                 point_coords=[[256, 256]])
+    assert rec.features.is_cuda and rec.coords.is_cuda
+    assert torch.equal(rec.features, prepare_sam_features(out["samvit"].view(64, 64, 256)))
+    assert orig.tolist() == [[256, 256]] and masks.shape == (1, 512, 512)
