@@ -714,7 +714,7 @@ struct SgridArgs {
 // MODE: kLookPacked (lookup_level3), kLookRef (lookup_level3_ref, scalar
 // accumulation), kLookBox (wave_box.h: each distinct corner row of the wave
 // read once through LDS).  All three give identical bits.
-constexpr int kLookPacked = 0, kLookRef = 1, kLookBox = 2;
+constexpr int kLookPacked = 0, kLookRef = 1, kLookBox = 2, kLookBox4 = 3;
 constexpr uint32_t kSgridBoxCap = 256;      // rows of 32 B per wave (8 KiB)
 
 template <int T, int MODE>
@@ -784,6 +784,104 @@ __global__ void __launch_bounds__(256) k_sgrid(SgridArgs a) {
     float4* dst = reinterpret_cast<float4*>(a.rows + (size_t)r * kRow + level * 8u);
     dst[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
     dst[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+}
+
+// k_sgrid with de-duplicated gathers (SAMNERF_LOOKUP=box4, wave_box.h).  A
+// block is 64 neighbouring rays x 4 sample quarters at one group of 4
+// levels (gridDim.y = 4): wave q sums samples q*T/4 .. q*T/4 + T/4 - 1 for
+// levels 4g .. 4g+3 (32 accumulators per lane).  Per sample the wave reduces
+// its positions' range once, lanes 0-3 evaluate the 4 levels' padded corner
+// boxes, and per level the wave loads each distinct corner row once into its
+// 8 KiB LDS slice and reads the 8 corners of every lane from there: the
+// vector-memory path carries one address per distinct row instead of 16 per
+// lane.  Same rows, weights, FMA order and quarter split as k_sgrid, so the
+// bits are identical.
+constexpr uint32_t kBoxSlots = 256;          // 32 B slots per wave (8 KiB)
+
+template <int T>
+__global__ void __launch_bounds__(256) k_sgrid_box4(SgridArgs a) {
+    constexpr int TQ = T / 4;
+    __shared__ float4 smem[4][kBoxSlots * 2];          // per wave: the box slice
+    const uint32_t lane = threadIdx.x & 63u, q = threadIdx.x >> 6;
+    const uint32_t r = xcd_chunk(blockIdx.x, (a.N + 63u) / 64u) * 64u + lane;
+    const uint32_t g = blockIdx.y;                      // levels 4g .. 4g+3
+    const bool live = r < a.N;
+    const uint32_t N = a.N, rr = live ? r : N - 1;
+    const LevelDesc L[4] = {a.grid.lv[4 * g], a.grid.lv[4 * g + 1], a.grid.lv[4 * g + 2],
+                            a.grid.lv[4 * g + 3]};
+    const uint32_t li = lane & 3u;                      // this lane's level for the box pass
+    const LevelDesc mine = {li == 0 ? L[0].off : li == 1 ? L[1].off : li == 2 ? L[2].off : L[3].off,
+                            li == 0 ? L[0].size : li == 1 ? L[1].size : li == 2 ? L[2].size : L[3].size,
+                            li == 0 ? L[0].res : li == 1 ? L[1].res : li == 2 ? L[2].res : L[3].res,
+                            0u};
+    float* slice = reinterpret_cast<float*>(smem[q]);
+    const char* base = reinterpret_cast<const char*>(a.grid.emb);
+    float acc[4][8];
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[l][c] = 0.0f;
+    const int k0 = (int)q * TQ;
+    float ux = a.u_in[((size_t)k0 * 3 + 0) * N + rr];
+    float uy = a.u_in[((size_t)k0 * 3 + 1) * N + rr];
+    float uz = a.u_in[((size_t)k0 * 3 + 2) * N + rr];
+    float w = a.w_in[(size_t)k0 * N + rr];
+    for (int k = k0; k < k0 + TQ; ++k) {
+        const int kn = k + 1 < k0 + TQ ? k + 1 : k;          // prefetch (clamped)
+        const float nx = a.u_in[((size_t)kn * 3 + 0) * N + rr];
+        const float ny = a.u_in[((size_t)kn * 3 + 1) * N + rr];
+        const float nz = a.u_in[((size_t)kn * 3 + 2) * N + rr];
+        const float nw = a.w_in[(size_t)kn * N + rr];
+        const URange ur = wave_urange(ux, uy, uz);
+        uint32_t p0, p1, p2;
+        pbox_lane(mine, ur, p0, p1, p2);
+        const f2v wv = {w, w};
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const PBox b = pbox_read(p0, p1, p2, l);
+            float f[8];
+            if (b.slots <= kBoxSlots) {
+                stage_pbox<8>(base, L[l], b, slice, lane);
+                lookup_level3_pbox<8>(a.grid.emb, L[l], b, slice, ux, uy, uz, f);
+            } else {
+                lookup_level3<8>(a.grid.emb, L[l], ux, uy, uz, f);
+            }
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+                const f2v s2 = f2v{acc[l][c], acc[l][c + 1]} + wv * f2v{f[c], f[c + 1]};
+                acc[l][c] = s2.x;
+                acc[l][c + 1] = s2.y;
+            }
+        }
+        ux = nx;
+        uy = ny;
+        uz = nz;
+        w = nw;
+    }
+    // quarters 1-3 hand their sums to quarter 0 through the (now free) slices
+    __syncthreads();
+    float* part = reinterpret_cast<float*>(smem);          // [3][32][64]
+    if (q > 0) {
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) part[((q - 1) * 32 + l * 8 + c) * 64 + lane] = acc[l][c];
+    }
+    __syncthreads();
+    if (q > 0 || !live) return;
+    float* dst = a.rows + (size_t)r * kRow + g * 32u;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int i = l * 8 + c;
+            v[c] = ((acc[l][c] + part[(0 * 32 + i) * 64 + lane]) + part[(1 * 32 + i) * 64 + lane]) +
+                   part[(2 * 32 + i) * 64 + lane];
+        }
+        reinterpret_cast<float4*>(dst + l * 8)[0] = make_float4(v[0], v[1], v[2], v[3]);
+        reinterpret_cast<float4*>(dst + l * 8)[1] = make_float4(v[4], v[5], v[6], v[7]);
+    }
 }
 
 // Backward of k_sgrid for the distillation step: grad_emb[row] += w_k *
@@ -956,6 +1054,7 @@ int lookup_mode() {
     if (!v || !*v) return kLookPacked;
     if (!strcmp(v, "ref")) return kLookRef;
     if (!strcmp(v, "box")) return kLookBox;
+    if (!strcmp(v, "box4")) return kLookBox4;
     return kLookPacked;
 }
 
@@ -973,6 +1072,19 @@ int prop_occ() {
     const char* v = getenv("SAMNERF_PROP_OCC");
     const int o = v ? atoi(v) : 1;
     return (o == 5 || o == 6) ? o : 1;
+}
+
+// Default k_sgrid form by launch size: the de-duplicated box gathers win
+// on a full view (TA-bound direct gathers), the direct gathers on one rank's
+// share of a sharded view (latency-bound at 3 waves per SIMD): measured
+// 0.94 vs 1.05 ms at 262,144 rays, 0.25 vs 0.21 ms at 32,768.
+constexpr uint32_t kBox4MinRays = 131072;
+
+// k_sgrid_box4 packs cell indices and extents into 10 bits
+bool box4_ok(const GridDesc<16>& g) {
+    for (int l = 0; l < 16; ++l)
+        if (g.lv[l].res > 1023u) return false;
+    return true;
 }
 
 template <int T, bool FIRST>
@@ -1196,8 +1308,11 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.rows = m->with_sam || feature_rows ? rows : nullptr;
     mark_stage(2, s);
     // segments per ray: enough waves to fill the resident slots (2 per SIMD)
-    if (N >= 65536u) k_final<32, 1><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
-    else if (N >= 32768u) k_final<32, 2><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
+    // (SAMNERF_FINAL_S = 1 | 2 | 4 overrides, for measurement)
+    const char* fs = getenv("SAMNERF_FINAL_S");
+    const int seg = fs ? atoi(fs) : (N >= 65536u ? 1 : N >= 32768u ? 2 : 4);
+    if (seg == 1) k_final<32, 1><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
+    else if (seg == 2) k_final<32, 2><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
     else k_final<32, 4><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
 
     if (m->with_sam) {
@@ -1211,6 +1326,9 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
         const dim3 sg(xcd_blocks(div_up(N, 64)), 16);
         if (look == kLookRef) k_sgrid<32, kLookRef><<<sg, 256, 0, s>>>(sa);
         else if (look == kLookBox) k_sgrid<32, kLookBox><<<sg, 256, 0, s>>>(sa);
+        else if ((look == kLookBox4 || (look == kLookPacked && N >= kBox4MinRays && !getenv("SAMNERF_LOOKUP")))
+                 && box4_ok(gs))
+            k_sgrid_box4<32><<<dim3(xcd_blocks(div_up(N, 64)), 4), 256, 0, s>>>(sa);
         else k_sgrid<32, kLookPacked><<<sg, 256, 0, s>>>(sa);
         if ((rc = check_launch("render"))) return rc;
         mark_stage(4, s);

@@ -195,3 +195,119 @@ __device__ __forceinline__ void lookup_level3_box(const float* __restrict__ emb,
 }
 
 }  // namespace samnerf
+
+namespace samnerf {
+
+// ---- power-of-two padded boxes, evaluated lane-parallel -----------------
+// The x and y extents are rounded up to powers of two so that slot decoding
+// and local corner indices are shifts and masks.  A wave that handles NL
+// levels evaluates level i's box in lane i (one pass of VALU work for all
+// levels) and reads the fields back with three readlanes.
+
+__device__ __forceinline__ uint32_t log2_ceil(uint32_t v) { return v <= 1u ? 0u : 32u - __clz(v - 1u); }
+
+struct PBox {
+    uint32_t x0, y0, z0, ex, ey, ez, lx, ly, slots;
+};
+
+// Packed per-lane form: p0 = x0 | y0 << 10 | z0 << 20, p1 = ex | ey << 10 |
+// ez << 20, p2 = lx | ly << 8 (every cell index and extent < 1024: the host
+// admits only grids with res <= 1023 on this path).
+__device__ __forceinline__ void pbox_lane(const LevelDesc& d, const URange& u, uint32_t& p0,
+                                          uint32_t& p1, uint32_t& p2) {
+    const uint32_t top = d.res - 1u;
+    const uint32_t x0 = cell_of(u.lo[0], d.res), y0 = cell_of(u.lo[1], d.res), z0 = cell_of(u.lo[2], d.res);
+    const uint32_t x1 = min(cell_of(u.hi[0], d.res) + 1u, top);
+    const uint32_t y1 = min(cell_of(u.hi[1], d.res) + 1u, top);
+    const uint32_t z1 = min(cell_of(u.hi[2], d.res) + 1u, top);
+    const uint32_t ex = x1 - x0 + 1u, ey = y1 - y0 + 1u, ez = z1 - z0 + 1u;
+    p0 = x0 | (y0 << 10) | (z0 << 20);
+    p1 = ex | (ey << 10) | (ez << 20);
+    p2 = log2_ceil(ex) | (log2_ceil(ey) << 8);
+}
+
+__device__ __forceinline__ PBox pbox_read(uint32_t p0, uint32_t p1, uint32_t p2, int lane) {
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)p0, lane);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)p1, lane);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)p2, lane);
+    PBox r;
+    r.x0 = a & 1023u;
+    r.y0 = (a >> 10) & 1023u;
+    r.z0 = a >> 20;
+    r.ex = b & 1023u;
+    r.ey = (b >> 10) & 1023u;
+    r.ez = b >> 20;
+    r.lx = c & 255u;
+    r.ly = c >> 8;
+    r.slots = r.ez << (r.lx + r.ly);
+    return r;
+}
+
+// Stage the box's rows (C floats each) into `slice`, slot j = bx | by << lx
+// | bz << (lx + ly); padding slots are left unwritten (never read).
+template <int C>
+__device__ __forceinline__ void stage_pbox(const char* __restrict__ base, const LevelDesc& d,
+                                           const PBox& b, float* slice, uint32_t lane) {
+    const uint32_t xm = (1u << b.lx) - 1u, ym = (1u << b.ly) - 1u;
+    for (uint32_t j = lane; j < b.slots; j += 64u) {
+        const uint32_t bx = j & xm, t = j >> b.lx, by = t & ym, bz = t >> b.ly;
+        if (bx < b.ex && by < b.ey) {
+            const uint32_t row = dense_or_hash_row(b.x0 + bx, b.y0 + by, b.z0 + bz, d);
+            float e[C];
+            load_row_b<C>(base, (d.off + row) * (uint32_t)(C * 4), e);
+#pragma unroll
+            for (int i = 0; i < C; i += 4)
+                *reinterpret_cast<float4*>(slice + j * C + i) = make_float4(e[i], e[i + 1], e[i + 2], e[i + 3]);
+        }
+    }
+}
+
+// lookup_level3 from a staged padded box (same rows, weights, FMA order);
+// a lane whose corners are outside the box gathers directly.
+template <int C>
+__device__ __forceinline__ void lookup_level3_pbox(const float* __restrict__ emb, const LevelDesc& d,
+                                                   const PBox& b, const float* slice, float ux,
+                                                   float uy, float uz, float* acc) {
+    uint32_t cx, cy, cz;
+    float fx, fy, fz;
+    locate_axis(ux, d.res, cx, fx);
+    locate_axis(uy, d.res, cy, fy);
+    locate_axis(uz, d.res, cz, fz);
+    const uint32_t top = d.res - 1u;
+    const uint32_t nx = min(cx + 1u, top), ny = min(cy + 1u, top), nz = min(cz + 1u, top);
+    const uint32_t lx0 = cx - b.x0, lx1 = nx - b.x0;
+    const uint32_t ly0 = cy - b.y0, ly1 = ny - b.y0;
+    const uint32_t lz0 = cz - b.z0, lz1 = nz - b.z0;
+    const bool inside = lx0 < b.ex && lx1 < b.ex && ly0 < b.ey && ly1 < b.ey && lz0 < b.ez && lz1 < b.ez;
+    if (!inside) {
+        lookup_level3<C>(emb, d, ux, uy, uz, acc);
+        return;
+    }
+    const uint32_t X[2] = {lx0, lx1};
+    const uint32_t Y[2] = {ly0 << b.lx, ly1 << b.lx};
+    const uint32_t Z[2] = {lz0 << (b.lx + b.ly), lz1 << (b.lx + b.ly)};
+    const float wx0 = 1.0f - fx, wy0 = 1.0f - fy, wz0 = 1.0f - fz;
+    const float wxy[4] = {wx0 * wy0, fx * wy0, wx0 * fy, fx * fy};
+    f2v a[C / 2];
+#pragma unroll
+    for (int i = 0; i < C / 2; ++i) a[i] = f2v{0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const float w = wxy[c & 3] * ((c & 4) ? fz : wz0);
+        const uint32_t j = X[c & 1] + Y[(c >> 1) & 1] + Z[c >> 2];
+        const f2v wc = {w, w};
+#pragma unroll
+        for (int i = 0; i < C; i += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(slice + j * C + i);
+            a[i / 2] = __builtin_elementwise_fma(wc, f2v{v.x, v.y}, a[i / 2]);
+            a[i / 2 + 1] = __builtin_elementwise_fma(wc, f2v{v.z, v.w}, a[i / 2 + 1]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < C / 2; ++i) {
+        acc[2 * i] = a[i].x;
+        acc[2 * i + 1] = a[i].y;
+    }
+}
+
+}  // namespace samnerf

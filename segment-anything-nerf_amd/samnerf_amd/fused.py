@@ -104,10 +104,17 @@ class FusedRenderer:
         return m
 
     def workspace(self, m, N, device):
+        """Scratch of one render call, one buffer per (device, stream): calls
+        on one stream reuse it in stream order; renders issued on different
+        streams (concurrent views) never share one."""
         need = lib().samnerf_render_workspace_size(ctypes.byref(m), N)
-        if self._ws is None or self._ws.numel() < need or self._ws.device != device:
-            self._ws = torch.empty(max(need, 1), dtype=torch.uint8, device=device)
-        return self._ws, need
+        key = (device, torch.cuda.current_stream(device).cuda_stream)
+        if self._ws is None:
+            self._ws = {}
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < need:
+            ws = self._ws[key] = torch.empty(max(need, 1), dtype=torch.uint8, device=device)
+        return ws, need
 
     # -------------------------------------------------------------- render --
     @torch.no_grad()

@@ -203,7 +203,7 @@ def test_sam_head_bf16x3_matches_exact_fp32(hip_lib, cuda):
     assert (exact[:256].cpu() - ref).abs().max().item() < 1e-4
 
 
-@pytest.mark.parametrize("mode", ["ref", "box"])
+@pytest.mark.parametrize("mode", ["ref", "box", "box4"])
 def test_gather_variants_bit_identical(hip_lib, cuda, monkeypatch, mode):
     """The packed-FMA gathers (default), the per-corner scalar form (ref) and
     the LDS box gathers of k_sgrid (box) read the same rows with the same
