@@ -715,6 +715,7 @@ struct SgridArgs {
 // accumulation), kLookBox (wave_box.h: each distinct corner row of the wave
 // read once through LDS).  All three give identical bits.
 constexpr int kLookPacked = 0, kLookRef = 1, kLookBox = 2, kLookBox4 = 3;
+constexpr int kLookAuto = 4;     // host-side only: packed, k_sgrid by launch size
 constexpr uint32_t kSgridBoxCap = 256;      // rows of 32 B per wave (8 KiB)
 
 template <int T, int MODE>
@@ -1051,7 +1052,7 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 // stages use packed).  Read per call (getenv is cheap next to a launch).
 int lookup_mode() {
     const char* v = getenv("SAMNERF_LOOKUP");
-    if (!v || !*v) return kLookPacked;
+    if (!v || !*v) return kLookAuto;
     if (!strcmp(v, "ref")) return kLookRef;
     if (!strcmp(v, "box")) return kLookBox;
     if (!strcmp(v, "box4")) return kLookBox4;
@@ -1326,8 +1327,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
         const dim3 sg(xcd_blocks(div_up(N, 64)), 16);
         if (look == kLookRef) k_sgrid<32, kLookRef><<<sg, 256, 0, s>>>(sa);
         else if (look == kLookBox) k_sgrid<32, kLookBox><<<sg, 256, 0, s>>>(sa);
-        else if ((look == kLookBox4 || (look == kLookPacked && N >= kBox4MinRays && !getenv("SAMNERF_LOOKUP")))
-                 && box4_ok(gs))
+        else if ((look == kLookBox4 || (look == kLookAuto && N >= kBox4MinRays)) && box4_ok(gs))
             k_sgrid_box4<32><<<dim3(xcd_blocks(div_up(N, 64)), 4), 256, 0, s>>>(sa);
         else k_sgrid<32, kLookPacked><<<sg, 256, 0, s>>>(sa);
         if ((rc = check_launch("render"))) return rc;

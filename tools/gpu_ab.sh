@@ -29,17 +29,18 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   fatal $rc && exit $rc
 fi
 
-for m in ${MODES:-packed ref box}; do
-  SAMNERF_LOOKUP=$m timeout -k 10 300 python bench.py --cpu-rays 0 --ref-gpu-rays 0 --steps 20 > "$OUT/bench_$m.log" 2>&1
+lk() { [ "$1" = "default" ] && echo "" || echo "$1"; }
+for m in ${MODES:-default packed ref box4}; do
+  SAMNERF_LOOKUP=$(lk $m) timeout -k 10 300 python bench.py --cpu-rays 0 --ref-gpu-rays 0 --steps 20 > "$OUT/bench_$m.log" 2>&1
   rc=$?; echo "bench $m rc=$rc"; summ "$OUT/bench_$m.log"; fatal $rc && exit $rc
   for h in ${SWEEP_H:-}; do
-    SAMNERF_LOOKUP=$m timeout -k 10 200 python bench.py --H $h --cpu-rays 0 --ref-gpu-rays 0 --steps 30 > "$OUT/bench_${m}_h$h.log" 2>&1
+    SAMNERF_LOOKUP=$(lk $m) timeout -k 10 200 python bench.py --H $h --cpu-rays 0 --ref-gpu-rays 0 --steps 30 > "$OUT/bench_${m}_h$h.log" 2>&1
     rc=$?; echo "bench $m H=$h rc=$rc"; summ "$OUT/bench_${m}_h$h.log"; fatal $rc && exit $rc
   done
 done
 
 [ "${SKIP_PROF:-0}" = "1" ] && exit 0
-export SAMNERF_LOOKUP=${PROF_MODE:-packed}
+export SAMNERF_LOOKUP=$(lk ${PROF_MODE:-default})
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_trace" -o trace \
   -- python "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --cpu-rays 0 --ref-gpu-rays 0 > "$OUT/prof_trace.log" 2>&1

@@ -12,7 +12,7 @@ gathers here are 8-32 B per lane, a width the guide lists as uncalibrated.
 `hbm_bytes` applies the guide's correction (2 * FETCH + WRITE); the raw fetch
 is kept beside it.  Passes are separate runs (FETCH_SIZE needs 3 TCC slots,
 WRITE_SIZE 2).
-usage: python tools/summarize_prof.py --tag r1
+usage: python tools/summarize_prof.py --tag r1 [--pmc-dir pmc]
 """
 import argparse
 import collections
@@ -27,7 +27,7 @@ PROF = os.path.join(REPO, "profiles")
 
 STAGE_OF = {"k_snf": "prop0", "k_prop_sigma<128": "prop0", "k_prop_pdf<128": "prop0",
             "k_prop_sigma<64": "prop1", "k_prop_pdf<64": "prop1", "k_final": "final",
-            "k_sgrid<": "s_grid", "k_sam_head": "sam_head", "k_pack": "sam_head",
+            "k_sgrid<": "s_grid", "k_sgrid_box4": "s_grid", "k_sam_head": "sam_head", "k_pack": "sam_head",
             "k_get_rays": "get_rays", "k_put_tables": "tables"}
 
 
@@ -38,24 +38,29 @@ def stage(name):
     return None
 
 
-def pmc(path, counter):
+def pmc(root, counter):
+    """Per-kernel average of `counter` over every counter_collection.csv
+    under `root` (one rocprofv3 --pmc pass per directory)."""
+    import glob
     d = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter:
-            d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(path)):
+            if r["Counter_Name"] == counter:
+                d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in d.items()}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", default="r1")
+    ap.add_argument("--pmc-dir", default="pmc", help="under gpurun_out/ (tools/gpu_ab.sh writes pmc/)")
     a = ap.parse_args()
     os.makedirs(PROF, exist_ok=True)
     stats = os.path.join(OUT, "prof_trace", "trace_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(PROF, f"{a.tag}_kernel_stats.csv"))
-    fetch = pmc(os.path.join(OUT, "prof_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
-    write = pmc(os.path.join(OUT, "prof_write", "write_counter_collection.csv"), "WRITE_SIZE")
+    fetch = pmc(os.path.join(OUT, a.pmc_dir), "FETCH_SIZE")
+    write = pmc(os.path.join(OUT, a.pmc_dir), "WRITE_SIZE")
     rows, traffic = [], {}
     for k in sorted(set(fetch) | set(write)):
         s = stage(k)
