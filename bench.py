@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--mode", choices=["render", "train"], default="render",
                     help="render: cfg 3 view throughput (the headline metric); train: cfg 5 "
                          "SAM-feature distillation step (4096 rays, forward + backward + Adam)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo for rehearsals")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="all ranks on GPU 0 (rehearsal of the N-rank path on a one-GPU box)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -85,12 +88,18 @@ def setup_dist(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    return rank, world, torch.device("cuda", local if world > 1 else 0)
+        # --dist-backend gloo --share-gpu: a rehearsal of the multi-rank code
+        # path with every rank on GPU 0 (RCCL needs one GPU per rank)
+        dev_index = 0 if args.share_gpu else local
+        torch.cuda.set_device(dev_index)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
+        return rank, world, torch.device("cuda", dev_index)
+    torch.cuda.set_device(0)
+    return rank, world, torch.device("cuda", 0)
 
 
 def build_net(with_sam, device):
@@ -292,7 +301,7 @@ def main():
     dt = time.perf_counter() - t0
     lib().samnerf_set_stage_events(None, 0)
     if world > 1:
-        t = torch.tensor([dt], device=dev)
+        t = torch.tensor([dt], device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     stage_avg = {}          # per step: summed over the chunks of the rank's band

@@ -37,11 +37,27 @@ def unpack_outputs(tile, keys, widths):
     return res
 
 
+class _Done:
+    """Work handle of a collective that has already completed."""
+
+    def wait(self):
+        return True
+
+
 def _all_gather(buf_out, local, group, async_op=False):
-    """all_gather of equal-size row blocks into buf_out [world * n, C]."""
+    """all_gather of equal-size row blocks into buf_out [world * n, C].  With
+    RCCL (`nccl`) this is one all_gather_into_tensor over xGMI.  Under `gloo`
+    (CPU tests, and the single-GPU rehearsal of the multi-rank bench) device
+    tensors are staged through host memory, synchronously."""
     if dist.get_backend(group) == "nccl":
         return dist.all_gather_into_tensor(buf_out, local, group=group, async_op=async_op)
     world = dist.get_world_size(group)
+    if local.is_cuda:
+        host = buf_out.new_empty(buf_out.shape, device="cpu")
+        parts = list(host.chunk(world, 0))
+        dist.all_gather(parts, local.cpu(), group=group)
+        buf_out.copy_(host)
+        return _Done() if async_op else None
     parts = list(buf_out.chunk(world, 0))
     return dist.all_gather(parts, local, group=group, async_op=async_op)
 

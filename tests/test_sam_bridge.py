@@ -39,7 +39,7 @@ def test_sam_predict_hands_off_like_the_reference(case):
     assert np.array_equal(rec.coords.numpy(), g[f"c{case}_coords"])
     assert np.array_equal(rec.labels.numpy(), g[f"c{case}_labels"])
     assert np.array_equal(orig, g[f"c{case}_orig"]) and not rec.multimask
-    assert masks.shape == (1, H, W)
+    assert masks.shape == (1, H, W)          # (fixture: 16 channels; the resize is per channel)
 
 
 def test_rendered_feature_map_layout():

@@ -49,7 +49,7 @@ def main():
     cases = [(512, 512, 64, 64, [[100, 300]]), (480, 640, 48, 64, [[10, 20], [300, 200]]),
              (640, 360, 64, 36, None)]
     for i, (H, W, h, w, pts) in enumerate(cases):
-        feats = torch.randn(1, 256, h, w, generator=g)
+        feats = torch.randn(1, 16, h, w, generator=g)          # the resize is per channel
         rec = Recorder()
         fake = types.SimpleNamespace(sam_predictor=rec, device="cpu")
         np.random.seed(100 + i)
