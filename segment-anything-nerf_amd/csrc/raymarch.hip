@@ -426,17 +426,25 @@ __device__ __forceinline__ floatx16 mfma3(uint4 ah, uint4 al, uint4 bh, uint4 bl
 // (size-1) (hashed), built from per-axis terms.  All 8*NL corner loads are
 // issued before the first is consumed (one memory round trip per call; the
 // compiler otherwise waits for each level before issuing the next).
+// Gathered corner rows of NL levels (both channels) and their fractions:
+// the issue half of gather_levels_c2, so a caller can start the loads of the
+// next sample before consuming them (k_final's cross-iteration prefetch).
 template <int NL>
-__device__ __forceinline__ void gather_levels_c2(const float2* __restrict__ emb, const LevelDesc* d,
-                                                 float ux, float uy, float uz, float* f) {
-    uint32_t row[NL][8];
+struct GatherC2 {
+    float2 e[NL][8];
     float fx[NL], fy[NL], fz[NL];
+};
+
+template <int NL>
+__device__ __forceinline__ void gather_issue_c2(const float2* __restrict__ emb, const LevelDesc* d,
+                                                float ux, float uy, float uz, GatherC2<NL>& g) {
+    uint32_t row[NL][8];
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
         uint32_t cx, cy, cz;
-        locate_axis(ux, d[l].res, cx, fx[l]);
-        locate_axis(uy, d[l].res, cy, fy[l]);
-        locate_axis(uz, d[l].res, cz, fz[l]);
+        locate_axis(ux, d[l].res, cx, g.fx[l]);
+        locate_axis(uy, d[l].res, cy, g.fy[l]);
+        locate_axis(uz, d[l].res, cz, g.fz[l]);
         const uint32_t top = d[l].res - 1u;
         const bool hashed = d[l].flags & kHashed;
         const uint32_t my = hashed ? kPrime1 : d[l].res, mz = hashed ? kPrime2 : d[l].res * d[l].res;
@@ -452,26 +460,43 @@ __device__ __forceinline__ void gather_levels_c2(const float2* __restrict__ emb,
     }
     // 32-bit byte offsets from the uniform table base (saddr loads)
     const char* base = reinterpret_cast<const char*>(emb);
-    float2 e[NL][8];
 #pragma unroll
     for (int l = 0; l < NL; ++l)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) e[l][c] = *reinterpret_cast<const float2*>(base + row[l][c]);
+        for (int c = 0; c < 8; ++c) g.e[l][c] = *reinterpret_cast<const float2*>(base + row[l][c]);
+}
+
+template <int NL>
+__device__ __forceinline__ void gather_finish_c2(const GatherC2<NL>& g, float* f) {
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
         float f0 = 0.0f, f1 = 0.0f;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            const float wx = (c & 1) ? fx[l] : 1.0f - fx[l];
-            const float wy = (c & 2) ? fy[l] : 1.0f - fy[l];
-            const float wz = (c & 4) ? fz[l] : 1.0f - fz[l];
+            const float wx = (c & 1) ? g.fx[l] : 1.0f - g.fx[l];
+            const float wy = (c & 2) ? g.fy[l] : 1.0f - g.fy[l];
+            const float wz = (c & 4) ? g.fz[l] : 1.0f - g.fz[l];
             const float w = (wx * wy) * wz;
-            f0 = __builtin_fmaf(w, e[l][c].x, f0);
-            f1 = __builtin_fmaf(w, e[l][c].y, f1);
+            f0 = __builtin_fmaf(w, g.e[l][c].x, f0);
+            f1 = __builtin_fmaf(w, g.e[l][c].y, f1);
         }
         f[2 * l] = f0;
         f[2 * l + 1] = f1;
     }
+}
+
+// Trilinear lookup of both channels of NL L16C2 levels whose descriptors
+// differ between the half-waves (lane-varying; no divergent branch): the row
+// of corner (x, y, z) is x + y*res + z*res^2 (dense) or (x ^ y*P1 ^ z*P2) &
+// (size-1) (hashed), built from per-axis terms.  All 8*NL corner loads are
+// issued before the first is consumed (one memory round trip per call; the
+// compiler otherwise waits for each level before issuing the next).
+template <int NL>
+__device__ __forceinline__ void gather_levels_c2(const float2* __restrict__ emb, const LevelDesc* d,
+                                                 float ux, float uy, float uz, float* f) {
+    GatherC2<NL> g;
+    gather_issue_c2<NL>(emb, d, ux, uy, uz, g);
+    gather_finish_c2<NL>(g, f);
 }
 
 __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const LevelDesc& q, bool hi) {
@@ -491,7 +516,7 @@ __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const Leve
 // final; per-slot partial sums of w, w*t and w*features are added at the end.
 // S > 1 only serves small N (one rank's share of a view): S-times more waves,
 // while a wave still gathers at adjacent samples of neighbouring rays.
-template <int T, int S>
+template <int T, int S, bool PF>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_final(FinalArgs a) {
     static_assert(S == 1 || S == 2 || S == 4, "segments per ray");
     constexpr int R = 32 / S, TS = T / S;
@@ -534,19 +559,54 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
     for (int q = 0; q < 8; ++q) fg[q] = 0.0f;
 
-    for (int i = 0; i < TS; ++i) {
+    // PF: the first k-block's gathers of sample i + 1 are issued before the
+    // layer-2/3 MFMAs of sample i, so their latency hides behind them
+    // level descriptors of k-block kb for this half-wave (scalar loads +
+    // selects, re-evaluated where used rather than held in VGPRs)
+    auto levels = [&](int kb, LevelDesc* dl) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dl[q] = select_level(G->lv[8 * kb + q], G->lv[8 * kb + 4 + q], hh != 0);
+    };
+    // rb_prev of sample i is rb_next of sample i - 1 when S == 1 (same bits;
+    // saves a division), recomputed from the bins otherwise
+    auto position = [&](int i, float& rbp, float& rbn, float& ux, float& uy, float& uz) {
         const int k = i * S + seg;
-        if (S > 1 && i > 0) rb_prev = real_bin(sn, sf, a.bins_in[(size_t)k * N + rr]);
-        const float rb_next = real_bin(sn, sf, a.bins_in[(size_t)(k + 1) * N + rr]);
-        const float t = (rb_next + rb_prev) / 2.0f;
+        if (S > 1 || i == 0) rbp = real_bin(sn, sf, a.bins_in[(size_t)k * N + rr]);
+        rbn = real_bin(sn, sf, a.bins_in[(size_t)(k + 1) * N + rr]);
+        const float t = (rbn + rbp) / 2.0f;
         float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
         contract3(x, y, z);
-        const float ux = a.gs(x), uy = a.gs(y), uz = a.gs(z);
+        ux = a.gs(x);
+        uy = a.gs(y);
+        uz = a.gs(z);
         if (sample_writer) {
             a.u_out[((size_t)k * 3 + 0) * N + r] = ux;
             a.u_out[((size_t)k * 3 + 1) * N + r] = uy;
             a.u_out[((size_t)k * 3 + 2) * N + r] = uz;
         }
+    };
+    GatherC2<4> pre;                                      // PF: kb 0 of the current sample
+    float p_rbp = rb_prev, p_rbn = 0.0f, p_ux = 0.0f, p_uy = 0.0f, p_uz = 0.0f;
+    if constexpr (PF) {
+        LevelDesc dl[4];
+        levels(0, dl);
+        position(0, p_rbp, p_rbn, p_ux, p_uy, p_uz);
+        gather_issue_c2<4>(emb, dl, p_ux, p_uy, p_uz, pre);
+    }
+
+    for (int i = 0; i < TS; ++i) {
+        const int k = i * S + seg;
+        float rb_next, ux, uy, uz;
+        if constexpr (PF) {
+            rb_prev = p_rbp;
+            rb_next = p_rbn;
+            ux = p_ux;
+            uy = p_uy;
+            uz = p_uz;
+        } else {
+            position(i, rb_prev, rb_next, ux, uy, uz);
+        }
+        const float t = (rb_next + rb_prev) / 2.0f;
         // weight fragments are re-read from LDS each sample rather than
         // hoisted into VGPRs for the whole loop (opaque offset defeats LICM)
         int wo = lane;
@@ -558,14 +618,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             float f[8];
-            LevelDesc dl[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) dl[i] = select_level(G->lv[8 * kb + i], G->lv[8 * kb + 4 + i], hh != 0);
-            gather_levels_c2<4>(emb, dl, ux, uy, uz, f);
+            if (PF && kb == 0) {
+                gather_finish_c2<4>(pre, f);
+            } else {
+                LevelDesc dl[4];
+                levels(kb, dl);
+                gather_levels_c2<4>(emb, dl, ux, uy, uz, f);
+            }
             uint4 bh, bl;
             split8(f, bh, bl);
             h1a = mfma3(FH[(kF1 + 2 * kb) * 64], FL[(kF1 + 2 * kb) * 64], bh, bl, h1a);
             h1b = mfma3(FH[(kF1 + 2 * kb + 1) * 64], FL[(kF1 + 2 * kb + 1) * 64], bh, bl, h1b);
+        }
+        if constexpr (PF) {
+            if (i + 1 < TS) {
+                LevelDesc dl[4];
+                levels(0, dl);
+                p_rbp = p_rbn;                            // S == 1: next rb_prev = this rb_next
+                position(i + 1, p_rbp, p_rbn, p_ux, p_uy, p_uz);
+                gather_issue_c2<4>(emb, dl, p_ux, p_uy, p_uz, pre);
+            }
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -1081,6 +1153,15 @@ int prop_occ() {
 // 0.94 vs 1.05 ms at 262,144 rays, 0.25 vs 0.21 ms at 32,768.
 constexpr uint32_t kBox4MinRays = 131072;
 
+// k_final's cross-sample prefetch of its first k-block's gathers pays where
+// the kernel is latency-bound (S >= 2: one rank's share of a view, 0.29 ->
+// 0.26 ms at 32K rays) and not at S = 1, where the held loads spill (1.05 ->
+// 1.41 ms).  SAMNERF_FINAL_PF = 0 | 1 forces it off / on.
+bool final_prefetch(int seg) {
+    const char* v = getenv("SAMNERF_FINAL_PF");
+    return v ? atoi(v) != 0 : seg > 1;
+}
+
 // k_sgrid_box4 packs cell indices and extents into 10 bits
 bool box4_ok(const GridDesc<16>& g) {
     for (int l = 0; l < 16; ++l)
@@ -1312,9 +1393,17 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     // (SAMNERF_FINAL_S = 1 | 2 | 4 overrides, for measurement)
     const char* fs = getenv("SAMNERF_FINAL_S");
     const int seg = fs ? atoi(fs) : (N >= 65536u ? 1 : N >= 32768u ? 2 : 4);
-    if (seg == 1) k_final<32, 1><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
-    else if (seg == 2) k_final<32, 2><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
-    else k_final<32, 4><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
+    const bool pf = final_prefetch(seg);
+    if (seg == 1) {
+        if (pf) k_final<32, 1, true><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
+        else k_final<32, 1, false><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
+    } else if (seg == 2) {
+        if (pf) k_final<32, 2, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
+        else k_final<32, 2, false><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
+    } else {
+        if (pf) k_final<32, 4, true><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
+        else k_final<32, 4, false><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
+    }
 
     if (m->with_sam) {
         SgridArgs sa{};

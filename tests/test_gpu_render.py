@@ -281,3 +281,26 @@ def test_sam_feature_handoff_stays_on_device(hip_lib, cuda):
     assert rec.features.is_cuda and rec.coords.is_cuda
     assert torch.equal(rec.features, prepare_sam_features(out["samvit"].view(64, 64, 256)))
     assert orig.tolist() == [[256, 256]] and masks.shape == (1, 512, 512)
+
+
+@pytest.mark.parametrize("n", [70000, 40000, 9000])
+def test_final_prefetch_bit_identical(hip_lib, cuda, monkeypatch, n):
+    """k_final with and without the cross-sample prefetch of its first
+    k-block's gathers (SAMNERF_FINAL_PF), for each ray-segment form S = 1, 2,
+    4 (chosen by N): identical bits."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer, ROW
+    spec = synth.ModelSpec(with_sam=True)
+    net = make_net(spec, synth.make_params(spec, seed=23, emb_scale=0.5, ln_jitter=0.1), cuda)
+    pose, intr = synth.gui_camera(512, 160, rot=synth.random_rotation(11))
+    ro, rd = ops.get_rays(pose, intr, 160, 512, device=cuda)
+    fr = FusedRenderer(net)
+    outs = []
+    for pf in ("0", "1"):
+        monkeypatch.setenv("SAMNERF_FINAL_PF", pf)
+        rows = torch.empty(n, ROW, device=cuda)
+        o = fr.render(ro[:n], rd[:n], rows=rows)
+        o["rows"] = rows
+        outs.append(o)
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
