@@ -72,9 +72,11 @@ def parse():
                          "overlap view i's (each stream has its own workspace).  0 = 1 on one GPU "
                          "(+2%% measured, and per-kernel HIP-event times stay unshared for the "
                          "roofline), 2 for 2-4 ranks, 3 for 8 (one rank's 32K-ray share: +16%%)")
-    ap.add_argument("--mode", choices=["render", "train"], default="render",
+    ap.add_argument("--mode", choices=["render", "train", "gui"], default="render",
                     help="render: cfg 3 view throughput (the headline metric); train: cfg 5 "
-                         "SAM-feature distillation step (4096 rays, forward + backward + Adam)")
+                         "SAM-feature distillation step (4096 rays, forward + backward + Adam); "
+                         "gui: the reference GUI's frame (readme.md:5) -- 512x512 RGB + 64x64 "
+                         "SAM-feature render")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo for rehearsals")
     ap.add_argument("--share-gpu", action="store_true",
                     help="all ranks on GPU 0 (rehearsal of the N-rank path on a one-GPU box)")
@@ -219,11 +221,56 @@ def train_main(args, dev):
     print(json.dumps(rec), flush=True)
 
 
+def gui_main(args, dev):
+    """The reference GUI's per-frame render work (nerf/gui.py:143-161 ->
+    utils.py:1647-1712 test_gui -> test_step): the H x W view without
+    features (return_feats=0: the reference still computes and drops them,
+    the fused path skips them) plus the 64 x 64 feature rays for the SAM
+    decoder.  readme.md:5 quotes 5 FPS on a V100 for this loop including the
+    decoder (not run here)."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer
+    from oracle import synth
+    net, _, _ = build_net(True, dev)
+    r = FusedRenderer(net)
+    H, W = args.H, args.W
+    pose, intr = synth.gui_camera(W, H)
+    pose_lr, intr_lr = synth.gui_camera(64, 64)
+
+    def frame():
+        ro, rd = ops.get_rays(pose, intr, H, W, device=dev)
+        img = r.render(ro, rd, feats=False)
+        ro2, rd2 = ops.get_rays(pose_lr, intr_lr, 64, 64, device=dev)
+        return img, r.render(ro2, rd2)
+
+    for _ in range(args.warmup):
+        frame()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    rays = H * W + 64 * 64
+    print(json.dumps({
+        "metric": "GUI frame: 512x512 RGB + 64x64 SAM-feature render (frames/s)", "value": 1.0 / dt,
+        "unit": "frames/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt * 1e3, "higher_is_better": True, "rays_per_s": rays / dt,
+        "dtype": "fp32 (SAM head: bf16x3 split-precision MFMA, fp32 accumulate)",
+        "data": "synthetic (random-init weights of the reference architecture, GUI camera)",
+        "config": {"workload": f"{H}x{W} RGB (features skipped) + 64x64 with 256-d SAM features",
+                   "reference": "readme.md:5: 5 FPS on V100 incl. the SAM decoder"},
+        "vs_baseline": None}), flush=True)
+
+
 def main():
     args = parse()
     if args.mode == "train":
         torch.cuda.set_device(0)
         return train_main(args, torch.device("cuda", 0))
+    if args.mode == "gui":
+        torch.cuda.set_device(0)
+        return gui_main(args, torch.device("cuda", 0))
     rank, world, dev = setup_dist(args)
     from samnerf_amd import ops
     from samnerf_amd._lib import lib

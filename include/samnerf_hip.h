@@ -185,8 +185,10 @@ size_t samnerf_render_workspace_size(const samnerf_model* model, uint32_t N);
  * SkipConnMLP + LayerNorm head.
  *   rays_o, rays_d [N,3]; cam_near_far [N,2] or [1,2] (n_cnf rows) or NULL;
  *   bg_color: scalar background (renderer.py:239-240, default 1);
- *   image [N,3], depth [N], weights_sum [N]; samvit [N,256] (NULL unless
- *   with_sam); feature_rows [N,164] optional: the per-ray head input
+ *   image [N,3], depth [N], weights_sum [N]; samvit [N,256] (with_sam; NULL
+ *   = features not wanted: the s_grid composite and the head are skipped --
+ *   renderer.py computes and drops them when return_feats == 0);
+ *   feature_rows [N,164] optional: the per-ray head input
  *   cat(f_sam, f_image, image, depth) (+1 pad), kept for training.
  * Outputs are written, never accumulated. */
 int samnerf_render_forward(const samnerf_model* model, const float* rays_o,

@@ -1301,7 +1301,10 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
         return fail(SAMNERF_EINVAL, "render: null pointer");
     if (m->num_steps[0] != 128 || m->num_steps[1] != 64 || m->num_steps[2] != 32)
         return fail(SAMNERF_EINVAL, "render: fused path is built for num_steps = [128, 64, 32]");
-    if (m->with_sam && !samvit) return fail(SAMNERF_EINVAL, "render: with_sam needs samvit");
+    // with_sam and samvit == NULL: the caller does not want the features
+    // (renderer.py computes them and drops them when return_feats == 0), so the
+    // s_grid composite runs only if feature_rows are requested and the head not
+    // at all
     if (cam_near_far && n_cnf != 1 && n_cnf != N)
         return fail(SAMNERF_EINVAL, "render: cam_near_far must have 1 or N rows");
     if (N == 0) return SAMNERF_OK;
@@ -1387,7 +1390,8 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.image = image;
     fa.depth = depth;
     fa.wsum = weights_sum;
-    fa.rows = m->with_sam || feature_rows ? rows : nullptr;
+    const bool sam_rows = m->with_sam && (samvit || feature_rows);
+    fa.rows = sam_rows || feature_rows ? rows : nullptr;
     mark_stage(2, s);
     // segments per ray: enough waves to fill the resident slots (2 per SIMD)
     // (SAMNERF_FINAL_S = 1 | 2 | 4 overrides, for measurement)
@@ -1405,7 +1409,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
         else k_final<32, 4, false><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
     }
 
-    if (m->with_sam) {
+    if (sam_rows) {
         SgridArgs sa{};
         sa.N = N;
         sa.grid = gs;
@@ -1421,7 +1425,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
         else k_sgrid<32, kLookPacked><<<sg, 256, 0, s>>>(sa);
         if ((rc = check_launch("render"))) return rc;
         mark_stage(4, s);
-        rc = sam_head_forward(m, rows, N, samvit, w.packed, s);
+        if (samvit) rc = sam_head_forward(m, rows, N, samvit, w.packed, s);
         mark_stage(5, s);
         return rc;
     }

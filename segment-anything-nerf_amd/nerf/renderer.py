@@ -180,7 +180,8 @@ class NeRFRenderer(nn.Module):
             from samnerf_amd.fused import FusedRenderer
             if self._fused is None or self._fused.net is not self:
                 self._fused = FusedRenderer(self)
-            out = self._fused.render(rays_o, rays_d, cam_near_far, bg_color)
+            out = self._fused.render(rays_o, rays_d, cam_near_far, bg_color,
+                                     feats=return_feats > 0)
             samvit = out.pop("samvit", None)
             if return_feats > 0 and samvit is not None:
                 out["samvit"] = samvit.view(H, W, -1) if H is not None else samvit

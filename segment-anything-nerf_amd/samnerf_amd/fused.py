@@ -119,11 +119,12 @@ class FusedRenderer:
     # -------------------------------------------------------------- render --
     @torch.no_grad()
     def render(self, rays_o, rays_d, cam_near_far=None, bg_color=None, rows=None,
-               keep_workspace=False):
+               keep_workspace=False, feats=True):
         """rays_o, rays_d [N,3] (CUDA fp32) -> dict(image [N,3], depth [N],
-        weights_sum [N], samvit [N,256] if with_sam).  `rows` (optional
-        [N,164] tensor) receives the head input cat(f_sam, f_image, image,
-        depth)."""
+        weights_sum [N], samvit [N,256] if with_sam and feats).  `rows`
+        (optional [N,164] tensor) receives the head input cat(f_sam, f_image,
+        image, depth).  feats=False skips the SAM-feature stages (the
+        reference computes and discards them when return_feats == 0)."""
         rays_o = rays_o.contiguous().float()
         rays_d = rays_d.contiguous().float()
         N = rays_o.shape[0]
@@ -141,7 +142,7 @@ class FusedRenderer:
         image = torch.empty(N, 3, device=dev)
         depth = torch.empty(N, device=dev)
         wsum = torch.empty(N, device=dev)
-        samvit = torch.empty(N, 256, device=dev) if m.with_sam else None
+        samvit = torch.empty(N, 256, device=dev) if (m.with_sam and feats) else None
         cnf = None
         n_cnf = 0
         if cam_near_far is not None:

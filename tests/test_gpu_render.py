@@ -304,3 +304,18 @@ def test_final_prefetch_bit_identical(hip_lib, cuda, monkeypatch, n):
         outs.append(o)
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+def test_render_without_features_matches(hip_lib, cuda):
+    """return_feats=0 skips the s_grid composite and the head (the reference
+    computes and drops them); the RGB outputs are the same bits."""
+    from samnerf_amd import ops
+    spec = synth.ModelSpec(with_sam=True, grid_log2=14, s_grid_log2=14, prop_log2=12)
+    net = make_net(spec, synth.make_params(spec, seed=31, emb_scale=0.5, ln_jitter=0.1), cuda)
+    pose, intr = synth.gui_camera(64, 64, rot=synth.random_rotation(12))
+    ro, rd = ops.get_rays(pose, intr, 64, 64, device=cuda)
+    a = net.render(ro, rd, return_feats=1)
+    b = net.render(ro, rd, return_feats=0)
+    assert "samvit" in a and "samvit" not in b
+    for k in ("image", "depth", "weights_sum"):
+        assert torch.equal(a[k], b[k]), k
