@@ -466,22 +466,40 @@ __device__ __forceinline__ void gather_issue_c2(const float2* __restrict__ emb, 
         for (int c = 0; c < 8; ++c) g.e[l][c] = *reinterpret_cast<const float2*>(base + row[l][c]);
 }
 
-template <int NL>
+// Weighted corner sums with the reference's weights (wx * wy) * wz.  PK: both
+// channels on one v_pk_fma_f32 per corner (each lane the scalar fma: same
+// bits).  The forms schedule differently: PK measured faster in k_final's
+// S = 1 form (1.04 -> 1.00 ms per view), scalar in its prefetching S = 2 form
+// (0.26 vs 0.29 ms at 32K rays).
+template <int NL, bool PK = false>
 __device__ __forceinline__ void gather_finish_c2(const GatherC2<NL>& g, float* f) {
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
-        float f0 = 0.0f, f1 = 0.0f;
+        if constexpr (PK) {
+            const float wx0 = 1.0f - g.fx[l], wy0 = 1.0f - g.fy[l], wz0 = 1.0f - g.fz[l];
+            const float wxy[4] = {wx0 * wy0, g.fx[l] * wy0, wx0 * g.fy[l], g.fx[l] * g.fy[l]};
+            f2v acc = {0.0f, 0.0f};
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const float wx = (c & 1) ? g.fx[l] : 1.0f - g.fx[l];
-            const float wy = (c & 2) ? g.fy[l] : 1.0f - g.fy[l];
-            const float wz = (c & 4) ? g.fz[l] : 1.0f - g.fz[l];
-            const float w = (wx * wy) * wz;
-            f0 = __builtin_fmaf(w, g.e[l][c].x, f0);
-            f1 = __builtin_fmaf(w, g.e[l][c].y, f1);
+            for (int c = 0; c < 8; ++c) {
+                const float w = wxy[c & 3] * ((c & 4) ? g.fz[l] : wz0);
+                acc = __builtin_elementwise_fma(f2v{w, w}, f2v{g.e[l][c].x, g.e[l][c].y}, acc);
+            }
+            f[2 * l] = acc.x;
+            f[2 * l + 1] = acc.y;
+        } else {
+            float f0 = 0.0f, f1 = 0.0f;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float wx = (c & 1) ? g.fx[l] : 1.0f - g.fx[l];
+                const float wy = (c & 2) ? g.fy[l] : 1.0f - g.fy[l];
+                const float wz = (c & 4) ? g.fz[l] : 1.0f - g.fz[l];
+                const float w = (wx * wy) * wz;
+                f0 = __builtin_fmaf(w, g.e[l][c].x, f0);
+                f1 = __builtin_fmaf(w, g.e[l][c].y, f1);
+            }
+            f[2 * l] = f0;
+            f[2 * l + 1] = f1;
         }
-        f[2 * l] = f0;
-        f[2 * l + 1] = f1;
     }
 }
 
@@ -491,12 +509,12 @@ __device__ __forceinline__ void gather_finish_c2(const GatherC2<NL>& g, float* f
 // (size-1) (hashed), built from per-axis terms.  All 8*NL corner loads are
 // issued before the first is consumed (one memory round trip per call; the
 // compiler otherwise waits for each level before issuing the next).
-template <int NL>
+template <int NL, bool PK = false>
 __device__ __forceinline__ void gather_levels_c2(const float2* __restrict__ emb, const LevelDesc* d,
                                                  float ux, float uy, float uz, float* f) {
     GatherC2<NL> g;
     gather_issue_c2<NL>(emb, d, ux, uy, uz, g);
-    gather_finish_c2<NL>(g, f);
+    gather_finish_c2<NL, PK>(g, f);
 }
 
 __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const LevelDesc& q, bool hi) {
@@ -619,11 +637,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         for (int kb = 0; kb < 2; ++kb) {
             float f[8];
             if (PF && kb == 0) {
-                gather_finish_c2<4>(pre, f);
+                gather_finish_c2<4, S == 1>(pre, f);
             } else {
                 LevelDesc dl[4];
                 levels(kb, dl);
-                gather_levels_c2<4>(emb, dl, ux, uy, uz, f);
+                gather_levels_c2<4, S == 1>(emb, dl, ux, uy, uz, f);
             }
             uint4 bh, bl;
             split8(f, bh, bl);
@@ -1153,13 +1171,13 @@ int prop_occ() {
 // 0.94 vs 1.05 ms at 262,144 rays, 0.25 vs 0.21 ms at 32,768.
 constexpr uint32_t kBox4MinRays = 131072;
 
-// k_final's cross-sample prefetch of its first k-block's gathers pays where
-// the kernel is latency-bound (S >= 2: one rank's share of a view, 0.29 ->
-// 0.26 ms at 32K rays) and not at S = 1, where the held loads spill (1.05 ->
+// k_final's cross-sample prefetch of its first k-block's gathers: 0.29 ->
+// 0.26 ms at one rank's 32K-ray share (S = 2), 1.01 -> 0.99 ms on a full view
+// (S = 1, packed corner sums; with the scalar sums the held loads spilled,
 // 1.41 ms).  SAMNERF_FINAL_PF = 0 | 1 forces it off / on.
 bool final_prefetch(int seg) {
     const char* v = getenv("SAMNERF_FINAL_PF");
-    return v ? atoi(v) != 0 : seg > 1;
+    return v ? atoi(v) != 0 : true;
 }
 
 // k_sgrid_box4 packs cell indices and extents into 10 bits
