@@ -802,17 +802,15 @@ struct SgridArgs {
 // gather), and the quarters are added through LDS.  A wave is 64 rays at one
 // (level, sample), so corner rows are shared across lanes.
 // MODE: kLookPacked (lookup_level3), kLookRef (lookup_level3_ref, scalar
-// accumulation), kLookBox (wave_box.h: each distinct corner row of the wave
-// read once through LDS).  All three give identical bits.
-constexpr int kLookPacked = 0, kLookRef = 1, kLookBox = 2, kLookBox4 = 3;
+// accumulation); k_sgrid_box4 below is the de-duplicated form.  All give
+// identical bits.
+constexpr int kLookPacked = 0, kLookRef = 1, kLookBox4 = 3;
 constexpr int kLookAuto = 4;     // host-side only: packed, k_sgrid by launch size
-constexpr uint32_t kSgridBoxCap = 256;      // rows of 32 B per wave (8 KiB)
 
 template <int T, int MODE>
 __global__ void __launch_bounds__(256) k_sgrid(SgridArgs a) {
     constexpr int TQ = T / 4;
     __shared__ float part[3][8][64];
-    __shared__ float4 boxes[MODE == kLookBox ? 4 : 1][MODE == kLookBox ? kSgridBoxCap * 2 : 1];
     const uint32_t lane = threadIdx.x & 63u, q = threadIdx.x >> 6;
     const uint32_t r = xcd_chunk(blockIdx.x, (a.N + 63u) / 64u) * 64u + lane;   // gridDim.x % 8 == 0
     const uint32_t level = blockIdx.y;
@@ -839,18 +837,7 @@ __global__ void __launch_bounds__(256) k_sgrid(SgridArgs a) {
 #pragma unroll
             for (int c = 0; c < 8; ++c) acc[c] = acc[c] + w * f[c];
         } else {
-            if constexpr (MODE == kLookBox) {
-                float* slice = reinterpret_cast<float*>(boxes[q]);
-                const Box b = level_box(lv, wave_urange(ux, uy, uz));
-                if (b.n <= kSgridBoxCap) {
-                    stage_box<8>(reinterpret_cast<const char*>(a.grid.emb), lv, b, slice, lane);
-                    lookup_level3_box<8>(a.grid.emb, lv, b, slice, ux, uy, uz, f);
-                } else {
-                    lookup_level3<8>(a.grid.emb, lv, ux, uy, uz, f);
-                }
-            } else {
-                lookup_level3<8>(a.grid.emb, lv, ux, uy, uz, f);
-            }
+            lookup_level3<8>(a.grid.emb, lv, ux, uy, uz, f);
             const f2v wv = {w, w};            // acc + w * f, two channels per packed mul / add
 #pragma unroll
             for (int c = 0; c < 8; c += 2) {
@@ -1144,7 +1131,7 @@ int lookup_mode() {
     const char* v = getenv("SAMNERF_LOOKUP");
     if (!v || !*v) return kLookAuto;
     if (!strcmp(v, "ref")) return kLookRef;
-    if (!strcmp(v, "box")) return kLookBox;
+    if (!strcmp(v, "box")) return kLookBox4;
     if (!strcmp(v, "box4")) return kLookBox4;
     return kLookPacked;
 }
@@ -1437,7 +1424,6 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
         mark_stage(3, s);
         const dim3 sg(xcd_blocks(div_up(N, 64)), 16);
         if (look == kLookRef) k_sgrid<32, kLookRef><<<sg, 256, 0, s>>>(sa);
-        else if (look == kLookBox) k_sgrid<32, kLookBox><<<sg, 256, 0, s>>>(sa);
         else if ((look == kLookBox4 || (look == kLookAuto && N >= kBox4MinRays)) && box4_ok(gs))
             k_sgrid_box4<32><<<dim3(xcd_blocks(div_up(N, 64)), 4), 256, 0, s>>>(sa);
         else k_sgrid<32, kLookPacked><<<sg, 256, 0, s>>>(sa);

@@ -10,11 +10,11 @@
 //   2. per level, the cell range of that range is exact (locate_axis is
 //      monotonic in u), so the box of corner cells [x0, x1] x [y0, y1] x
 //      [z0, z1] holds every corner any lane needs;
-//   3. if the box has at most CAP rows, the wave loads it once into its own
-//      LDS slice (box cell j = slot j, x fastest) and every lane reads its 8
-//      corners from LDS; a bigger box takes the direct gathers.
+//   3. if the box has at most CAP slots, the wave loads it once into its own
+//      LDS slice and every lane reads its 8 corners from LDS; a bigger box
+//      takes the direct gathers.
 // Rows, weights and FMA order are lookup_level3's, so results are
-// bit-identical to the direct path.  A lane whose corners fall outside the
+// bit-identical to the direct path (k_sgrid_box4 in raymarch.hip).  A lane whose corners fall outside the
 // box anyway (a NaN position clamps to cell 0, and fminf/fmaxf skip NaN in
 // the range) gathers directly.
 #pragma once
@@ -80,118 +80,6 @@ __device__ __forceinline__ uint32_t cell_of(float u, uint32_t res) {
     float p = __builtin_fmaf(u, (float)res, -0.5f);
     p = fminf(fmaxf(p, 0.0f), (float)(res - 1u));
     return (uint32_t)floorf(p);
-}
-
-// Corner-cell box of one level: cells x0 .. x0 + ex - 1, etc.
-struct Box {
-    uint32_t x0, y0, z0, ex, ey, ez, exy, n;
-};
-
-__device__ __forceinline__ Box level_box(const LevelDesc& d, const URange& u) {
-    const uint32_t top = d.res - 1u;
-    Box b;
-    b.x0 = cell_of(u.lo[0], d.res);
-    b.y0 = cell_of(u.lo[1], d.res);
-    b.z0 = cell_of(u.lo[2], d.res);
-    const uint32_t x1 = min(cell_of(u.hi[0], d.res) + 1u, top);
-    const uint32_t y1 = min(cell_of(u.hi[1], d.res) + 1u, top);
-    const uint32_t z1 = min(cell_of(u.hi[2], d.res) + 1u, top);
-    b.ex = x1 - b.x0 + 1u;
-    b.ey = y1 - b.y0 + 1u;
-    b.ez = z1 - b.z0 + 1u;
-    b.exy = b.ex * b.ey;
-    b.n = b.exy * b.ez;
-    return b;
-}
-
-// q = j / d, r = j % d for j, d < 2^16: float estimate, one fix-up step.
-__device__ __forceinline__ void small_divmod(uint32_t j, uint32_t d, float inv_d, uint32_t& q,
-                                             uint32_t& r) {
-    q = (uint32_t)((float)j * inv_d);
-    int rr = (int)j - (int)(q * d);
-    if (rr < 0) { --q; rr += (int)d; }
-    if (rr >= (int)d) { ++q; rr -= (int)d; }
-    r = (uint32_t)rr;
-}
-
-// Load the b.n rows of the box into `slice` (C floats per row), each once.
-template <int C>
-__device__ __forceinline__ void stage_box(const char* __restrict__ base, const LevelDesc& d,
-                                          const Box& b, float* slice, uint32_t lane) {
-    const float inv_exy = 1.0f / (float)b.exy, inv_ex = 1.0f / (float)b.ex;
-    for (uint32_t j = lane; j < b.n; j += 64u) {
-        uint32_t bz, rem, by, bx;
-        small_divmod(j, b.exy, inv_exy, bz, rem);
-        small_divmod(rem, b.ex, inv_ex, by, bx);
-        const uint32_t row = dense_or_hash_row(b.x0 + bx, b.y0 + by, b.z0 + bz, d);
-        float e[C];
-        load_row_b<C>(base, (d.off + row) * (uint32_t)(C * 4), e);
-        if constexpr (C == 2) {
-            *reinterpret_cast<float2*>(slice + j * 2u) = make_float2(e[0], e[1]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < C; i += 4)
-                *reinterpret_cast<float4*>(slice + j * C + i) = make_float4(e[i], e[i + 1], e[i + 2], e[i + 3]);
-        }
-    }
-}
-
-// Trilinear lookup of one level from a staged box (lookup_level3's rows,
-// weights and FMA order); lanes outside the box gather directly.
-template <int C>
-__device__ __forceinline__ void lookup_level3_box(const float* __restrict__ emb, const LevelDesc& d,
-                                                  const Box& b, const float* slice, float ux, float uy,
-                                                  float uz, float* acc) {
-    uint32_t cx, cy, cz;
-    float fx, fy, fz;
-    locate_axis(ux, d.res, cx, fx);
-    locate_axis(uy, d.res, cy, fy);
-    locate_axis(uz, d.res, cz, fz);
-    const uint32_t top = d.res - 1u;
-    const uint32_t nx = min(cx + 1u, top), ny = min(cy + 1u, top), nz = min(cz + 1u, top);
-    const uint32_t lx0 = cx - b.x0, lx1 = nx - b.x0;
-    const uint32_t ly0 = cy - b.y0, ly1 = ny - b.y0;
-    const uint32_t lz0 = cz - b.z0, lz1 = nz - b.z0;
-    // unsigned: a cell below the box start wraps to a huge offset
-    const bool inside = lx0 < b.ex && lx1 < b.ex && ly0 < b.ey && ly1 < b.ey && lz0 < b.ez && lz1 < b.ez;
-    if (!inside) {
-        lookup_level3<C>(emb, d, ux, uy, uz, acc);
-        return;
-    }
-    const uint32_t X[2] = {lx0, lx1};
-    const uint32_t Y[2] = {ly0 * b.ex, ly1 * b.ex};
-    const uint32_t Z[2] = {lz0 * b.exy, lz1 * b.exy};
-    const float wx0 = 1.0f - fx, wy0 = 1.0f - fy, wz0 = 1.0f - fz;
-    const float wxy[4] = {wx0 * wy0, fx * wy0, wx0 * fy, fx * fy};
-    f2v a[C / 2];
-#pragma unroll
-    for (int i = 0; i < C / 2; ++i) a[i] = f2v{0.0f, 0.0f};
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const float w = wxy[c & 3] * ((c & 4) ? fz : wz0);
-        const uint32_t j = X[c & 1] + Y[(c >> 1) & 1] + Z[c >> 2];
-        float e[C];
-        if constexpr (C == 2) {
-            const float2 v = *reinterpret_cast<const float2*>(slice + j * 2u);
-            e[0] = v.x;
-            e[1] = v.y;
-        } else {
-#pragma unroll
-            for (int i = 0; i < C; i += 4) {
-                const float4 v = *reinterpret_cast<const float4*>(slice + j * C + i);
-                e[i] = v.x; e[i + 1] = v.y; e[i + 2] = v.z; e[i + 3] = v.w;
-            }
-        }
-        const f2v wc = {w, w};
-#pragma unroll
-        for (int i = 0; i < C / 2; ++i)
-            a[i] = __builtin_elementwise_fma(wc, f2v{e[2 * i], e[2 * i + 1]}, a[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < C / 2; ++i) {
-        acc[2 * i] = a[i].x;
-        acc[2 * i + 1] = a[i].y;
-    }
 }
 
 }  // namespace samnerf
