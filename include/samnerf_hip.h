@@ -190,7 +190,8 @@ size_t samnerf_render_workspace_size(const samnerf_model* model, uint32_t N);
  *   renderer.py computes and drops them when return_feats == 0);
  *   feature_rows [N,164] optional: the per-ray head input
  *   cat(f_sam, f_image, image, depth) (+1 pad), kept for training.
- * Outputs are written, never accumulated. */
+ * Outputs are written, never accumulated.  N = 0 returns SAMNERF_OK without
+ * touching any buffer (they may be NULL). */
 int samnerf_render_forward(const samnerf_model* model, const float* rays_o,
                            const float* rays_d, uint32_t N, const float* cam_near_far,
                            uint32_t n_cnf, float bg_color, float* image, float* depth,

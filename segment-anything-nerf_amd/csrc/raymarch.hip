@@ -911,6 +911,7 @@ __global__ void __launch_bounds__(256) k_sgrid_box4(SgridArgs a) {
         const float nz = a.u_in[((size_t)kn * 3 + 2) * N + rr];
         const float nw = a.w_in[(size_t)kn * N + rr];
         const URange ur = wave_urange(ux, uy, uz);
+        const bool ordered = wave_positions_ordered(ux, uy, uz);
         uint32_t p0, p1, p2;
         pbox_lane(mine, ur, p0, p1, p2);
         const f2v wv = {w, w};
@@ -919,8 +920,13 @@ __global__ void __launch_bounds__(256) k_sgrid_box4(SgridArgs a) {
             const PBox b = pbox_read(p0, p1, p2, l);
             float f[8];
             if (b.slots <= kBoxSlots) {
+                wave_lds_sync();                        // previous level's reads done
                 stage_pbox<8>(base, L[l], b, slice, lane);
-                lookup_level3_pbox<8>(a.grid.emb, L[l], b, slice, ux, uy, uz, f);
+                wave_lds_sync();
+                if (ordered)
+                    lookup_level3_pbox<8, false>(a.grid.emb, L[l], b, slice, ux, uy, uz, f);
+                else
+                    lookup_level3_pbox<8, true>(a.grid.emb, L[l], b, slice, ux, uy, uz, f);
             } else {
                 lookup_level3<8>(a.grid.emb, L[l], ux, uy, uz, f);
             }
@@ -1302,7 +1308,11 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
                            float* image, float* depth, float* weights_sum, float* samvit,
                            float* feature_rows, void* workspace, size_t workspace_bytes,
                            samnerf_stream_t stream) {
-    if (!m || !rays_o || !rays_d || !image || !depth || !weights_sum)
+    // N = 0 is a no-op whatever the buffers (an empty torch tensor has a null
+    // data pointer)
+    if (!m) return fail(SAMNERF_EINVAL, "render: null pointer");
+    if (N == 0) return SAMNERF_OK;
+    if (!rays_o || !rays_d || !image || !depth || !weights_sum)
         return fail(SAMNERF_EINVAL, "render: null pointer");
     if (m->num_steps[0] != 128 || m->num_steps[1] != 64 || m->num_steps[2] != 32)
         return fail(SAMNERF_EINVAL, "render: fused path is built for num_steps = [128, 64, 32]");

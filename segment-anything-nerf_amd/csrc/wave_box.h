@@ -150,9 +150,24 @@ __device__ __forceinline__ void stage_pbox(const char* __restrict__ base, const 
     }
 }
 
+// Orders a wave's LDS stores before its later LDS loads of other lanes'
+// slots (and the loads before the next stores): the LDS queue of one wave is
+// in order, this only keeps the compiler from moving the accesses across.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// True if no lane's position is NaN (all lanes active).  Then every lane's
+// corners lie in the exact box and lookup_level3_pbox<C, false> may skip the
+// per-lane inside test.
+__device__ __forceinline__ bool wave_positions_ordered(float ux, float uy, float uz) {
+    return __builtin_amdgcn_ballot_w64(ux != ux || uy != uy || uz != uz) == 0;
+}
+
 // lookup_level3 from a staged padded box (same rows, weights, FMA order);
-// a lane whose corners are outside the box gathers directly.
-template <int C>
+// with CHECK, a lane whose corners are outside the box gathers directly.
+template <int C, bool CHECK = true>
 __device__ __forceinline__ void lookup_level3_pbox(const float* __restrict__ emb, const LevelDesc& d,
                                                    const PBox& b, const float* slice, float ux,
                                                    float uy, float uz, float* acc) {
@@ -166,10 +181,12 @@ __device__ __forceinline__ void lookup_level3_pbox(const float* __restrict__ emb
     const uint32_t lx0 = cx - b.x0, lx1 = nx - b.x0;
     const uint32_t ly0 = cy - b.y0, ly1 = ny - b.y0;
     const uint32_t lz0 = cz - b.z0, lz1 = nz - b.z0;
-    const bool inside = lx0 < b.ex && lx1 < b.ex && ly0 < b.ey && ly1 < b.ey && lz0 < b.ez && lz1 < b.ez;
-    if (!inside) {
-        lookup_level3<C>(emb, d, ux, uy, uz, acc);
-        return;
+    if constexpr (CHECK) {
+        const bool inside = lx0 < b.ex && lx1 < b.ex && ly0 < b.ey && ly1 < b.ey && lz0 < b.ez && lz1 < b.ez;
+        if (!inside) {
+            lookup_level3<C>(emb, d, ux, uy, uz, acc);
+            return;
+        }
     }
     const uint32_t X[2] = {lx0, lx1};
     const uint32_t Y[2] = {ly0 << b.lx, ly1 << b.lx};

@@ -7,7 +7,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsamnerf_hip.so")
+# SAMNERF_LIB: another build of the same library (A/B timing of two builds in
+# one GPU session, tools/gpu_ab.sh); the in-tree build otherwise.
+LIB_PATH = os.environ.get("SAMNERF_LIB") or os.path.join(_HERE, "libsamnerf_hip.so")
 
 _u32 = ctypes.c_uint32
 _f32 = ctypes.c_float

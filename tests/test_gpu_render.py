@@ -319,3 +319,24 @@ def test_render_without_features_matches(hip_lib, cuda):
     assert "samvit" in a and "samvit" not in b
     for k in ("image", "depth", "weights_sum"):
         assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 65, 257])
+def test_fused_ragged_ray_counts(hip_lib, cuda, n):
+    """Ray counts that do not fill a wave / block (partial waves in every
+    kernel, the S = 4 segment form): outputs match the oracle; N = 0 is a
+    no-op returning empty tensors."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer
+    spec = synth.ModelSpec(with_sam=True, grid_log2=12, s_grid_log2=11, prop_log2=10)
+    params = synth.make_params(spec, seed=14, emb_scale=0.5, ln_jitter=0.1)
+    net = make_net(spec, params, cuda)
+    pose, intr = synth.gui_camera(32, 32, rot=synth.random_rotation(13))
+    ro, rd = ops.get_rays(pose, intr, 32, 32, device=cuda)
+    idx = torch.randperm(1024, generator=torch.Generator().manual_seed(n))[:n].to(cuda)
+    out = FusedRenderer(net).render(ro[idx], rd[idx])
+    assert out["image"].shape == (n, 3) and out["samvit"].shape == (n, 256)
+    if n == 0:
+        return
+    ref = oracle_for(spec, params).run(ro[idx].cpu(), rd[idx].cpu(), return_feats=1)
+    _check_outputs(out, ref)
