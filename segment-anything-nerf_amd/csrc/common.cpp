@@ -41,6 +41,8 @@ LevelDesc make_level(uint32_t off, uint32_t size, uint32_t res, uint32_t gridtyp
     d.off = off;
     d.size = size;
     d.res = res;
+    d.fres = (float)res;
+    d.ftop = (float)(res - 1u);
     // Running stride of get_grid_index (gridencoder.cu:63-76), uint32 wrap.
     uint32_t stride = 1u, dims = 0u;
     while (dims < 3u && stride <= size) {

@@ -442,9 +442,9 @@ __device__ __forceinline__ void gather_issue_c2(const float2* __restrict__ emb, 
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
         uint32_t cx, cy, cz;
-        locate_axis(ux, d[l].res, cx, g.fx[l]);
-        locate_axis(uy, d[l].res, cy, g.fy[l]);
-        locate_axis(uz, d[l].res, cz, g.fz[l]);
+        locate_axis(ux, d[l], cx, g.fx[l]);
+        locate_axis(uy, d[l], cy, g.fy[l]);
+        locate_axis(uz, d[l], cz, g.fz[l]);
         const uint32_t top = d[l].res - 1u;
         const bool hashed = d[l].flags & kHashed;
         const uint32_t my = hashed ? kPrime1 : d[l].res, mz = hashed ? kPrime2 : d[l].res * d[l].res;
@@ -518,7 +518,8 @@ __device__ __forceinline__ void gather_levels_c2(const float2* __restrict__ emb,
 }
 
 __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const LevelDesc& q, bool hi) {
-    return LevelDesc{hi ? q.off : p.off, hi ? q.size : p.size, hi ? q.res : p.res, hi ? q.flags : p.flags};
+    return LevelDesc{hi ? q.off : p.off, hi ? q.size : p.size, hi ? q.res : p.res, hi ? q.flags : p.flags,
+                     hi ? q.fres : p.fres, hi ? q.ftop : p.ftop};
 }
 
 // One wave marches 32 (ray, slot) columns: with S slots per ray, lane (j, h)
@@ -891,7 +892,9 @@ __global__ void __launch_bounds__(256) k_sgrid_box4(SgridArgs a) {
     const LevelDesc mine = {li == 0 ? L[0].off : li == 1 ? L[1].off : li == 2 ? L[2].off : L[3].off,
                             li == 0 ? L[0].size : li == 1 ? L[1].size : li == 2 ? L[2].size : L[3].size,
                             li == 0 ? L[0].res : li == 1 ? L[1].res : li == 2 ? L[2].res : L[3].res,
-                            0u};
+                            0u,
+                            li == 0 ? L[0].fres : li == 1 ? L[1].fres : li == 2 ? L[2].fres : L[3].fres,
+                            li == 0 ? L[0].ftop : li == 1 ? L[1].ftop : li == 2 ? L[2].ftop : L[3].ftop};
     float* slice = reinterpret_cast<float*>(smem[q]);
     const char* base = reinterpret_cast<const char*>(a.grid.emb);
     float acc[4][8];
@@ -992,9 +995,9 @@ k_sgrid_backward(uint32_t N, GridDesc<16> g, const float* __restrict__ u_in,
         const float wg = w_in[(size_t)k * N + rr] * gv;
         uint32_t cx, cy, cz;
         float fx, fy, fz;
-        locate_axis(ux, d.res, cx, fx);
-        locate_axis(uy, d.res, cy, fy);
-        locate_axis(uz, d.res, cz, fz);
+        locate_axis(ux, d, cx, fx);
+        locate_axis(uy, d, cy, fy);
+        locate_axis(uz, d, cz, fz);
         const uint32_t top = d.res - 1u;
         const uint32_t nx = min(cx + 1u, top), ny = min(cy + 1u, top), nz = min(cz + 1u, top);
 #pragma unroll
@@ -1235,7 +1238,7 @@ int make_grid_desc(const samnerf_grid& g, uint32_t C, uint32_t L, GridDesc<16>& 
             if ((uint64_t)(off + size) * C * sizeof(float) > (1ull << 32))
                 return fail(SAMNERF_EINVAL, "render: %s exceeds 4 GiB (32-bit gather offsets)", name);
         } else {
-            d.lv[l] = LevelDesc{0, 1, 1, 0};
+            d.lv[l] = LevelDesc{0, 1, 1, 0, 1.0f, 0.0f};
         }
     }
     return SAMNERF_OK;

@@ -39,6 +39,7 @@ struct LevelDesc {
     uint32_t size;     // rows in the level
     uint32_t res;      // indexing resolution
     uint32_t flags;    // bit0: hashed, bit1: size is a power of two
+    float fres, ftop;  // (float)res, (float)(res - 1): no per-lane conversions
 };
 constexpr uint32_t kHashed = 1u, kPow2 = 2u;
 
@@ -62,6 +63,16 @@ __device__ __forceinline__ void locate_axis(float u, uint32_t res, uint32_t& cel
     p = fminf(fmaxf(p, 0.0f), (float)(res - 1u));
     cell = (uint32_t)floorf(p);
     frac = p - (float)cell;
+}
+
+// The same with the level's float resolution precomputed: frac = p -
+// floorf(p) is p - (float)cell exactly (p in [0, res - 1], res < 2^24).
+__device__ __forceinline__ void locate_axis(float u, const LevelDesc& d, uint32_t& cell, float& frac) {
+    float p = __builtin_fmaf(u, d.fres, -0.5f);
+    p = fminf(fmaxf(p, 0.0f), d.ftop);
+    const float fl = floorf(p);
+    cell = (uint32_t)fl;
+    frac = p - fl;
 }
 
 // Fused-path row index.  The host (make_grid_desc) only admits levels that
@@ -131,9 +142,9 @@ __device__ __forceinline__ void corner_rows(const LevelDesc& d, float ux, float 
                                             uint32_t* off, float* w) {
     uint32_t cx, cy, cz;
     float fx, fy, fz;
-    locate_axis(ux, d.res, cx, fx);
-    locate_axis(uy, d.res, cy, fy);
-    locate_axis(uz, d.res, cz, fz);
+    locate_axis(ux, d, cx, fx);
+    locate_axis(uy, d, cy, fy);
+    locate_axis(uz, d, cz, fz);
     const uint32_t top = d.res - 1u;
     const uint32_t nx = min(cx + 1u, top), ny = min(cy + 1u, top), nz = min(cz + 1u, top);
     constexpr uint32_t RB = C * 4u;

@@ -76,9 +76,9 @@ __device__ __forceinline__ URange wave_urange(float ux, float uy, float uz) {
     return r;
 }
 
-__device__ __forceinline__ uint32_t cell_of(float u, uint32_t res) {
-    float p = __builtin_fmaf(u, (float)res, -0.5f);
-    p = fminf(fmaxf(p, 0.0f), (float)(res - 1u));
+__device__ __forceinline__ uint32_t cell_of(float u, const LevelDesc& d) {
+    float p = __builtin_fmaf(u, d.fres, -0.5f);
+    p = fminf(fmaxf(p, 0.0f), d.ftop);
     return (uint32_t)floorf(p);
 }
 
@@ -104,10 +104,10 @@ struct PBox {
 __device__ __forceinline__ void pbox_lane(const LevelDesc& d, const URange& u, uint32_t& p0,
                                           uint32_t& p1, uint32_t& p2) {
     const uint32_t top = d.res - 1u;
-    const uint32_t x0 = cell_of(u.lo[0], d.res), y0 = cell_of(u.lo[1], d.res), z0 = cell_of(u.lo[2], d.res);
-    const uint32_t x1 = min(cell_of(u.hi[0], d.res) + 1u, top);
-    const uint32_t y1 = min(cell_of(u.hi[1], d.res) + 1u, top);
-    const uint32_t z1 = min(cell_of(u.hi[2], d.res) + 1u, top);
+    const uint32_t x0 = cell_of(u.lo[0], d), y0 = cell_of(u.lo[1], d), z0 = cell_of(u.lo[2], d);
+    const uint32_t x1 = min(cell_of(u.hi[0], d) + 1u, top);
+    const uint32_t y1 = min(cell_of(u.hi[1], d) + 1u, top);
+    const uint32_t z1 = min(cell_of(u.hi[2], d) + 1u, top);
     const uint32_t ex = x1 - x0 + 1u, ey = y1 - y0 + 1u, ez = z1 - z0 + 1u;
     p0 = x0 | (y0 << 10) | (z0 << 20);
     p1 = ex | (ey << 10) | (ez << 20);
@@ -173,9 +173,9 @@ __device__ __forceinline__ void lookup_level3_pbox(const float* __restrict__ emb
                                                    float uy, float uz, float* acc) {
     uint32_t cx, cy, cz;
     float fx, fy, fz;
-    locate_axis(ux, d.res, cx, fx);
-    locate_axis(uy, d.res, cy, fy);
-    locate_axis(uz, d.res, cz, fz);
+    locate_axis(ux, d, cx, fx);
+    locate_axis(uy, d, cy, fy);
+    locate_axis(uz, d, cz, fz);
     const uint32_t top = d.res - 1u;
     const uint32_t nx = min(cx + 1u, top), ny = min(cy + 1u, top), nz = min(cz + 1u, top);
     const uint32_t lx0 = cx - b.x0, lx1 = nx - b.x0;
