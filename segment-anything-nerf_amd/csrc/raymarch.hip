@@ -137,6 +137,11 @@ __device__ __forceinline__ void grid_features(const GridDesc<16>& g, float ux, f
     }
 }
 
+// Gather forms (SAMNERF_LOOKUP, lookup_mode): direct packed / direct per-
+// corner reference / de-duplicated box; auto picks per stage.
+constexpr int kLookPacked = 0, kLookRef = 1, kLookBox4 = 3;
+constexpr int kLookAuto = 4;     // host-side only
+
 struct PropArgs {
     const float* rays_o;
     const float* rays_d;
@@ -168,14 +173,31 @@ constexpr uint32_t prop_sigma_blocks(uint32_t N) {
     return xcd_blocks((N + 63u) / 64u) * (T / 4);
 }
 
-template <int T, bool FIRST, bool REF, int OCC>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) k_prop_sigma(PropArgs a) {
+//
+// LOOK = kLookPacked / kLookRef: direct corner gathers (lookup_level3 /
+// lookup_level3_ref).  LOOK = kLookBox4: de-duplicated gathers (wave_box.h):
+// the 64 positions of a wave span a few cells of each proposal level (the
+// padded corner box of a 512^2 view's wave holds at most 64 rows at every
+// level), so the wave loads each level's box once (one row per lane) into
+// its LDS slice and reads its 40 corners from there: 5 vector-memory
+// instructions per sample instead of 40.  Same rows, weights and FMA order:
+// identical bits.
+constexpr uint32_t kPropBoxSlots = 128;      // rows per level slice (8 B each)
+
+template <int T, bool FIRST, int LOOK>
+__global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
     static_assert(T % 4 == 0, "T must be a multiple of 4");
     constexpr uint32_t Q = T / 4;
     const uint32_t b = blockIdx.x, i = b >> 3;
     const uint32_t q = i % Q, g = (b & 7u) * xcd_per((a.N + 63u) / 64u) + i / Q;
-    const uint32_t r = g * 64u + (threadIdx.x & 63u), k = q * 4u + (threadIdx.x >> 6);
-    if (r >= a.N) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t r0 = g * 64u + lane, k = q * 4u + (threadIdx.x >> 6);
+    if (g * 64u >= a.N) return;                     // whole wave past the end
+    // box form: every lane stays active for the wave reductions (lanes past
+    // the end recompute ray N - 1 and store nothing)
+    if (LOOK != kLookBox4 && r0 >= a.N) return;
+    const bool live = r0 < a.N;
+    const uint32_t r = live ? r0 : a.N - 1u;
     const uint32_t N = a.N;
     float o[3], d[3];
 #pragma unroll
@@ -197,14 +219,53 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
     float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
     contract3(x, y, z);
     float feat[10];
-    grid_features<5, 2, REF>(a.grid, a.gs(x), a.gs(y), a.gs(z), feat);
+    if constexpr (LOOK == kLookBox4) {
+        __shared__ float2 smem[4][5 * kPropBoxSlots];
+        float* slice = reinterpret_cast<float*>(smem[threadIdx.x >> 6]);
+        const float ux = a.gs(x), uy = a.gs(y), uz = a.gs(z);
+        const URange ur = wave_urange(ux, uy, uz);
+        const bool ordered = wave_positions_ordered(ux, uy, uz);
+        // lane l < 5 sizes level l's box (pbox_lane reads res, fres, ftop)
+        const LevelDesc* lv = a.grid.lv;
+        LevelDesc mine = lv[0];
+#pragma unroll
+        for (int l = 1; l < 5; ++l) {
+            const bool me = lane == (uint32_t)l;
+            mine.res = me ? lv[l].res : mine.res;
+            mine.fres = me ? lv[l].fres : mine.fres;
+            mine.ftop = me ? lv[l].ftop : mine.ftop;
+        }
+        uint32_t p0, p1, p2;
+        pbox_lane(mine, ur, p0, p1, p2);
+        PBox bx[5];
+#pragma unroll
+        for (int l = 0; l < 5; ++l) bx[l] = pbox_read(p0, p1, p2, l);
+        const char* base = reinterpret_cast<const char*>(a.grid.emb);
+#pragma unroll
+        for (int l = 0; l < 5; ++l)
+            if (bx[l].slots <= kPropBoxSlots)
+                stage_pbox<2>(base, a.grid.lv[l], bx[l], slice + l * kPropBoxSlots * 2, lane);
+        wave_lds_sync();
+#pragma unroll
+        for (int l = 0; l < 5; ++l) {
+            const float* sl = slice + l * kPropBoxSlots * 2;
+            if (bx[l].slots > kPropBoxSlots)
+                lookup_level3<2>(a.grid.emb, a.grid.lv[l], ux, uy, uz, feat + 2 * l);
+            else if (ordered)
+                lookup_level3_pbox<2, false>(a.grid.emb, a.grid.lv[l], bx[l], sl, ux, uy, uz, feat + 2 * l);
+            else
+                lookup_level3_pbox<2, true>(a.grid.emb, a.grid.lv[l], bx[l], sl, ux, uy, uz, feat + 2 * l);
+        }
+    } else {
+        grid_features<5, 2, LOOK == kLookRef>(a.grid, a.gs(x), a.gs(y), a.gs(z), feat);
+    }
     float h[16], sv;
-    if constexpr (REF) dense<16, 10, true>(a.W0, feat, h);
+    if constexpr (LOOK == kLookRef) dense<16, 10, true>(a.W0, feat, h);
     else dense_pk<16, 10, true>(a.W0, feat, h);
     dense<1, 16, false>(a.W1, h, &sv);
     // the only store, after the weight reads: an earlier store could alias
     // W0/W1 and would demote the uniform weight reads to per-lane vector loads
-    a.wtmp[(size_t)k * N + r] = (rb_next - rb_prev) * expf(sv);          // trunc_exp forward
+    if (live) a.wtmp[(size_t)k * N + r] = (rb_next - rb_prev) * expf(sv);          // trunc_exp forward
 }
 
 // Stage 0 ray setup, one thread per ray: near/far from the AABB slab test
@@ -805,8 +866,6 @@ struct SgridArgs {
 // MODE: kLookPacked (lookup_level3), kLookRef (lookup_level3_ref, scalar
 // accumulation); k_sgrid_box4 below is the de-duplicated form.  All give
 // identical bits.
-constexpr int kLookPacked = 0, kLookRef = 1, kLookBox4 = 3;
-constexpr int kLookAuto = 4;     // host-side only: packed, k_sgrid by launch size
 
 template <int T, int MODE>
 __global__ void __launch_bounds__(256) k_sgrid(SgridArgs a) {
@@ -1152,15 +1211,6 @@ void mark_stage(uint32_t i, hipStream_t s) {
     if (i < g_n_stage_events && g_stage_events[i]) (void)hipEventRecord(g_stage_events[i], s);
 }
 
-// Minimum waves per SIMD the proposal-sigma kernel is compiled for
-// (SAMNERF_PROP_OCC = 1 (no bound, the compiler's choice) | 5 | 6): fewer
-// registers per wave, more waves to hide the gather latency.
-int prop_occ() {
-    const char* v = getenv("SAMNERF_PROP_OCC");
-    const int o = v ? atoi(v) : 1;
-    return (o == 5 || o == 6) ? o : 1;
-}
-
 // Default k_sgrid form by launch size: the de-duplicated box gathers win
 // on a full view (TA-bound direct gathers), the direct gathers on one rank's
 // share of a sharded view (latency-bound at 3 waves per SIMD): measured
@@ -1183,13 +1233,18 @@ bool box4_ok(const GridDesc<16>& g) {
     return true;
 }
 
+// Proposal gather form: direct by default (packed / auto), the box form for
+// SAMNERF_LOOKUP = box / box4.  The box form trades the kernel's 40 corner
+// gathers for ~200 VALU instructions of range reduction, box staging and LDS
+// addressing per sample; the direct form is only slightly TA-bound (704 TA
+// vs 575 VALU cycles per wave) so the box form is slower, 0.88 vs 0.83 ms.
 template <int T, bool FIRST>
-void launch_prop_sigma(int look, int occ, uint32_t N, hipStream_t s, const PropArgs& pa) {
+void launch_prop_sigma(int look, uint32_t N, hipStream_t s, const PropArgs& pa) {
     const uint32_t nb = prop_sigma_blocks<T>(N);
-    if (look == kLookRef) k_prop_sigma<T, FIRST, true, 1><<<nb, 256, 0, s>>>(pa);
-    else if (occ == 5) k_prop_sigma<T, FIRST, false, 5><<<nb, 256, 0, s>>>(pa);
-    else if (occ == 6) k_prop_sigma<T, FIRST, false, 6><<<nb, 256, 0, s>>>(pa);
-    else k_prop_sigma<T, FIRST, false, 1><<<nb, 256, 0, s>>>(pa);
+    if (look == kLookRef) k_prop_sigma<T, FIRST, kLookRef><<<nb, 256, 0, s>>>(pa);
+    else if (look == kLookBox4 && box4_ok(pa.grid))
+        k_prop_sigma<T, FIRST, kLookBox4><<<nb, 256, 0, s>>>(pa);
+    else k_prop_sigma<T, FIRST, kLookPacked><<<nb, 256, 0, s>>>(pa);
 }
 
 Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
@@ -1372,7 +1427,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     const int look = lookup_mode();
     mark_stage(0, s);
     k_snf<<<div_up(N, 256), 256, 0, s>>>(pa);
-    launch_prop_sigma<128, true>(look, prop_occ(), N, s, pa);
+    launch_prop_sigma<128, true>(look, N, s, pa);
     k_prop_pdf<128, 65, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
 
     // stage 1: 64 samples -> 33 bins
@@ -1383,7 +1438,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.bins_in = w.bins1;
     pa.bins_out = w.bins2;
     mark_stage(1, s);
-    launch_prop_sigma<64, false>(look, prop_occ(), N, s, pa);
+    launch_prop_sigma<64, false>(look, N, s, pa);
     k_prop_pdf<64, 33, false><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
 
     // stage 2: 32 samples through the full network

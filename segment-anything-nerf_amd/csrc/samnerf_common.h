@@ -174,10 +174,58 @@ __device__ __forceinline__ void corner_rows(const LevelDesc& d, float ux, float 
 // into `acc` on packed-fp32 FMAs (two channels per v_pk_fma_f32; each lane
 // of it is the same IEEE fma as the scalar form, so the bits are unchanged).
 // Fused-path tables only (32-bit byte offsets, see load_row_b).
+typedef float f4a8 __attribute__((ext_vector_type(4), aligned(8)));
+
+// Dense C = 2 level: corners c and c | 1 (x and x + 1 at the same y, z) are
+// adjacent 8-byte rows, so one 16-byte load fetches both -- 4 vector-memory
+// instructions per level instead of 8, and the texture-address unit's cost is
+// per lane and instruction, not per byte.  At the top x cell (cx = res - 1,
+// nx = cx) the pair is loaded from cx - 1 and both corners take its upper
+// row.  Rows, weights and FMA order are lookup_level3's.
+__device__ __forceinline__ void lookup_dense_c2_paired(const float* __restrict__ emb,
+                                                       const LevelDesc& d, float ux, float uy,
+                                                       float uz, float* acc) {
+    uint32_t cx, cy, cz;
+    float fx, fy, fz;
+    locate_axis(ux, d, cx, fx);
+    locate_axis(uy, d, cy, fy);
+    locate_axis(uz, d, cz, fz);
+    const uint32_t top = d.res - 1u;
+    const uint32_t ny = min(cy + 1u, top), nz = min(cz + 1u, top);
+    const bool edge = cx == top;
+    const uint32_t bx = d.off + (edge ? cx - 1u : cx);
+    const uint32_t r2 = d.res * d.res;
+    const uint32_t y0 = __umul24(cy, d.res), y1 = __umul24(ny, d.res);
+    const uint32_t z0 = __umul24(cz, r2), z1 = __umul24(nz, r2);
+    const uint32_t pr[4] = {bx + y0 + z0, bx + y1 + z0, bx + y0 + z1, bx + y1 + z1};
+    const char* base = reinterpret_cast<const char*>(emb);
+    f4a8 v[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) v[p] = *reinterpret_cast<const f4a8*>(base + pr[p] * 8u);
+    const float wx0 = 1.0f - fx, wy0 = 1.0f - fy, wz0 = 1.0f - fz;
+    const float wxy[4] = {wx0 * wy0, fx * wy0, wx0 * fy, fx * fy};
+    f2v a = {0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const f4a8& q = v[c >> 1];              // pair (y, z) = (c >> 1 & 1, c >> 2)
+        const f2v e = (c & 1) ? f2v{q.z, q.w} : (edge ? f2v{q.z, q.w} : f2v{q.x, q.y});
+        const float w = wxy[c & 3] * ((c & 4) ? fz : wz0);
+        a = __builtin_elementwise_fma(f2v{w, w}, e, a);
+    }
+    acc[0] = a.x;
+    acc[1] = a.y;
+}
+
 template <int C>
 __device__ __forceinline__ void lookup_level3(const float* __restrict__ emb, const LevelDesc& d,
                                               float ux, float uy, float uz, float* acc) {
     static_assert(C % 2 == 0, "packed accumulation needs an even channel count");
+    if constexpr (C == 2) {
+        if (!(d.flags & kHashed)) {
+            lookup_dense_c2_paired(emb, d, ux, uy, uz, acc);
+            return;
+        }
+    }
     uint32_t off[8];
     float w[8];
     corner_rows<C>(d, ux, uy, uz, off, w);

@@ -143,9 +143,13 @@ __device__ __forceinline__ void stage_pbox(const char* __restrict__ base, const 
             const uint32_t row = dense_or_hash_row(b.x0 + bx, b.y0 + by, b.z0 + bz, d);
             float e[C];
             load_row_b<C>(base, (d.off + row) * (uint32_t)(C * 4), e);
+            if constexpr (C == 2) {
+                *reinterpret_cast<float2*>(slice + j * 2) = make_float2(e[0], e[1]);
+            } else {
 #pragma unroll
-            for (int i = 0; i < C; i += 4)
-                *reinterpret_cast<float4*>(slice + j * C + i) = make_float4(e[i], e[i + 1], e[i + 2], e[i + 3]);
+                for (int i = 0; i < C; i += 4)
+                    *reinterpret_cast<float4*>(slice + j * C + i) = make_float4(e[i], e[i + 1], e[i + 2], e[i + 3]);
+            }
         }
     }
 }
@@ -201,11 +205,16 @@ __device__ __forceinline__ void lookup_level3_pbox(const float* __restrict__ emb
         const float w = wxy[c & 3] * ((c & 4) ? fz : wz0);
         const uint32_t j = X[c & 1] + Y[(c >> 1) & 1] + Z[c >> 2];
         const f2v wc = {w, w};
+        if constexpr (C == 2) {
+            const float2 v = *reinterpret_cast<const float2*>(slice + j * 2);
+            a[0] = __builtin_elementwise_fma(wc, f2v{v.x, v.y}, a[0]);
+        } else {
 #pragma unroll
-        for (int i = 0; i < C; i += 4) {
-            const float4 v = *reinterpret_cast<const float4*>(slice + j * C + i);
-            a[i / 2] = __builtin_elementwise_fma(wc, f2v{v.x, v.y}, a[i / 2]);
-            a[i / 2 + 1] = __builtin_elementwise_fma(wc, f2v{v.z, v.w}, a[i / 2 + 1]);
+            for (int i = 0; i < C; i += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(slice + j * C + i);
+                a[i / 2] = __builtin_elementwise_fma(wc, f2v{v.x, v.y}, a[i / 2]);
+                a[i / 2 + 1] = __builtin_elementwise_fma(wc, f2v{v.z, v.w}, a[i / 2 + 1]);
+            }
         }
     }
 #pragma unroll
