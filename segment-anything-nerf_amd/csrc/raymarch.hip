@@ -379,6 +379,7 @@ struct FinalArgs {
     float* depth;      // [N]
     float* wsum;       // [N]
     float* rows;       // [N, kRow] or null
+    uint32_t classes;  // 1: k_final's uniform slot paths (SAMNERF_FINAL_CLASSES, default on)
 };
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -425,11 +426,17 @@ __device__ __forceinline__ int hidden_unit(int kb, int h, int m) {
     return (kb >> 1) * 32 + rho(8 * (kb & 1) + m) + 4 * h;
 }
 
+// Level gathered by half-wave h in slot q of k-block kb (its B operand of the
+// first layer holds that level's two channels at k = 2q, 2q + 1).  Adjacent
+// levels share a slot: the dense levels (the coarse ones) then pair up in
+// both half-waves, so their slots take gather_issue_c2's uniform dense path.
+__host__ __device__ constexpr int final_level(int kb, int h, int q) { return 8 * kb + 2 * q + h; }
+
 __device__ float grid_weight(const FinalArgs& a, int slot, int lane, int m) {
     const int i = lane & 31, h = lane >> 5;
-    if (slot < kF2) {                          // input k = 2*level + channel = 16kb + 8h + m
+    if (slot < kF2) {                          // input k = 2*level + channel, level = final_level(kb, h, m / 2)
         const int kb = slot >> 1, ob = slot & 1;
-        return a.G0[(ob * 32 + i) * 32 + 16 * kb + 8 * h + m];
+        return a.G0[(ob * 32 + i) * 32 + 2 * final_level(kb, h, m >> 1) + (m & 1)];
     }
     if (slot < kF3) {
         const int t = slot - kF2, kb = t >> 1, ob = t & 1;
@@ -496,9 +503,22 @@ struct GatherC2 {
     float fx[NL], fy[NL], fz[NL];
 };
 
+// Wave-uniform classes of the NL level slots of one call: bit l of `dense`
+// = the level of slot l is dense in both half-waves, of `hashed` = hashed in
+// both.  Such a slot skips the per-lane dense/hash selects, and a dense one
+// fetches its x-adjacent corner pairs with one 16-B load each (the rows
+// (x, y, z) and (x + 1, y, z) are adjacent).  Mixed slots keep the
+// lane-varying form.
+struct SlotKinds {
+    uint32_t dense, hashed;
+};
+
 template <int NL>
 __device__ __forceinline__ void gather_issue_c2(const float2* __restrict__ emb, const LevelDesc* d,
-                                                float ux, float uy, float uz, GatherC2<NL>& g) {
+                                                float ux, float uy, float uz, GatherC2<NL>& g,
+                                                SlotKinds kinds = SlotKinds{0u, 0u}) {
+    // byte offsets of every corner (dense-pair slots: of the 4 pairs) first,
+    // then all loads, so they are in flight together
     uint32_t row[NL][8];
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
@@ -507,24 +527,59 @@ __device__ __forceinline__ void gather_issue_c2(const float2* __restrict__ emb, 
         locate_axis(uy, d[l], cy, g.fy[l]);
         locate_axis(uz, d[l], cz, g.fz[l]);
         const uint32_t top = d[l].res - 1u;
-        const bool hashed = d[l].flags & kHashed;
-        const uint32_t my = hashed ? kPrime1 : d[l].res, mz = hashed ? kPrime2 : d[l].res * d[l].res;
-        const uint32_t mask = hashed ? d[l].size - 1u : 0xffffffffu;
-        const uint32_t X[2] = {cx, min(cx + 1u, top)};
-        const uint32_t Y[2] = {cy * my, min(cy + 1u, top) * my};
-        const uint32_t Z[2] = {cz * mz, min(cz + 1u, top) * mz};
+        const uint32_t ny = min(cy + 1u, top), nz = min(cz + 1u, top);
+        if ((kinds.dense >> l) & 1u) {
+            // pair (cx, cx + 1); in the top cell (cx = top, so fx = 0) the pair
+            // (top - 1, top) is loaded and the x weights swapped (fx := 1):
+            // corner 0 then adds 0 * row(top - 1), an exact no-op (the running
+            // sum is never -0), and corner 1 adds row(top) with corner 0's
+            // original weight (1 * wy) * wz -- the same bits as the reference
+            const bool edge = cx == top;
+            g.fx[l] = edge ? 1.0f : g.fx[l];
+            const uint32_t bx = d[l].off + (edge ? cx - 1u : cx);
+            const uint32_t r2 = d[l].res * d[l].res;
+            const uint32_t Y[2] = {(uint32_t)__umul24(cy, d[l].res), (uint32_t)__umul24(ny, d[l].res)};
+            const uint32_t Z[2] = {(uint32_t)__umul24(cz, r2), (uint32_t)__umul24(nz, r2)};
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const uint32_t xs = X[c & 1], ys = Y[(c >> 1) & 1], zs = Z[c >> 2];
-            row[l][c] = (d[l].off + (hashed ? ((xs ^ ys ^ zs) & mask) : (xs + ys + zs))) << 3;
+            for (int p = 0; p < 4; ++p) row[l][p] = (bx + Y[p & 1] + Z[p >> 1]) << 3;
+        } else if ((kinds.hashed >> l) & 1u) {
+            const uint32_t mask = d[l].size - 1u;
+            const uint32_t X[2] = {cx, min(cx + 1u, top)};
+            const uint32_t Y[2] = {cy * kPrime1, ny * kPrime1};
+            const uint32_t Z[2] = {cz * kPrime2, nz * kPrime2};
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                row[l][c] = (d[l].off + ((X[c & 1] ^ Y[(c >> 1) & 1] ^ Z[c >> 2]) & mask)) << 3;
+        } else {
+            const bool hashed = d[l].flags & kHashed;
+            const uint32_t my = hashed ? kPrime1 : d[l].res, mz = hashed ? kPrime2 : d[l].res * d[l].res;
+            const uint32_t mask = hashed ? d[l].size - 1u : 0xffffffffu;
+            const uint32_t X[2] = {cx, min(cx + 1u, top)};
+            const uint32_t Y[2] = {cy * my, ny * my};
+            const uint32_t Z[2] = {cz * mz, nz * mz};
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t xs = X[c & 1], ys = Y[(c >> 1) & 1], zs = Z[c >> 2];
+                row[l][c] = (d[l].off + (hashed ? ((xs ^ ys ^ zs) & mask) : (xs + ys + zs))) << 3;
+            }
         }
     }
     // 32-bit byte offsets from the uniform table base (saddr loads)
     const char* base = reinterpret_cast<const char*>(emb);
 #pragma unroll
-    for (int l = 0; l < NL; ++l)
+    for (int l = 0; l < NL; ++l) {
+        if ((kinds.dense >> l) & 1u) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) g.e[l][c] = *reinterpret_cast<const float2*>(base + row[l][c]);
+            for (int p = 0; p < 4; ++p) {
+                const f4a8 v = *reinterpret_cast<const f4a8*>(base + row[l][p]);
+                g.e[l][2 * p] = make_float2(v.x, v.y);
+                g.e[l][2 * p + 1] = make_float2(v.z, v.w);
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) g.e[l][c] = *reinterpret_cast<const float2*>(base + row[l][c]);
+        }
+    }
 }
 
 // Weighted corner sums with the reference's weights (wx * wy) * wz.  PK: both
@@ -572,9 +627,10 @@ __device__ __forceinline__ void gather_finish_c2(const GatherC2<NL>& g, float* f
 // compiler otherwise waits for each level before issuing the next).
 template <int NL, bool PK = false>
 __device__ __forceinline__ void gather_levels_c2(const float2* __restrict__ emb, const LevelDesc* d,
-                                                 float ux, float uy, float uz, float* f) {
+                                                 float ux, float uy, float uz, float* f,
+                                                 SlotKinds kinds = SlotKinds{0u, 0u}) {
     GatherC2<NL> g;
-    gather_issue_c2<NL>(emb, d, ux, uy, uz, g);
+    gather_issue_c2<NL>(emb, d, ux, uy, uz, g, kinds);
     gather_finish_c2<NL, PK>(g, f);
 }
 
@@ -586,8 +642,9 @@ __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const Leve
 // One wave marches 32 (ray, slot) columns: with S slots per ray, lane (j, h)
 // owns slot j / R of ray j % R (R = 32 / S rays per wave), i.e. samples
 // slot, slot + S, slot + 2S, ...  For k-block kb it gathers both channels of
-// levels 8kb + 4h .. 8kb + 4h + 3 -- exactly its B operand of the first layer
-// (input index 2*level + channel) -- so the hash grid feeds the matrix cores
+// levels final_level(kb, h, 0..3) = 8kb + h, 8kb + 2 + h, .. -- exactly its B
+// operand of the first layer (grid_weight permutes the weight columns to
+// match) -- so the hash grid feeds the matrix cores
 // with no data movement.  grid_mlp 32->64->64->16 runs on bf16x3 MFMAs,
 // view_mlp 31->32->32->3 (once per ray) on fp32 MFMAs.  Compositing: each
 // step the S slots of a ray exchange their optical depths by shuffle and
@@ -645,7 +702,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     // selects, re-evaluated where used rather than held in VGPRs)
     auto levels = [&](int kb, LevelDesc* dl) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dl[q] = select_level(G->lv[8 * kb + q], G->lv[8 * kb + 4 + q], hh != 0);
+        for (int q = 0; q < 4; ++q)
+            dl[q] = select_level(G->lv[final_level(kb, 0, q)], G->lv[final_level(kb, 1, q)], hh != 0);
+    };
+    // wave-uniform slot classes (scalar loads).  S = 1 only: the S = 2 / 4
+    // prefetching forms are at the register limit and the extra code paths
+    // made them spill
+    auto kinds = [&](int kb) {
+        SlotKinds k{0u, 0u};
+        if (S != 1 || !a.classes) return k;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool ha = G->lv[final_level(kb, 0, q)].flags & kHashed;
+            const bool hb = G->lv[final_level(kb, 1, q)].flags & kHashed;
+            k.dense |= (!ha && !hb) ? 1u << q : 0u;
+            k.hashed |= (ha && hb) ? 1u << q : 0u;
+        }
+        return k;
+    };
+    // PF prefetches k-block kPre = 1 (levels 8-15: hashed in every grid of
+    // the path) and gathers k-block 0 -- which holds the dense levels and
+    // their pair loads -- inside the iteration.  Pair loads in the prefetched
+    // block made the PF form nondeterministic (16-ray groups differing run to
+    // run, tools/diag/final_determinism.py), so the prefetch never uses them.
+    // Both forms accumulate layer 1 in the order kPre, 1 - kPre: PF on and off
+    // give identical bits.
+    constexpr int kPre = 1;
+    auto pf_kinds = [&](int kb) {
+        SlotKinds k = kinds(kb);
+        k.dense = 0u;
+        return k;
     };
     // rb_prev of sample i is rb_next of sample i - 1 when S == 1 (same bits;
     // saves a division), recomputed from the bins otherwise
@@ -665,13 +751,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
             a.u_out[((size_t)k * 3 + 2) * N + r] = uz;
         }
     };
-    GatherC2<4> pre;                                      // PF: kb 0 of the current sample
+    GatherC2<4> pre;                                      // PF: kb kPre of the current sample
     float p_rbp = rb_prev, p_rbn = 0.0f, p_ux = 0.0f, p_uy = 0.0f, p_uz = 0.0f;
     if constexpr (PF) {
         LevelDesc dl[4];
-        levels(0, dl);
+        levels(kPre, dl);
         position(0, p_rbp, p_rbn, p_ux, p_uy, p_uz);
-        gather_issue_c2<4>(emb, dl, p_ux, p_uy, p_uz, pre);
+        gather_issue_c2<4>(emb, dl, p_ux, p_uy, p_uz, pre, pf_kinds(kPre));
     }
 
     for (int i = 0; i < TS; ++i) {
@@ -696,14 +782,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 
         floatx16 h1a = {}, h1b = {};
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
+        for (int kbi = 0; kbi < 2; ++kbi) {
+            const int kb = kbi == 0 ? kPre : 1 - kPre;
             float f[8];
-            if (PF && kb == 0) {
+            if (PF && kbi == 0) {
                 gather_finish_c2<4, S == 1>(pre, f);
             } else {
                 LevelDesc dl[4];
                 levels(kb, dl);
-                gather_levels_c2<4, S == 1>(emb, dl, ux, uy, uz, f);
+                gather_levels_c2<4, S == 1>(emb, dl, ux, uy, uz, f, kinds(kb));
             }
             uint4 bh, bl;
             split8(f, bh, bl);
@@ -713,10 +800,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         if constexpr (PF) {
             if (i + 1 < TS) {
                 LevelDesc dl[4];
-                levels(0, dl);
+                levels(kPre, dl);
                 p_rbp = p_rbn;                            // S == 1: next rb_prev = this rb_next
                 position(i + 1, p_rbp, p_rbn, p_ux, p_uy, p_uz);
-                gather_issue_c2<4>(emb, dl, p_ux, p_uy, p_uz, pre);
+                gather_issue_c2<4>(emb, dl, p_ux, p_uy, p_uz, pre, pf_kinds(kPre));
             }
         }
 #pragma unroll
@@ -1221,6 +1308,14 @@ constexpr uint32_t kBox4MinRays = 131072;
 // 0.26 ms at one rank's 32K-ray share (S = 2), 1.01 -> 0.99 ms on a full view
 // (S = 1, packed corner sums; with the scalar sums the held loads spilled,
 // 1.41 ms).  SAMNERF_FINAL_PF = 0 | 1 forces it off / on.
+// k_final's wave-uniform slot paths (dense pair loads, select-free hashed
+// rows): on by default; SAMNERF_FINAL_CLASSES=0 takes the lane-varying form
+// everywhere (same bits: the A/B parity test).
+uint32_t final_classes() {
+    const char* v = getenv("SAMNERF_FINAL_CLASSES");
+    return (v && atoi(v) == 0) ? 0u : 1u;
+}
+
 bool final_prefetch(int seg) {
     const char* v = getenv("SAMNERF_FINAL_PF");
     return v ? atoi(v) != 0 : true;
@@ -1457,6 +1552,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.V1 = m->view_mlp[1];
     fa.V2 = m->view_mlp[2];
     fa.bins_in = w.bins2;
+    fa.classes = final_classes();
     fa.snf = w.snf;
     fa.u_out = w.u_f;
     fa.w_out = w.w_f;

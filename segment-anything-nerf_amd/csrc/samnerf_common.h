@@ -180,8 +180,11 @@ typedef float f4a8 __attribute__((ext_vector_type(4), aligned(8)));
 // adjacent 8-byte rows, so one 16-byte load fetches both -- 4 vector-memory
 // instructions per level instead of 8, and the texture-address unit's cost is
 // per lane and instruction, not per byte.  At the top x cell (cx = res - 1,
-// nx = cx) the pair is loaded from cx - 1 and both corners take its upper
-// row.  Rows, weights and FMA order are lookup_level3's.
+// nx = cx, so fx = 0) the pair (top - 1, top) is loaded and the x weights
+// swapped (fx := 1): corner 0 then adds 0 * row(top - 1), an exact no-op (the
+// running sum starts at +0 and is never -0; rows are finite), and corner 1
+// adds row(top) with corner 0's original weight (1 * wy) * wz.  Same bits as
+// lookup_level3 (the SAMNERF_LOOKUP=ref parity test), no per-corner selects.
 __device__ __forceinline__ void lookup_dense_c2_paired(const float* __restrict__ emb,
                                                        const LevelDesc& d, float ux, float uy,
                                                        float uz, float* acc) {
@@ -193,6 +196,7 @@ __device__ __forceinline__ void lookup_dense_c2_paired(const float* __restrict__
     const uint32_t top = d.res - 1u;
     const uint32_t ny = min(cy + 1u, top), nz = min(cz + 1u, top);
     const bool edge = cx == top;
+    fx = edge ? 1.0f : fx;
     const uint32_t bx = d.off + (edge ? cx - 1u : cx);
     const uint32_t r2 = d.res * d.res;
     const uint32_t y0 = __umul24(cy, d.res), y1 = __umul24(ny, d.res);
@@ -208,7 +212,7 @@ __device__ __forceinline__ void lookup_dense_c2_paired(const float* __restrict__
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         const f4a8& q = v[c >> 1];              // pair (y, z) = (c >> 1 & 1, c >> 2)
-        const f2v e = (c & 1) ? f2v{q.z, q.w} : (edge ? f2v{q.z, q.w} : f2v{q.x, q.y});
+        const f2v e = (c & 1) ? f2v{q.z, q.w} : f2v{q.x, q.y};
         const float w = wxy[c & 3] * ((c & 4) ? fz : wz0);
         a = __builtin_elementwise_fma(f2v{w, w}, e, a);
     }

@@ -340,3 +340,30 @@ def test_fused_ragged_ray_counts(hip_lib, cuda, n):
         return
     ref = oracle_for(spec, params).run(ro[idx].cpu(), rd[idx].cpu(), return_feats=1)
     _check_outputs(out, ref)
+
+
+@pytest.mark.parametrize("n", [70000, 9000])
+def test_final_slot_classes_bit_identical(hip_lib, cuda, monkeypatch, n):
+    """k_final's wave-uniform slot paths -- one 16-B load per x-adjacent corner
+    pair on dense levels (with the top-cell weight swap) and select-free
+    hashed rows -- against the lane-varying form (SAMNERF_FINAL_CLASSES=0):
+    identical bits, on a view whose far samples reach the top cells of the
+    coarse levels, with PF on and off."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer, ROW
+    spec = synth.ModelSpec(with_sam=True)
+    net = make_net(spec, synth.make_params(spec, seed=29, emb_scale=0.5, ln_jitter=0.1), cuda)
+    pose, intr = synth.gui_camera(512, 160, rot=synth.random_rotation(17))
+    ro, rd = ops.get_rays(pose, intr, 160, 512, device=cuda)
+    fr = FusedRenderer(net)
+    for pf in ("0", "1"):
+        monkeypatch.setenv("SAMNERF_FINAL_PF", pf)
+        outs = []
+        for cl in ("0", "1"):
+            monkeypatch.setenv("SAMNERF_FINAL_CLASSES", cl)
+            rows = torch.empty(n, ROW, device=cuda)
+            o = fr.render(ro[:n], rd[:n], rows=rows)
+            o["rows"] = rows
+            outs.append(o)
+        for k in outs[0]:
+            assert torch.equal(outs[0][k], outs[1][k]), (pf, k)
