@@ -705,12 +705,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         for (int q = 0; q < 4; ++q)
             dl[q] = select_level(G->lv[final_level(kb, 0, q)], G->lv[final_level(kb, 1, q)], hh != 0);
     };
-    // wave-uniform slot classes (scalar loads).  S = 1 only: the S = 2 / 4
-    // prefetching forms are at the register limit and the extra code paths
-    // made them spill
+    // wave-uniform slot classes (scalar loads)
     auto kinds = [&](int kb) {
         SlotKinds k{0u, 0u};
-        if (S != 1 || !a.classes) return k;
+        if (!a.classes) return k;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const bool ha = G->lv[final_level(kb, 0, q)].flags & kHashed;
@@ -1304,10 +1302,11 @@ void mark_stage(uint32_t i, hipStream_t s) {
 // 0.94 vs 1.05 ms at 262,144 rays, 0.25 vs 0.21 ms at 32,768.
 constexpr uint32_t kBox4MinRays = 131072;
 
-// k_final's cross-sample prefetch of its first k-block's gathers: 0.29 ->
-// 0.26 ms at one rank's 32K-ray share (S = 2), 1.01 -> 0.99 ms on a full view
-// (S = 1, packed corner sums; with the scalar sums the held loads spilled,
-// 1.41 ms).  SAMNERF_FINAL_PF = 0 | 1 forces it off / on.
+// k_final's cross-sample prefetch of one k-block's gathers: on for S = 1
+// (a full view: 1.01 -> 0.99 ms), off for S = 2 / 4 (one rank's share), whose
+// prefetching forms spill once the slot-class paths are in: at 32,768 rays
+// 0.260 ms without it vs 0.288 with it (0.303 for the earlier default, PF
+// without slot classes).  SAMNERF_FINAL_PF = 0 | 1 forces it off / on.
 // k_final's wave-uniform slot paths (dense pair loads, select-free hashed
 // rows): on by default; SAMNERF_FINAL_CLASSES=0 takes the lane-varying form
 // everywhere (same bits: the A/B parity test).
@@ -1318,7 +1317,7 @@ uint32_t final_classes() {
 
 bool final_prefetch(int seg) {
     const char* v = getenv("SAMNERF_FINAL_PF");
-    return v ? atoi(v) != 0 : true;
+    return v ? atoi(v) != 0 : seg == 1;
 }
 
 // k_sgrid_box4 packs cell indices and extents into 10 bits
