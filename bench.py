@@ -106,7 +106,7 @@ def setup_dist(args):
 
 def build_net(with_sam, device):
     from nerf.network import NeRFNetwork, default_opt
-    from oracle import synth
+    from samnerf_amd import synth
     spec = synth.ModelSpec(with_sam=with_sam)
     params = synth.make_params(spec, seed=0, emb_scale=1e-4, ln_jitter=0.0)
     net = NeRFNetwork(default_opt(with_sam=with_sam))
@@ -179,7 +179,7 @@ def train_main(args, dev):
     import torch.nn.functional as F
     from samnerf_amd import ops
     from samnerf_amd.fused import FusedRenderer, render_sam_train
-    from oracle import synth
+    from samnerf_amd import synth
     net, spec, params = build_net(True, dev)
     net.train()
     for k, p in net.named_parameters():
@@ -230,7 +230,7 @@ def gui_main(args, dev):
     decoder (not run here)."""
     from samnerf_amd import ops
     from samnerf_amd.fused import FusedRenderer
-    from oracle import synth
+    from samnerf_amd import synth
     net, _, _ = build_net(True, dev)
     r = FusedRenderer(net)
     H, W = args.H, args.W
@@ -276,7 +276,7 @@ def main():
     from samnerf_amd._lib import lib
     from samnerf_amd.dist import ShardedViewPipeline, render_view_sharded, shard_range
     from samnerf_amd.fused import FusedRenderer
-    from oracle import synth
+    from samnerf_amd import synth
 
     with_sam = not args.no_sam
     net, spec, params = build_net(with_sam, dev)

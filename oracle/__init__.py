@@ -10,8 +10,8 @@ Contents
                reference's gridencoder / shencoder / freqencoder .cu kernels)
   renderer.py  torch-CPU restatement of nerf/renderer.py + nerf/network.py
                (+ get_rays from nerf/utils.py), op for op, citing file:line
-  synth.py     deterministic parameter / camera synthesis shared by tests,
-               golden generation and the bench
+  synth.py     re-export of samnerf_amd/synth.py (deterministic parameter /
+               camera synthesis) for the tests and the golden generator
 
 Pinning: tests/test_oracle.py checks this oracle against
   * tests/golden/*.npz -- produced by tools/make_golden.py, which imports the
