@@ -80,6 +80,12 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo for rehearsals")
     ap.add_argument("--share-gpu", action="store_true",
                     help="all ranks on GPU 0 (rehearsal of the N-rank path on a one-GPU box)")
+    ap.add_argument("--rank-share", type=int, default=0,
+                    help="one GPU renders only the row band rank --share-rank of N = this value "
+                         "would render in an N-rank strong-scaled view (the 512x512 camera, not a "
+                         "smaller view): the per-rank load of the N-GPU bench; value = that band's "
+                         "rays/s")
+    ap.add_argument("--share-rank", type=int, default=-1, help="band index for --rank-share (default N//2)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -285,6 +291,10 @@ def main():
     pose, intr = synth.gui_camera(W, H)
     r0, r1 = shard_range(H, rank, world)                      # row band of this rank
     n_total = H * W
+    if world == 1 and args.rank_share > 1:                     # one rank's band, on one GPU
+        k = args.share_rank if args.share_rank >= 0 else args.rank_share // 2
+        r0, r1 = shard_range(H, k, args.rank_share)
+        n_total = (r1 - r0) * W
     band_rays = (r1 - r0) * W
     chunks = max(1, args.chunks) if world > 1 else 1
 
@@ -378,7 +388,9 @@ def main():
             "data": "synthetic (random-init weights of the reference architecture, GUI camera)",
             "config": {"workload": ("cfg3: 512x512 view, RGB + 256-d SAM feature per ray" if with_sam
                                     else "cfg2: 512x512 view, RGB only") if (H, W) == (512, 512)
-                       else f"{H}x{W} view", "rays_per_step": n_total, "num_steps": [128, 64, 32],
+                       else f"{H}x{W} view", **({"rank_share": f"rows {r0}-{r1} of {args.rank_share} bands"}
+                                                 if world == 1 and args.rank_share > 1 else {}),
+                       "rays_per_step": n_total, "num_steps": [128, 64, 32],
                        "parallelism": (f"ray-sharded row bands x{world}, RCCL all-gather of each view "
                                        f"overlapped with the next view's rendering, views issued on "
                                        f"{len(streams)} HIP streams" if args.chunks == 0 else

@@ -309,15 +309,31 @@ __global__ void __launch_bounds__(256) k_prop_pdf(PropArgs a) {
     if (r0 >= N) return;
     const uint32_t nr = min(64u, N - r0);
     float* row = sw + lane * SW;
+    // All four waves stage the ds rows (sample-major wtmp, coalesced across
+    // the wave): T/4 independent loads per thread in flight at once, instead
+    // of one thread per ray loading its whole row in dependent batches.
+    // (Staging the input bins of stage > 0 as well doubles the LDS of
+    // k_prop_pdf<64> and halves its occupancy: measured slower.)
+    if (lane < nr) {
+        constexpr int TQ = T / 4;
+        float v[TQ];
+#pragma unroll
+        for (int k = 0; k < TQ; ++k) v[k] = a.wtmp[(size_t)(part * TQ + k) * N + r0 + lane];
+#pragma unroll
+        for (int k = 0; k < TQ; ++k) row[part * TQ + k] = v[k];
+    }
+    __syncthreads();
     if (part == 0 && lane < nr) {
-        // ds rows from the sample-major wtmp: coalesced across the wave
-        for (int k = 0; k < T; ++k) row[k] = a.wtmp[(size_t)k * N + r0 + lane];
+        // unrolled by 8: the LDS reads run ahead of the double-precision
+        // chains (a full unroll takes 248 VGPRs and halves occupancy)
         double cum = 0.0;
+#pragma unroll 8
         for (int k = 0; k < T; ++k) row[k] = composite_step(row[k], cum, k == T - 1);
         const float wsum = torch_row_sum(T, [&](int i) { return row[i] + 0.01f; });
         double c = 0.0;
         float wnext = row[0];
         row[0] = 0.0f;
+#pragma unroll 8
         for (int i = 0; i < T; ++i) {
             const float wi = wnext;
             if (i + 1 < T) wnext = row[i + 1];

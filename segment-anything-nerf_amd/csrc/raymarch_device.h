@@ -65,10 +65,11 @@ __device__ __forceinline__ void contract3(float& x, float& y, float& z) {
 }
 
 // torch.nan_to_num: NaN -> 0, +-inf -> +-FLT_MAX
+// (branch-free: a clamp and one select, no divergent blocks in the
+// unrolled compositing chains)
 __device__ __forceinline__ float nan_to_num(float v) {
-    if (isnan(v)) return 0.0f;
-    if (isinf(v)) return v > 0.0f ? FLT_MAX : -FLT_MAX;
-    return v;
+    const float c = fmaxf(fminf(v, FLT_MAX), -FLT_MAX);
+    return v == v ? c : 0.0f;
 }
 
 // One compositing step (renderer.py:310-326): given delta*sigma of sample k
