@@ -20,6 +20,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <limits.h>
 #include <stdint.h>
 
 #include "samnerf_common.h"
@@ -65,14 +66,52 @@ struct URange {
     float lo[3], hi[3];
 };
 
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+
+// Signed-integer min / max of float bit patterns over the 64 lanes: the DPP
+// steps fold into v_min_i32 / v_max_i32 (fminf / fmaxf need a canonicalising
+// v_max per operand), the cross-row step is scalar.
+__device__ __forceinline__ int wave_imin(int v) {
+    v = min(v, dpp_i<0xB1>(v));
+    v = min(v, dpp_i<0x4E>(v));
+    v = min(v, dpp_i<0x141>(v));
+    v = min(v, dpp_i<0x140>(v));
+    const int r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+    const int r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+    return min(min(r0, r1), min(r2, r3));
+}
+
+__device__ __forceinline__ int wave_imax(int v) {
+    v = max(v, dpp_i<0xB1>(v));
+    v = max(v, dpp_i<0x4E>(v));
+    v = max(v, dpp_i<0x141>(v));
+    v = max(v, dpp_i<0x140>(v));
+    const int r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+    const int r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+    return max(max(r0, r1), max(r2, r3));
+}
+
+// The range feeds only cell_of, which clamps below at cell 0.  Signed-integer
+// order of float bits is the float order on non-negative values and puts
+// every negative value (-0.0 included) below them, so the integer min / max
+// select a value in the same cell as the float min / max: a negative result
+// occurs exactly when the float result is negative (or -0.0), and both clamp
+// to cell 0.  NaN lanes are neutral (INT_MAX in the min, INT_MIN in the max),
+// as fminf / fmaxf skip NaN; an all-NaN wave yields NaN bits / -0.0, cell 0
+// like the float reduction's NaN.
 __device__ __forceinline__ URange wave_urange(float ux, float uy, float uz) {
+    const float u[3] = {ux, uy, uz};
     URange r;
-    r.lo[0] = wave_fmin(ux);
-    r.lo[1] = wave_fmin(uy);
-    r.lo[2] = wave_fmin(uz);
-    r.hi[0] = wave_fmax(ux);
-    r.hi[1] = wave_fmax(uy);
-    r.hi[2] = wave_fmax(uz);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const int b = __float_as_int(u[c]);
+        const bool nan = u[c] != u[c];
+        r.lo[c] = __int_as_float(wave_imin(nan ? INT_MAX : b));
+        r.hi[c] = __int_as_float(wave_imax(nan ? INT_MIN : b));
+    }
     return r;
 }
 
