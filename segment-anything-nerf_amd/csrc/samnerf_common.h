@@ -65,11 +65,20 @@ __device__ __forceinline__ void locate_axis(float u, uint32_t res, uint32_t& cel
     frac = p - (float)cell;
 }
 
+// fminf(fmaxf(p, 0), top) for top >= 0 as one v_med3_f32 (fminf / fmaxf
+// also canonicalise an operand loaded from memory: 3 VALU -> 1).  Same
+// value for every p: med3 of a NaN input is min3 = 0 (IEEE minNum skips the
+// quiet NaN), as fminf(fmaxf(NaN, 0), top) = 0; p = fma(u, res, -0.5) is
+// never -0.
+__device__ __forceinline__ float clamp_med3(float p, float top) {
+    return __builtin_amdgcn_fmed3f(p, 0.0f, top);
+}
+
 // The same with the level's float resolution precomputed: frac = p -
 // floorf(p) is p - (float)cell exactly (p in [0, res - 1], res < 2^24).
 __device__ __forceinline__ void locate_axis(float u, const LevelDesc& d, uint32_t& cell, float& frac) {
     float p = __builtin_fmaf(u, d.fres, -0.5f);
-    p = fminf(fmaxf(p, 0.0f), d.ftop);
+    p = clamp_med3(p, d.ftop);
     const float fl = floorf(p);
     cell = (uint32_t)fl;
     frac = p - fl;

@@ -29,6 +29,8 @@ for tag, seed, es, n in (("parity", 23, 0.5, 262144), ("default", 0, 1e-4, 26214
     net = make_net(spec, synth.make_params(spec, seed=seed, emb_scale=es, ln_jitter=0.1), cuda)
     pose, intr = synth.gui_camera(512, 512, rot=synth.random_rotation(seed + 5))
     ro, rd = ops.get_rays(pose, intr, 512, 512, device=cuda)
+    rd[1000] = float("nan")                      # a NaN ray (NaN positions in every kernel)
+    rd[2000, 1] = float("inf")
     rows = torch.empty(n, ROW, device=cuda)
     o = FusedRenderer(net).render(ro[:n], rd[:n], rows=rows)
     torch.cuda.synchronize()
