@@ -86,6 +86,11 @@ def parse():
                          "smaller view): the per-rank load of the N-GPU bench; value = that band's "
                          "rays/s")
     ap.add_argument("--share-rank", type=int, default=-1, help="band index for --rank-share (default N//2)")
+    ap.add_argument("--gather-codec", choices=["fp32", "q16"], default=None,
+                    help="transport of the per-view all-gather at N > 1 (samnerf_amd/dist.py): "
+                         "q16 = 536 B/ray records, samvit as int16 with a per-ray power-of-two "
+                         "scale (|err| <= 2^-14 of the ray's max, own band exact); fp32 = 1,044 B/ray. "
+                         "Default q16 with SAM features, fp32 without")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -335,7 +340,9 @@ def main():
             return pipe.collect_ready()
         return render_fn(*ray_fn(r0, r1 - r0))
 
-    pipe = ShardedViewPipeline(renderer.render, H, W) if world > 1 and args.chunks == 0 else None
+    codec = args.gather_codec or ("q16" if with_sam else "fp32")
+    pipe = (ShardedViewPipeline(renderer.render, H, W, codec=codec)
+            if world > 1 and args.chunks == 0 else None)
 
     for _ in range(args.warmup):
         step()
@@ -396,7 +403,11 @@ def main():
                                        f"{len(streams)} HIP streams" if args.chunks == 0 else
                                        f"ray-sharded row bands x{world}, {chunks} chunks per band, "
                                        "async RCCL all-gather per chunk") if world > 1
-                       else "single GPU"},
+                       else "single GPU",
+                       **({"gather_codec": codec + (" (536 B/ray: samvit int16 x per-ray power-of-two "
+                                                    "scale, |err| <= 2^-14 of the ray max; own band fp32)"
+                                                    if codec == "q16" else " (1,044 B/ray)")}
+                          if world > 1 and args.chunks == 0 else {})},
             # with > 1 stream the HIP-event stage times include the overlap with
             # the other streams' views (longer than a kernel alone)
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,

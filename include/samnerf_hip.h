@@ -208,6 +208,19 @@ int samnerf_sgrid_backward(const samnerf_model* model, const float* grad_fsam, u
                            float* grad_embeddings, const void* workspace,
                            size_t workspace_bytes, samnerf_stream_t stream);
 
+/* Transport record of the per-ray outputs for the all-gather of a
+ * ray-sharded view (samnerf_amd/dist.py; no reference counterpart: the
+ * reference renders on one GPU, nerf/renderer.py:185-219).  One record of
+ * samnerf_tile_words() 32-bit words per ray: image[3], depth, weights_sum
+ * (fp32, exact), a power-of-two scale s and samvit[256] as int16 q = rint(v/s)
+ * (|v - q s| <= 2^-14 of the ray's max |samvit|; NaN / inf rays decode to NaN).
+ * samvit must be 16-B aligned, tile 8-B aligned; N = 0 is a no-op. */
+uint32_t samnerf_tile_words(void);
+int samnerf_tile_encode(const float* image, const float* depth, const float* weights_sum,
+                        const float* samvit, uint32_t N, void* tile, samnerf_stream_t stream);
+int samnerf_tile_decode(const void* tile, uint32_t N, float* image, float* depth,
+                        float* weights_sum, float* samvit, samnerf_stream_t stream);
+
 /* Measurement hook (bench.py): when set, samnerf_render_forward records
  * events[i] (hipEvent_t) on its stream before stage i (0 prop0, 1 prop1,
  * 2 final, 3 s_grid, 4 SAM head) and events[5] after the last one.  n = 0 or

@@ -313,7 +313,9 @@ __global__ void __launch_bounds__(256) k_prop_pdf(PropArgs a) {
     // the wave): T/4 independent loads per thread in flight at once, instead
     // of one thread per ray loading its whole row in dependent batches.
     // (Staging the input bins of stage > 0 as well doubles the LDS of
-    // k_prop_pdf<64> and halves its occupancy: measured slower.)
+    // k_prop_pdf<64> and halves its occupancy: measured slower.  32 rays per
+    // block -- twice the resident phase-A waves -- measured no faster: 0.593
+    // -> 0.611 ms prop0 at a full view, 0.103 -> 0.101 ms at 32K rays.)
     if (lane < nr) {
         constexpr int TQ = T / 4;
         float v[TQ];

@@ -62,6 +62,9 @@ _SIGS = {
                                 _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp], _int),
     "samnerf_sgrid_backward": ([ctypes.POINTER(SamnerfModel), _vp, _u32, _vp, _vp, _sz, _vp],
                                _int),
+    "samnerf_tile_words": ([], _u32),
+    "samnerf_tile_encode": ([_vp, _vp, _vp, _vp, _u32, _vp, _vp], _int),
+    "samnerf_tile_decode": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp], _int),
     "samnerf_set_stage_events": ([ctypes.POINTER(_vp), _u32], _int),
 }
 

@@ -148,33 +148,77 @@ class ShardedViewPipeline:
     collective on RCCL's stream); collect_ready()/flush() make the current
     stream wait for the oldest gather and return its outputs in image order.
     One full-size launch per view and rank (no chunking): the communication
-    hides behind the next view's kernels instead of shrinking them."""
+    hides behind the next view's kernels instead of shrinking them.
+
+    codec = "fp32" gathers the outputs as they are (1,044 B per ray with the
+    SAM features).  codec = "q16" gathers the transport records of
+    ops.tile_encode (tile_codec.hip: 536 B per ray; image / depth /
+    weights_sum exact, samvit as int16 with a per-ray power-of-two scale,
+    |error| <= 2^-14 of the ray's max |samvit|); each rank's own band is put
+    back in fp32 after decoding, so only the other ranks' copies carry the
+    quantisation.  q16 needs CUDA outputs with samvit (there is no CPU codec)."""
 
     def __init__(self, render_fn, H, W, keys=("image", "depth", "weights_sum", "samvit"),
-                 group=None, depth=1):
+                 group=None, depth=1, codec="fp32"):
+        if codec not in ("fp32", "q16"):
+            raise ValueError(f"codec must be 'fp32' or 'q16', got {codec!r}")
         self.render_fn, self.H, self.W = render_fn, H, W
-        self.keys, self.group, self.depth = keys, group, depth
+        self.keys, self.group, self.depth, self.codec = keys, group, depth, codec
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         if H % self.world:
             raise ValueError(f"H={H} must be divisible by the world size {self.world}")
         self.band = H // self.world
         self.inflight = []
+        self.side = None
 
     def submit(self, ray_fn, render_fn=None):
         ro, rd = ray_fn(self.rank * self.band, self.band)
         out = (render_fn or self.render_fn)(ro, rd)
         keys = [k for k in self.keys if k in out]
         widths = [out[k].reshape(out[k].shape[0], -1).shape[1] for k in keys]
-        tile = pack_outputs(out, keys)
+        if self.codec == "q16":
+            from .ops import tile_encode
+            if keys != ["image", "depth", "weights_sum", "samvit"]:
+                raise RuntimeError("q16 codec: needs image, depth, weights_sum and samvit outputs")
+            tile = tile_encode(out)
+        else:
+            tile = pack_outputs(out, keys)
         buf = tile.new_empty(self.world * tile.shape[0], tile.shape[1])
         work = _all_gather(buf, tile, self.group, async_op=True)
-        self.inflight.append((work, buf, tile, keys, widths))
+        ready = None
+        if self.codec == "q16":                # this view's outputs (and a host-staged gather)
+            ready = torch.cuda.Event()
+            ready.record()
+        self.inflight.append((work, buf, tile, keys, widths, out, ready))
 
     def _pop(self):
-        work, buf, _tile, keys, widths = self.inflight.pop(0)
-        work.wait()
-        return unpack_outputs(buf, keys, widths)          # rank-major bands = image order
+        work, buf, _tile, keys, widths, own, ready = self.inflight.pop(0)
+        if self.codec == "fp32":
+            work.wait()
+            return unpack_outputs(buf, keys, widths)      # rank-major bands = image order
+        # Decode on a side stream so it overlaps the next view's kernels: the
+        # side stream waits for this view's outputs (event recorded at submit)
+        # and the collective; the caller's stream waits for the decode only
+        # before the work it queues after this call.
+        from .ops import tile_decode
+        cur = torch.cuda.current_stream(buf.device)
+        if self.side is None:
+            self.side = torch.cuda.Stream(buf.device)
+        self.side.wait_event(ready)
+        with torch.cuda.stream(self.side):
+            work.wait()
+            res = tile_decode(buf)
+            n = own["depth"].shape[0]
+            for k in keys:                                 # this rank's band stays exact
+                res[k][self.rank * n:(self.rank + 1) * n] = own[k]
+        buf.record_stream(self.side)
+        for k in keys:
+            own[k].record_stream(self.side)
+        cur.wait_stream(self.side)
+        for v in res.values():
+            v.record_stream(cur)
+        return res
 
     def collect_ready(self):
         """Outputs of the oldest view once more than `depth` views are in flight."""

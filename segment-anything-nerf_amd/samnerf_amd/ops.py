@@ -199,3 +199,38 @@ def linspace_host(start, end, steps):
     buf = (ctypes.c_float * steps)()
     lib().samnerf_linspace_host(float(start), float(end), steps, buf)
     return list(buf)
+
+
+def tile_words():
+    return int(lib().samnerf_tile_words())
+
+
+def tile_encode(out):
+    """Per-ray render outputs (image [N,3], depth [N], weights_sum [N], samvit
+    [N,256]) -> transport records [N, tile_words()] int32 (tile_codec.hip)."""
+    t = {k: out[k].contiguous() for k in ("image", "depth", "weights_sum", "samvit")}
+    for k, v in t.items():
+        _f32(v, k)
+        _cuda(v, k)
+    N = t["depth"].shape[0]
+    if t["samvit"].shape != (N, 256) or t["image"].shape != (N, 3) or t["weights_sum"].shape != (N,):
+        raise RuntimeError("tile_encode: expected image [N,3], depth [N], weights_sum [N], samvit [N,256]")
+    tile = torch.empty(N, tile_words(), dtype=torch.int32, device=t["depth"].device)
+    check(lib().samnerf_tile_encode(_ptr(t["image"]), _ptr(t["depth"]), _ptr(t["weights_sum"]),
+                                    _ptr(t["samvit"]), N, _ptr(tile), _stream(tile)), "tile_encode")
+    return tile
+
+
+def tile_decode(tile):
+    """Inverse of tile_encode: records [N, tile_words()] int32 -> dict of fp32 outputs."""
+    _cuda(tile, "tile")
+    _contig(tile, "tile")
+    if tile.dtype != torch.int32 or tile.dim() != 2 or tile.shape[1] != tile_words():
+        raise RuntimeError(f"tile_decode: expected an int32 [N, {tile_words()}] tensor")
+    N, dev = tile.shape[0], tile.device
+    out = {"image": torch.empty(N, 3, device=dev), "depth": torch.empty(N, device=dev),
+           "weights_sum": torch.empty(N, device=dev), "samvit": torch.empty(N, 256, device=dev)}
+    check(lib().samnerf_tile_decode(_ptr(tile), N, _ptr(out["image"]), _ptr(out["depth"]),
+                                    _ptr(out["weights_sum"]), _ptr(out["samvit"]), _stream(tile)),
+          "tile_decode")
+    return out
