@@ -47,6 +47,10 @@ ALG_BYTES_PER_RAY = {
     "sam_head": 164 * 4 + 256 * 4,
 }
 ALG_BYTES_RAY_TOTAL = 226_348
+# SAM head (network.py:36-75): 163->256, 256->256, 419->256, 256->256, 256->256
+HEAD_FLOP_PER_RAY = 2 * 256 * (163 + 256 + 419 + 256 + 256)  # 691,200
+BF16_MFMA_PEAK_TFS = 2500.0    # MI355X_MICROARCH.md: dense BF16 ~2.5 PF
+F32_MFMA_PEAK_TFS = 157.3      # MI355X_MICROARCH.md: F32 matrix = vector peak
 
 
 def parse():
@@ -415,6 +419,25 @@ def main():
                          "alg_bytes_per_launch": dom_bytes,
                          "avg_launch_ms": stage_avg[dom]},
             "stage_ms": stage_avg,
+            # every stage against its own roofline: gather stages by algorithmic
+            # bytes (as `roofline`), the SAM head by FLOP on the matrix cores --
+            # useful fp32-equivalent FLOP/s, and the bf16 MFMA issue rate it
+            # implies (bf16x3: three bf16 products per fp32 product) vs 2.5 PF
+            "stage_roofline": {
+                **{st: {"bound": "hbm", "unit": "GB/s",
+                        "achieved": ALG_BYTES_PER_RAY[st] * band_rays / (stage_avg[st] * 1e-3) / 1e9,
+                        "frac": ALG_BYTES_PER_RAY[st] * band_rays / (stage_avg[st] * 1e-3) / 1e9
+                        / HBM_PEAK_GBS}
+                   for st in STAGES if st != "sam_head" and stage_avg.get(st, 0) > 0},
+                **({"sam_head": {
+                    "bound": "mfma", "unit": "TFLOP/s",
+                    "achieved_fp32_equiv": HEAD_FLOP_PER_RAY * band_rays / (stage_avg["sam_head"] * 1e-3) / 1e12,
+                    "vs_f32_mfma_peak": HEAD_FLOP_PER_RAY * band_rays / (stage_avg["sam_head"] * 1e-3) / 1e12
+                    / F32_MFMA_PEAK_TFS,
+                    "mfma_issue_frac": (1 if args.head_mode == 1 else 3) * HEAD_FLOP_PER_RAY * band_rays
+                    / (stage_avg["sam_head"] * 1e-3) / 1e12
+                    / (F32_MFMA_PEAK_TFS if args.head_mode == 1 else BF16_MFMA_PEAK_TFS)}}
+                   if with_sam and stage_avg.get("sam_head", 0) > 0 else {})},
         }
         if world == 1 and args.ref_gpu_rays > 0:
             ro_all, rd_all = ops.get_rays(pose, intr, H, W, device=dev)
