@@ -347,7 +347,10 @@ struct HeadStepper {
         }
     }
 
-    // one k-block of the current layer for all 8 output tiles
+    // one k-block of the current layer for all 8 output tiles.  (Holding the
+    // next step's fragments in registers, read under this step's MFMAs with
+    // the skip layer's h-part moved first to make room, measured no faster:
+    // 0.581 vs 0.575 ms per view, with 21 VGPRs spilled.)
     __device__ __forceinline__ void run(floatx16 (&acc)[8], const uint4& bh, const uint4& bl) {
         const bool ahead = step + 2 < kSteps;
         if (ahead) issue(step + 2);
