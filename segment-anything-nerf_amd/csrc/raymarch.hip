@@ -1315,10 +1315,12 @@ void mark_stage(uint32_t i, hipStream_t s) {
 }
 
 // Default k_sgrid form by launch size: the de-duplicated box gathers win
-// on a full view (TA-bound direct gathers), the direct gathers on one rank's
-// share of a sharded view (latency-bound at 3 waves per SIMD): measured
-// 0.94 vs 1.05 ms at 262,144 rays, 0.25 vs 0.21 ms at 32,768.
-constexpr uint32_t kBox4MinRays = 131072;
+// on a full view (TA-bound direct gathers): 0.83 vs 1.05 ms at 262,144 rays.
+// Since the integer-bit range reduction and v_med3 clamp they also win on one
+// rank's share of a sharded view: 0.120 vs 0.132 ms at 32,768 rays, 0.228 vs
+// 0.262 at 65,536 (bands of the 512x512 view, bench --rank-share 8 / 4).
+// Below 32,768 rays (not measured) the direct form stays.
+constexpr uint32_t kBox4MinRays = 32768;
 
 // k_final's cross-sample prefetch of one k-block's gathers: on for S = 1
 // (a full view: 1.01 -> 0.99 ms), off for S = 2 / 4 (one rank's share), whose
