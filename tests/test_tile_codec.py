@@ -132,3 +132,74 @@ def test_pipeline_q16_keeps_own_band_exact(hip_lib, cuda, tmp_path):
             ShardedViewPipeline(render_fn, H, W, codec="fp16")
     finally:
         dist.destroy_process_group()
+
+
+def _q16_worker(rank, world, port, q):
+    """One rank of a world-2 gloo group on GPU 0 (both ranks share the card,
+    as in the single-GPU rehearsal of the multi-rank bench)."""
+    import os
+    import sys
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "segment-anything-nerf_amd"))
+        from samnerf_amd.dist import ShardedViewPipeline
+        dev = torch.device("cuda", 0)
+        H, W = 8, 12
+
+        def band(r, n):                      # rank r's outputs, reproducible on every rank
+            g = torch.Generator().manual_seed(100 + r)
+            return {"image": torch.rand(n, 3, generator=g), "depth": torch.rand(n, generator=g),
+                    "weights_sum": torch.rand(n, generator=g),
+                    "samvit": torch.randn(n, 256, generator=g) * (1 + 3 * r)}
+
+        def render_fn(ro, rd):
+            return {k: v.to(dev) for k, v in band(rank, ro.shape[0]).items()}
+
+        def ray_fn(row0, rows):
+            return torch.zeros(rows * W, 3, device=dev), torch.zeros(rows * W, 3, device=dev)
+
+        pipe = ShardedViewPipeline(render_fn, H, W, codec="q16")
+        pipe.submit(ray_fn)
+        (res,) = pipe.flush()
+        n = H * W // world
+        ok = True
+        for r in range(world):
+            ref = band(r, n)
+            got = {k: v[r * n:(r + 1) * n].cpu() for k, v in res.items()}
+            for k in ("image", "depth", "weights_sum"):
+                ok &= torch.equal(got[k], ref[k])
+            if r == rank:
+                ok &= torch.equal(got["samvit"], ref["samvit"])        # own band exact
+            else:
+                err = (got["samvit"] - ref["samvit"]).abs().amax(dim=1)
+                ok &= bool((err <= ref["samvit"].abs().amax(dim=1) * 2.0 ** -14).all())
+                ok &= not torch.equal(got["samvit"], ref["samvit"])    # it did go through q16
+        q.put((rank, bool(ok)))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_pipeline_q16_world2_gloo_on_one_gpu(hip_lib, cuda):
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_q16_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok in res:
+        assert ok is True, f"rank {rank}: {ok}"
