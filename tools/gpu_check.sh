@@ -20,9 +20,9 @@ timeout -k 10 200 python bench.py --H $h --cpu-rays 0 --steps 20 > "$OUT/bench_h
 done
 if [ "${SKIP_PROF:-0}" != "1" ]; then
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_trace" -o trace -- python "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --cpu-rays 0 > "$OUT/prof_trace.log" 2>&1; rc=$?; echo "prof trace rc=$rc"; stop_if_fatal $rc prof_trace
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_trace" -o trace -- python "$GRAFT_REPO_ROOT/bench.py" --streams 1 --steps 5 --warmup 2 --cpu-rays 0 > "$OUT/prof_trace.log" 2>&1; rc=$?; echo "prof trace rc=$rc"; stop_if_fatal $rc prof_trace
 [ "${TRACE_ONLY:-0}" = "1" ] && exit 0
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/prof_fetch" -o fetch -- python "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-rays 0 > "$OUT/prof_fetch.log" 2>&1; rc=$?; echo "prof fetch rc=$rc"; stop_if_fatal $rc prof_fetch
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/prof_write" -o write -- python "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-rays 0 > "$OUT/prof_write.log" 2>&1; rc=$?; echo "prof write rc=$rc"; stop_if_fatal $rc prof_write
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/prof_fetch" -o fetch -- python "$GRAFT_REPO_ROOT/bench.py" --streams 1 --steps 3 --warmup 1 --cpu-rays 0 > "$OUT/prof_fetch.log" 2>&1; rc=$?; echo "prof fetch rc=$rc"; stop_if_fatal $rc prof_fetch
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/prof_write" -o write -- python "$GRAFT_REPO_ROOT/bench.py" --streams 1 --steps 3 --warmup 1 --cpu-rays 0 > "$OUT/prof_write.log" 2>&1; rc=$?; echo "prof write rc=$rc"; stop_if_fatal $rc prof_write
 fi
 find "$OUT" -name "*.csv" | head -20
