@@ -178,43 +178,42 @@ class ShardedViewPipeline:
         keys = [k for k in self.keys if k in out]
         widths = [out[k].reshape(out[k].shape[0], -1).shape[1] for k in keys]
         if self.codec == "q16":
+            # encode + gather (+ later decode) on a side stream, ordered after
+            # this view's kernels, so they overlap the next view's
             from .ops import tile_encode
             if keys != ["image", "depth", "weights_sum", "samvit"]:
                 raise RuntimeError("q16 codec: needs image, depth, weights_sum and samvit outputs")
-            tile = tile_encode(out)
+            dev = out["samvit"].device
+            if self.side is None:
+                self.side = torch.cuda.Stream(dev)
+            self.side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(self.side):
+                tile = tile_encode(out)
+                buf = tile.new_empty(self.world * tile.shape[0], tile.shape[1])
+                work = _all_gather(buf, tile, self.group, async_op=True)
+            for k in keys:
+                out[k].record_stream(self.side)
         else:
             tile = pack_outputs(out, keys)
-        buf = tile.new_empty(self.world * tile.shape[0], tile.shape[1])
-        work = _all_gather(buf, tile, self.group, async_op=True)
-        ready = None
-        if self.codec == "q16":                # this view's outputs (and a host-staged gather)
-            ready = torch.cuda.Event()
-            ready.record()
-        self.inflight.append((work, buf, tile, keys, widths, out, ready))
+            buf = tile.new_empty(self.world * tile.shape[0], tile.shape[1])
+            work = _all_gather(buf, tile, self.group, async_op=True)
+        self.inflight.append((work, buf, tile, keys, widths, out))
 
     def _pop(self):
-        work, buf, _tile, keys, widths, own, ready = self.inflight.pop(0)
+        work, buf, _tile, keys, widths, own = self.inflight.pop(0)
         if self.codec == "fp32":
             work.wait()
             return unpack_outputs(buf, keys, widths)      # rank-major bands = image order
-        # Decode on a side stream so it overlaps the next view's kernels: the
-        # side stream waits for this view's outputs (event recorded at submit)
-        # and the collective; the caller's stream waits for the decode only
-        # before the work it queues after this call.
+        # Decode on the side stream, behind the collective; the caller's
+        # stream waits for it only before the work it queues after this call.
         from .ops import tile_decode
         cur = torch.cuda.current_stream(buf.device)
-        if self.side is None:
-            self.side = torch.cuda.Stream(buf.device)
-        self.side.wait_event(ready)
         with torch.cuda.stream(self.side):
             work.wait()
             res = tile_decode(buf)
             n = own["depth"].shape[0]
             for k in keys:                                 # this rank's band stays exact
                 res[k][self.rank * n:(self.rank + 1) * n] = own[k]
-        buf.record_stream(self.side)
-        for k in keys:
-            own[k].record_stream(self.side)
         cur.wait_stream(self.side)
         for v in res.values():
             v.record_stream(cur)
