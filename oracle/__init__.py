@@ -10,6 +10,8 @@ Contents
                reference's gridencoder / shencoder / freqencoder .cu kernels)
   renderer.py  torch-CPU restatement of nerf/renderer.py + nerf/network.py
                (+ get_rays from nerf/utils.py), op for op, citing file:line
+  tile_codec.py  numpy restatement of the multi-GPU gather's transport record
+               (tile_codec.hip), checked against its own error bound
   synth.py     re-export of samnerf_amd/synth.py (deterministic parameter /
                camera synthesis) for the tests and the golden generator
 
