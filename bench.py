@@ -5,22 +5,28 @@ Workload (BASELINE.json configs[2] = "garden --with_sam: RGB + 256-dim SAM
 feature head, 512x512, 1xMI355X"): one STEP renders one 512x512 GUI view
 (262,144 rays: get_rays + 3 proposal rounds 128/64/32 + hash grids + MLPs +
 compositing + 256-d SAM head per ray) on synthetic random-init weights of the
-reference architecture.  With --gpus N > 1 (torchrun, one rank per GPU) the
-view's rows are split into N equal bands (strong scaling on a fixed view) and
-the packed per-ray outputs [rays/N, 3+1+1+256] are all-gathered over RCCL, as
-BASELINE config 4 / SURVEY.md 8e describe.  Each step is one full view on every
-rank; view i's all-gather runs behind view i+1's kernels, and the last view's
-gather completes inside the timed region.
+reference architecture.  With --gpus N > 1 the view's rows are split into N
+equal bands, one rank per GPU (strong scaling on a fixed view), and the packed
+per-ray outputs [rays/N, 3+1+1+256] are all-gathered over RCCL, as BASELINE
+config 4 / SURVEY.md 8e describe.  `python bench.py --gpus N` starts the N
+ranks itself (torch.distributed.run, as a child process) when it is not
+already running under a launcher.  Each step is one full view on every rank;
+view i's all-gather runs behind view i+1's kernels, and the last view's
+gather completes inside the timed region.  The headline gathers fp32 (exact);
+the lossy q16 transport is timed after it and reported beside it.
 
 Prints ONE JSON line (rank 0).  `value` = rays of the whole view x steps /
 (max over ranks of the timed region).  `roofline` prices the dominant kernel
-from HIP events recorded on the launch stream inside the timed steps;
-`cpu_baseline` times the CPU oracle (torch-CPU restatement of the reference
-renderer + C restatement of its encoders) on a bounded sample of rays.
+against the unit that binds it (the texture-address path of the gathers,
+DESIGN.md 5) from HIP events recorded on the launch stream inside the timed
+steps; `cpu_baseline` times the CPU oracle (torch-CPU restatement of the
+reference renderer + C restatement of its encoders) on the view's rays, and
+`parity_vs_ref` compares a parity-weight render of the same view with it.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -34,6 +40,15 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "rays/sec (RGB+256-d SAM feat) at 512×512, 1/2/4/8 MI355X; PSNR vs ref"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md: L2 ~34.5 TB/s aggregate
+CLOCK_GHZ = 2.4                # MI355X_MICROARCH.md: max clock
+N_CU, N_SIMD = 256, 1024
+# Texture-address path: a 64-lane gather instruction holds TA for ~16 cycles
+# whatever its width or coalescing (TA_BUSY and TCP_TOTAL_CACHE_ACCESSES per
+# VMEM instruction, profiles/r1s4_pmc_counters.txt), i.e. 4 lane
+# addresses per clock per CU.
+TA_LANES_PER_CLK = 4
+TA_PEAK_GADDR = N_CU * TA_LANES_PER_CLK * CLOCK_GHZ           # 2,457.6 G lane-addresses/s
 
 # Algorithmic bytes per ray and stage (SURVEY.md 8d / BASELINE.md 3): fp32
 # embedding gathers (8 corners x C x 4 B per level per sample) + the stage's
@@ -47,15 +62,35 @@ ALG_BYTES_PER_RAY = {
     "sam_head": 164 * 4 + 256 * 4,
 }
 ALG_BYTES_RAY_TOTAL = 226_348
+# Gather lane-addresses per ray the kernels issue (the TA work), from their
+# gather code: dense levels load each x-adjacent corner pair with one 16-B
+# load (4 addresses instead of 8), hashed levels 8 per level.
+#   k_prop_sigma<128>: prop0 has 3 dense + 2 hashed levels -> 28 per sample
+#   k_prop_sigma<64>:  prop1 has 2 dense + 3 hashed levels -> 32 per sample
+#   k_final:           levels 0-3 dense in paired slots (16), level 4 dense but
+#                      sharing its slot with hashed level 5, 12 levels x 8 -> 112
+GATHER_ADDR_PER_RAY = {"prop0": 128 * 28, "prop1": 64 * 32, "final": 32 * 112}
 # SAM head (network.py:36-75): 163->256, 256->256, 419->256, 256->256, 256->256
 HEAD_FLOP_PER_RAY = 2 * 256 * (163 + 256 + 419 + 256 + 256)  # 691,200
+# MFMA issue of the head per 32 rays (one wave): 86 k-blocks of 16 (K padded
+# 176 + 256 + 432 + 256 + 256) x 8 output tiles x 3 bf16 products
+# (v_mfma_f32_32x32x16_bf16, 32 cycles); exact mode: 688 k-steps of 2 x 8
+# tiles on v_mfma_f32_32x32x2_f32 (64 cycles).
+HEAD_MFMA_CYCLES_PER_32 = {0: 86 * 8 * 3 * 32, 1: 688 * 8 * 64}
 BF16_MFMA_PEAK_TFS = 2500.0    # MI355X_MICROARCH.md: dense BF16 ~2.5 PF
 F32_MFMA_PEAK_TFS = 157.3      # MI355X_MICROARCH.md: F32 matrix = vector peak
+DTYPE = {0: "fp32 in the reference's op order for everything that decides a discrete result "
+            "(near/far, bins, proposal grids + MLPs, compositing, sample_pdf); grid_mlp "
+            "(32->64->64->16 per sample) and the SAM head (163->256x5) on bf16x3 split-precision "
+            "MFMA with fp32 accumulate (~1e-5 relative); view_mlp on fp32 MFMA",
+         1: "fp32 throughout: grid_mlp, view_mlp and the SAM head on fp32 MFMA "
+            "(v_mfma_f32_32x32x2_f32), the rest in the reference's op order"}
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without a launcher environment bench.py starts them")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--H", type=int, default=512)
@@ -66,16 +101,19 @@ def parse():
     ap.add_argument("--ref-gpu-rays", type=int, default=262144,
                     help="rays of the view rendered by run_torch, the reference's unfused op "
                          "sequence on the same GPU (0 = skip)")
-    ap.add_argument("--head-mode", type=int, default=0, help="0 bf16x3 SAM head, 1 exact fp32")
+    ap.add_argument("--head-mode", type=int, default=0,
+                    help="0 = bf16x3 split-precision grid_mlp + SAM head (default), 1 = exact fp32 MFMA")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="skip the side measurements after the headline (exact-fp32 precision at "
+                         "N=1, q16 transport at N>1)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="N > 1: 0 = one launch per view with its all-gather pipelined behind "
                          "the next view's rendering; k > 0 = k row chunks per view, each "
                          "chunk's all-gather behind the next chunk")
     ap.add_argument("--streams", type=int, default=0,
                     help="HIP streams the views are issued on round-robin, so view i+1's kernels "
-                         "overlap view i's (each stream has its own workspace).  0 = 1 on one GPU "
-                         "(+2%% measured, and per-kernel HIP-event times stay unshared for the "
-                         "roofline), 2 for 2-4 ranks, 3 for 8 (one rank's 32K-ray share: +16%%)")
+                         "overlap view i's (each stream has its own workspace).  0 = 2 for 1-4 "
+                         "ranks, 3 for 8 (one rank's 32K-ray share: +16%%)")
     ap.add_argument("--mode", choices=["render", "train", "gui"], default="render",
                     help="render: cfg 3 view throughput (the headline metric); train: cfg 5 "
                          "SAM-feature distillation step (4096 rays, forward + backward + Adam); "
@@ -90,19 +128,43 @@ def parse():
                          "smaller view): the per-rank load of the N-GPU bench; value = that band's "
                          "rays/s")
     ap.add_argument("--share-rank", type=int, default=-1, help="band index for --rank-share (default N//2)")
-    ap.add_argument("--gather-codec", choices=["fp32", "q16"], default=None,
-                    help="transport of the per-view all-gather at N > 1 (samnerf_amd/dist.py): "
-                         "q16 = 536 B/ray records, samvit as int16 with a per-ray power-of-two "
-                         "scale (|err| <= 2^-14 of the ray's max, own band exact); fp32 = 1,044 B/ray. "
-                         "Default q16 with SAM features, fp32 without")
+    ap.add_argument("--gather-codec", choices=["fp32", "q16"], default="fp32",
+                    help="transport of the headline's per-view all-gather at N > 1 "
+                         "(samnerf_amd/dist.py): fp32 = 1,044 B/ray, exact (default); q16 = 536 B/ray "
+                         "records, samvit as int16 with a per-ray power-of-two scale (|err| <= 2^-14 "
+                         "of the ray's max, own band exact).  The other codec is timed after the "
+                         "headline and reported beside it (unless --no-alt)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
+
+
+def maybe_launch(args):
+    """`--gpus N` > 1 outside a torch.distributed launcher: start the N ranks
+    (torch.distributed.run on 127.0.0.1, one process per GPU) as a child
+    process and return its exit status.  Runs before anything touches the
+    GPU; returns None when this process is already a rank (or N = 1)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC for RCCL on this host
+    return subprocess.call(cmd, env=env)
 
 
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; run "
+                         f"`python bench.py --gpus {args.gpus}` (it launches the ranks) or a "
+                         f"launcher with --nproc-per-node {args.gpus}")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # --dist-backend gloo --share-gpu: a rehearsal of the multi-rank code
@@ -119,11 +181,14 @@ def setup_dist(args):
     return rank, world, torch.device("cuda", 0)
 
 
-def build_net(with_sam, device):
+def build_net(with_sam, device, seed=0, emb_scale=1e-4):
+    """NeRFNetwork with synthesised weights: the bench's default-init scene
+    (embeddings U(+-1e-4) as grid.py:144-146) or, with emb_scale 0.5, the
+    parity-weight scene of the tests."""
     from nerf.network import NeRFNetwork, default_opt
     from samnerf_amd import synth
     spec = synth.ModelSpec(with_sam=with_sam)
-    params = synth.make_params(spec, seed=0, emb_scale=1e-4, ln_jitter=0.0)
+    params = synth.make_params(spec, seed=seed, emb_scale=emb_scale, ln_jitter=0.0)
     net = NeRFNetwork(default_opt(with_sam=with_sam))
     net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
     return net.to(device).eval(), spec, params
@@ -154,7 +219,7 @@ def cpu_baseline(spec, params, pose, intr, H, W, n_rays, gpu_out=None):
         g = {k: v.detach().float().cpu() for k, v in gpu_out.items()}
         img_g, img_r = g["image"][idx], ref["image"].reshape(-1, 3)
         mse = float(((img_g - img_r) ** 2).mean())
-        parity = {"rays": n_rays, "weights": "the bench's default-init weights (see tests/ for parity weights)",
+        parity = {"rays": n_rays, "weights": "parity weights: embeddings U(+-0.5), seed 33 (tests/, SURVEY.md 8c)",
                   "psnr_image_db": float("inf") if mse == 0 else -10.0 * float(np.log10(mse)),
                   "max_abs_image": float((img_g - img_r).abs().max()),
                   "max_abs_depth_rel": float(((g["depth"][idx] - ref["depth"].reshape(-1)).abs()
@@ -278,18 +343,192 @@ def gui_main(args, dev):
         "vs_baseline": None}), flush=True)
 
 
+class ViewRunner:
+    """Issues views of this rank's row band on `n_streams` HIP streams (each
+    with its own workspace) and, at N > 1, all-gathers each view through a
+    ShardedViewPipeline (view i's gather behind view i+1's kernels)."""
+
+    def __init__(self, args, renderer, world, dev, H, W, pose, intr, r0, r1, codec):
+        from samnerf_amd.dist import ShardedViewPipeline
+        self.args, self.renderer, self.world, self.dev = args, renderer, world, dev
+        self.H, self.W, self.pose, self.intr, self.r0, self.r1 = H, W, pose, intr, r0, r1
+        self.chunks = max(1, args.chunks) if world > 1 else 1
+        # measured best (DESIGN.md 7): 2 streams up to 4 ranks (N=1: 3.25 -> 3.18
+        # ms per view), 3 at 8 ranks
+        n_streams = args.streams or (2 if world <= 4 else 3)
+        self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
+                                                           for _ in range(n_streams - 1)]
+        self.n_step = 0
+        self.pipe = (ShardedViewPipeline(renderer.render, H, W, codec=codec)
+                     if world > 1 and args.chunks == 0 else None)
+
+    def _step_on_stream(self, raws=None):
+        from samnerf_amd import ops
+        from samnerf_amd._lib import lib
+        from samnerf_amd.dist import render_view_sharded
+        it = iter(raws or [])
+        H, W, dev = self.H, self.W, self.dev
+
+        def ray_fn(row0, rows):
+            return ops.get_rays(self.pose, self.intr, H, W, device=dev, row0=row0, rows=rows)
+
+        def render_fn(ro, rd):
+            raw = next(it, None)
+            lib().samnerf_set_stage_events(raw, 6 if raw is not None else 0)
+            return self.renderer.render(ro, rd)
+
+        if self.world > 1 and self.args.chunks > 0:
+            return render_view_sharded(render_fn, ray_fn, H, W, chunks=self.chunks)
+        if self.world > 1:
+            self.pipe.submit(ray_fn, render_fn)   # this view's gather overlaps the next view
+            return self.pipe.collect_ready()
+        return render_fn(*ray_fn(self.r0, self.r1 - self.r0))
+
+    def step(self, raws=None):
+        s = self.streams[self.n_step % len(self.streams)]
+        self.n_step += 1
+        with torch.cuda.stream(s):
+            return self._step_on_stream(raws)
+
+    def _flush(self):
+        return self.pipe.flush() if self.pipe is not None else []
+
+    def run(self, steps, warmup, stages=True):
+        """Warm up, then time exactly `steps` views bracketed by a barrier and
+        a device synchronisation on both sides; returns (max-over-ranks
+        seconds, the last view's outputs, per-stage ms, their source)."""
+        from samnerf_amd._lib import lib
+        import ctypes
+
+        def make_event_set():
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+            for e in evs:                      # create the underlying hipEvent_t
+                e.record()
+            raw = (ctypes.c_void_p * 6)(*[e.cuda_event for e in evs])
+            return evs, raw
+
+        for _ in range(warmup):
+            self.step()
+        self._flush()
+        sets = [[make_event_set() for _ in range(self.chunks)] for _ in range(steps)] if stages else None
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        last = None
+        for i in range(steps):
+            last = self.step([raw for _, raw in sets[i]] if stages else None)
+        flushed = self._flush()                  # the last view's gather is inside the timed region
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        lib().samnerf_set_stage_events(None, 0)
+        if flushed:
+            last = flushed[-1]
+        if self.world > 1:
+            t = torch.tensor([dt], device=self.dev if self.args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = t.item()
+        if not stages:
+            return dt, last, None, None
+        stage_src = "the timed views"
+        if len(self.streams) > 1:
+            # Stage times for the rooflines from a single-stream pass after the
+            # timed region: with several views in flight, one view's HIP events
+            # also span the other streams' kernels.  Every rank runs it (the
+            # views' gathers are collectives).
+            n_roof = min(steps, 5)
+            sets = [[make_event_set() for _ in range(self.chunks)] for _ in range(n_roof)]
+            torch.cuda.synchronize()
+            for i in range(n_roof):
+                self._step_on_stream([raw for _, raw in sets[i]])
+            self._flush()
+            torch.cuda.synchronize()
+            lib().samnerf_set_stage_events(None, 0)
+            stage_src = f"a single-stream pass of {n_roof} views after the timed region"
+        stage_avg = {}          # per step: summed over the chunks of the rank's band
+        for j, st in enumerate(STAGES):
+            stage_avg[st] = float(np.mean([sum(evs[j].elapsed_time(evs[j + 1]) for evs, _ in chunk_sets)
+                                           for chunk_sets in sets]))
+        return dt, last, stage_avg, stage_src
+
+
+def rooflines(stage_avg, band_rays, head_mode, band_traffic):
+    """`roofline` of the dominant kernel and every stage against the unit its
+    counters say binds it: the gather kernels against the
+    texture-address rate, the SAM head against its MFMA issue rate.  frac <= 1
+    by construction: the counts are of work the kernels issue."""
+    def ta(st):
+        ms = stage_avg.get(st, 0.0)
+        if ms <= 0:
+            return None
+        addr = GATHER_ADDR_PER_RAY[st] * band_rays
+        ach = addr / (ms * 1e-3) / 1e9
+        alg = ALG_BYTES_PER_RAY[st] * band_rays
+        return {"bound": "ta", "unit": "Gaddr/s", "achieved": ach, "peak": TA_PEAK_GADDR,
+                "frac": ach / TA_PEAK_GADDR, "lane_addresses_per_ray": GATHER_ADDR_PER_RAY[st],
+                "l2_frac_of_alg_bytes": alg / (ms * 1e-3) / 1e9 / L2_PEAK_GBS}
+
+    stages = {st: ta(st) for st in ("prop0", "prop1", "final")}
+    if stage_avg.get("sam_head", 0) > 0:
+        ms = stage_avg["sam_head"]
+        cyc = HEAD_MFMA_CYCLES_PER_32[head_mode] * band_rays / 32
+        frac = cyc / (N_SIMD * CLOCK_GHZ * 1e9 * ms * 1e-3)
+        stages["sam_head"] = {
+            "bound": "mfma", "unit": "TFLOP/s", "frac": frac,
+            "achieved_fp32_equiv": HEAD_FLOP_PER_RAY * band_rays / (ms * 1e-3) / 1e12,
+            "peak": F32_MFMA_PEAK_TFS if head_mode == 1 else BF16_MFMA_PEAK_TFS,
+            "basis": "MFMA issue cycles of the head's structure (bf16x3: 86 k-blocks x 8 tiles x 3 "
+                     "v_mfma_f32_32x32x16_bf16 per 32 rays) / (1024 SIMDs x 2.4 GHz x time)"}
+    if stage_avg.get("s_grid", 0) > 0:
+        ms = stage_avg["s_grid"]
+        alg = ALG_BYTES_PER_RAY["s_grid"] * band_rays
+        stages["s_grid"] = {
+            "bound": "valu", "frac": None,
+            "note": "de-duplicated LDS box gathers: VALU-bound (77% VALU busy, 24% TA, "
+                    "profiles/r1s4_pmc_counters.txt); the algorithmic gather rate below is not a "
+                    "roofline (rows are read once per wave, not per lane)",
+            "alg_gather_tbs": alg / (ms * 1e-3) / 1e12}
+    stages = {k: v for k, v in stages.items() if v is not None}
+    cands = {k: stage_avg[k] for k in ("prop0", "prop1", "final") if stage_avg.get(k, 0) > 0}
+    dom = max(cands, key=cands.get)
+    roof = dict(stages[dom])
+    roof.update({"kernel": dom, "avg_launch_ms": stage_avg[dom],
+                 "alg_bytes_per_launch": ALG_BYTES_PER_RAY[dom] * band_rays})
+    t = band_traffic.get(dom) if band_traffic else None
+    roof["traffic"] = t
+    roof["hbm_frac_counters"] = (t / (stage_avg[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS) if t else None
+    return roof, stages
+
+
+def pmc_traffic(band_rays, n_view):
+    """HBM bytes per launch of each stage from the committed rocprofv3 PMC
+    passes (profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE per the
+    guide's gfx950 correction), scaled to this band."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        return {k: v["hbm_bytes"] * band_rays / n_view for k, v in d.items() if "hbm_bytes" in v}
+    except Exception:
+        return {}
+
+
 def main():
     args = parse()
-    if args.mode == "train":
+    rc = maybe_launch(args)
+    if rc is not None:
+        sys.exit(rc)
+    if args.mode in ("train", "gui"):
+        if args.gpus != 1:
+            raise SystemExit(f"--mode {args.mode} runs on one GPU")
         torch.cuda.set_device(0)
-        return train_main(args, torch.device("cuda", 0))
-    if args.mode == "gui":
-        torch.cuda.set_device(0)
-        return gui_main(args, torch.device("cuda", 0))
+        fn = train_main if args.mode == "train" else gui_main
+        return fn(args, torch.device("cuda", 0))
     rank, world, dev = setup_dist(args)
     from samnerf_amd import ops
-    from samnerf_amd._lib import lib
-    from samnerf_amd.dist import ShardedViewPipeline, render_view_sharded, shard_range
+    from samnerf_amd.dist import shard_range
     from samnerf_amd.fused import FusedRenderer
     from samnerf_amd import synth
 
@@ -305,115 +544,49 @@ def main():
         r0, r1 = shard_range(H, k, args.rank_share)
         n_total = (r1 - r0) * W
     band_rays = (r1 - r0) * W
-    chunks = max(1, args.chunks) if world > 1 else 1
+    codec = args.gather_codec
 
-    import ctypes
-
-    def make_event_set():
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-        for e in evs:                      # create the underlying hipEvent_t
-            e.record()
-        raw = (ctypes.c_void_p * 6)(*[e.cuda_event for e in evs])
-        return evs, raw
-
-    # measured best: 2 streams up to 4 ranks (N=1: 3.25 -> 3.18 ms
-    # per view), 3 at 8 ranks
-    n_streams = args.streams or (2 if world <= 4 else 3)
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_streams - 1)]
-    n_step = [0]
-
-    def step(raws=None):
-        s = streams[n_step[0] % len(streams)]
-        n_step[0] += 1
-        with torch.cuda.stream(s):
-            return step_on_stream(raws)
-
-    def step_on_stream(raws=None):
-        it = iter(raws or [])
-
-        def ray_fn(row0, rows):
-            return ops.get_rays(pose, intr, H, W, device=dev, row0=row0, rows=rows)
-
-        def render_fn(ro, rd):
-            raw = next(it, None)
-            lib().samnerf_set_stage_events(raw, 6 if raw is not None else 0)
-            return renderer.render(ro, rd)
-
-        if world > 1 and args.chunks > 0:
-            return render_view_sharded(render_fn, ray_fn, H, W, chunks=chunks)
-        if world > 1:
-            pipe.submit(ray_fn, render_fn)   # this view's gather overlaps the next view
-            return pipe.collect_ready()
-        return render_fn(*ray_fn(r0, r1 - r0))
-
-    codec = args.gather_codec or ("q16" if with_sam else "fp32")
-    pipe = (ShardedViewPipeline(renderer.render, H, W, codec=codec)
-            if world > 1 and args.chunks == 0 else None)
-
-    for _ in range(args.warmup):
-        step()
-    if pipe is not None:
-        pipe.flush()
-    sets = [[make_event_set() for _ in range(chunks)] for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    last = None
-    for i in range(args.steps):
-        last = step([raw for _, raw in sets[i]])
-    if pipe is not None:
-        pipe.flush()                         # the last view's gather is inside the timed region
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    lib().samnerf_set_stage_events(None, 0)
-    if world > 1:
-        t = torch.tensor([dt], device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
-    stage_src = "the timed views"
-    if len(streams) > 1:
-        # Stage times for the rooflines from a single-stream pass after the
-        # timed region: with several views in flight, one view's HIP events
-        # also span the other streams' kernels.  Every rank runs it (the
-        # views' gathers are collectives).
-        n_roof = min(args.steps, 5)
-        sets = [[make_event_set() for _ in range(chunks)] for _ in range(n_roof)]
-        torch.cuda.synchronize()
-        for i in range(n_roof):
-            step_on_stream([raw for _, raw in sets[i]])
-        if pipe is not None:
-            pipe.flush()
-        torch.cuda.synchronize()
-        lib().samnerf_set_stage_events(None, 0)
-        stage_src = f"a single-stream pass of {n_roof} views after the timed region"
-    stage_avg = {}          # per step: summed over the chunks of the rank's band
-    for j, s in enumerate(STAGES):
-        stage_avg[s] = float(np.mean([sum(evs[j].elapsed_time(evs[j + 1]) for evs, _ in chunk_sets)
-                                      for chunk_sets in sets]))
-
+    runner = ViewRunner(args, renderer, world, dev, H, W, pose, intr, r0, r1, codec)
+    dt, last, stage_avg, stage_src = runner.run(args.steps, args.warmup)
     value = n_total * args.steps / dt
-    dom = max(stage_avg, key=stage_avg.get)
-    dom_bytes = ALG_BYTES_PER_RAY[dom] * band_rays
-    achieved = dom_bytes / (stage_avg[dom] * 1e-3) / 1e9 if stage_avg[dom] > 0 else 0.0
-    traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            t = json.load(open(pmc)).get(dom)
-            traffic = t["hbm_bytes"] * band_rays / n_total if t else None
-        except Exception:
-            traffic = None
+    roof, stage_roof = rooflines(stage_avg, band_rays, args.head_mode,
+                                 pmc_traffic(band_rays, H * W))
+
+    side = {}
+    if not args.no_alt and world > 1 and with_sam and args.chunks == 0:
+        # the other transport, same views, after the headline
+        other = "q16" if codec == "fp32" else "fp32"
+        r2 = ViewRunner(args, renderer, world, dev, H, W, pose, intr, r0, r1, other)
+        dt2, last2, _, _ = r2.run(args.steps, args.warmup, stages=False)
+        err = (last2["samvit"] - last["samvit"]).abs().max().reshape(1).float()
+        if args.dist_backend != "nccl":
+            err = err.cpu()
+        dist.all_reduce(err, op=dist.ReduceOp.MAX)
+        side[f"gather_codec_{other}"] = {
+            "value": n_total * args.steps / dt2, "unit": "rays/s", "ms_per_step": dt2 * 1e3 / args.steps,
+            "max_abs_samvit_vs_" + codec: float(err.item()),
+            "what": "q16: 536 B/ray transport, samvit int16 x per-ray power-of-two scale, |err| <= "
+                    "2^-14 of the ray's max |samvit|, own band fp32" if other == "q16" else
+                    "fp32: 1,044 B/ray exact transport"}
+    if not args.no_alt and world == 1 and args.rank_share <= 1:
+        # the other precision mode on the same view (DTYPE)
+        other = 1 - args.head_mode
+        r3 = ViewRunner(args, FusedRenderer(net, head_mode=other), 1, dev, H, W, pose, intr, r0, r1, codec)
+        dt3, last3, st3, _ = r3.run(max(3, args.steps // 2), 2)
+        side["precision_" + ("exact_fp32" if other == 1 else "bf16x3")] = {
+            "value": n_total * max(3, args.steps // 2) / dt3, "unit": "rays/s",
+            "ms_per_step": dt3 * 1e3 / max(3, args.steps // 2), "stage_ms": st3, "dtype": DTYPE[other],
+            "max_abs_samvit_vs_headline": float((last3["samvit"] - last["samvit"]).abs().max())
+            if with_sam else None,
+            "max_abs_image_vs_headline": float((last3["image"] - last["image"]).abs().max())}
 
     if rank == 0:
         rec = {
             "metric": METRIC, "value": value, "unit": "rays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt * 1e3 / args.steps,
-            "streams": len(streams),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32" if args.head_mode == 1 else "fp32 (SAM head: bf16x3 split-precision MFMA, fp32 accumulate)",
+            "streams": len(runner.streams),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": DTYPE[args.head_mode],
             "data": "synthetic (random-init weights of the reference architecture, GUI camera)",
             "config": {"workload": ("cfg3: 512x512 view, RGB + 256-d SAM feature per ray" if with_sam
                                     else "cfg2: 512x512 view, RGB only") if (H, W) == (512, 512)
@@ -422,39 +595,19 @@ def main():
                        "rays_per_step": n_total, "num_steps": [128, 64, 32],
                        "parallelism": (f"ray-sharded row bands x{world}, RCCL all-gather of each view "
                                        f"overlapped with the next view's rendering, views issued on "
-                                       f"{len(streams)} HIP streams" if args.chunks == 0 else
-                                       f"ray-sharded row bands x{world}, {chunks} chunks per band, "
+                                       f"{len(runner.streams)} HIP streams" if args.chunks == 0 else
+                                       f"ray-sharded row bands x{world}, {runner.chunks} chunks per band, "
                                        "async RCCL all-gather per chunk") if world > 1
                        else "single GPU",
                        **({"gather_codec": codec + (" (536 B/ray: samvit int16 x per-ray power-of-two "
                                                     "scale, |err| <= 2^-14 of the ray max; own band fp32)"
-                                                    if codec == "q16" else " (1,044 B/ray)")}
+                                                    if codec == "q16" else " (1,044 B/ray, exact)")}
                           if world > 1 and args.chunks == 0 else {})},
             "stage_ms_source": stage_src,
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "alg_bytes_per_launch": dom_bytes,
-                         "avg_launch_ms": stage_avg[dom]},
+            "roofline": roof,
             "stage_ms": stage_avg,
-            # every stage against its own roofline: gather stages by algorithmic
-            # bytes (as `roofline`), the SAM head by FLOP on the matrix cores --
-            # useful fp32-equivalent FLOP/s, and the bf16 MFMA issue rate it
-            # implies (bf16x3: three bf16 products per fp32 product) vs 2.5 PF
-            "stage_roofline": {
-                **{st: {"bound": "hbm", "unit": "GB/s",
-                        "achieved": ALG_BYTES_PER_RAY[st] * band_rays / (stage_avg[st] * 1e-3) / 1e9,
-                        "frac": ALG_BYTES_PER_RAY[st] * band_rays / (stage_avg[st] * 1e-3) / 1e9
-                        / HBM_PEAK_GBS}
-                   for st in STAGES if st != "sam_head" and stage_avg.get(st, 0) > 0},
-                **({"sam_head": {
-                    "bound": "mfma", "unit": "TFLOP/s",
-                    "achieved_fp32_equiv": HEAD_FLOP_PER_RAY * band_rays / (stage_avg["sam_head"] * 1e-3) / 1e12,
-                    "vs_f32_mfma_peak": HEAD_FLOP_PER_RAY * band_rays / (stage_avg["sam_head"] * 1e-3) / 1e12
-                    / F32_MFMA_PEAK_TFS,
-                    "mfma_issue_frac": (1 if args.head_mode == 1 else 3) * HEAD_FLOP_PER_RAY * band_rays
-                    / (stage_avg["sam_head"] * 1e-3) / 1e12
-                    / (F32_MFMA_PEAK_TFS if args.head_mode == 1 else BF16_MFMA_PEAK_TFS)}}
-                   if with_sam and stage_avg.get("sam_head", 0) > 0 else {})},
+            "stage_roofline": stage_roof,
+            **side,
         }
         if world == 1 and args.ref_gpu_rays > 0:
             ro_all, rd_all = ops.get_rays(pose, intr, H, W, device=dev)
@@ -462,8 +615,14 @@ def main():
             ref["speedup"] = value / ref["value"]
             rec["reference_equivalent_gpu"] = ref
         if world == 1 and args.cpu_rays > 0:
+            # parity weights (embeddings U(+-0.5)): a non-trivial
+            # scene for the PSNR / max-error comparison; the same view
+            pnet, pspec, pparams = build_net(with_sam, dev, seed=33, emb_scale=0.5)
+            ro_all, rd_all = ops.get_rays(pose, intr, H, W, device=dev)
+            pout = FusedRenderer(pnet, head_mode=args.head_mode).render(ro_all, rd_all)
+            torch.cuda.synchronize()
             rec["cpu_baseline"], rec["parity_vs_ref"] = cpu_baseline(
-                spec, params, pose, intr, H, W, args.cpu_rays, gpu_out=last)
+                pspec, pparams, pose, intr, H, W, args.cpu_rays, gpu_out=pout)
         else:
             rec["cpu_baseline"] = None
         print(json.dumps(rec), flush=True)

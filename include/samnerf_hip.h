@@ -221,6 +221,33 @@ int samnerf_tile_encode(const float* image, const float* depth, const float* wei
 int samnerf_tile_decode(const void* tile, uint32_t N, float* image, float* depth,
                         float* weights_sum, float* samvit, samnerf_stream_t stream);
 
+/* Parity taps (tests only; no reference counterpart -- they expose what
+ * nerf/renderer.py:261-307 computes between its ops).  While set, every
+ * samnerf_render_forward call of this thread over exactly N rays writes the
+ * proposal stages' intermediates to these device buffers instead of its
+ * workspace (the same kernels run; outputs are unchanged), sample-major:
+ *   ds0 [128][N], ds1 [64][N]   optical depth delta * sigma of each proposal
+ *                               sample (renderer.py:310-311)
+ *   w0 [128][N], w1 [64][N]     their composited weights (renderer.py:312-326),
+ *                               the input of sample_pdf
+ *   bins1 [65][N], bins2 [33][N]  the resampled bins of sample_pdf
+ *                               (renderer.py:274-275)
+ *   inds1 [65][N], inds2 [33][N]  its torch.searchsorted(cdf, u, right=True)
+ *                               indices (renderer.py:105), int32
+ * Any pointer may be NULL.  taps = NULL clears them; a render over another
+ * ray count fails with SAMNERF_EINVAL while they are set.  Thread-local. */
+typedef struct {
+    float* ds0;
+    float* ds1;
+    float* w0;
+    float* w1;
+    float* bins1;
+    float* bins2;
+    int32_t* inds1;
+    int32_t* inds2;
+} samnerf_taps;
+int samnerf_set_taps(const samnerf_taps* taps, uint32_t N);
+
 /* Measurement hook (bench.py): when set, samnerf_render_forward records
  * events[i] (hipEvent_t) on its stream before stage i (0 prop0, 1 prop1,
  * 2 final, 3 s_grid, 4 SAM head) and events[5] after the last one.  n = 0 or

@@ -107,6 +107,12 @@ def composite_weights(real_bins, sigmas, last_sample=True):
     """nerf/renderer.py:310-326: sigmas -> weights."""
     deltas = (real_bins[..., 1:] - real_bins[..., :-1])
     deltas_sigmas = deltas * sigmas
+    return composite_from_ds(deltas_sigmas, last_sample)
+
+
+def composite_from_ds(deltas_sigmas, last_sample=True):
+    """nerf/renderer.py:312-326, from the optical depths deltas * sigmas on
+    (the parity taps of the fused path hand these over, samnerf_set_taps)."""
     if last_sample:
         deltas_sigmas = torch.cat(
             [deltas_sigmas[..., :-1], torch.full_like(deltas_sigmas[..., -1:], torch.inf)], dim=-1)

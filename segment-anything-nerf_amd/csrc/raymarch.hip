@@ -159,6 +159,8 @@ struct PropArgs {
     float* snf;            // [2][N] spacing(near), spacing(far)
     float* wtmp;           // [T][N]: ds per sample
     float* bins_out;       // [TN][N]
+    int32_t* inds_out;     // [TN][N] searchsorted indices, or null (parity taps only)
+    float* w_out;          // [T][N] composited weights, or null (parity taps only)
 };
 
 // Proposal stage, part 1: one thread per (ray, sample).  A wave is 64
@@ -331,6 +333,8 @@ __global__ void __launch_bounds__(256) k_prop_pdf(PropArgs a) {
         double cum = 0.0;
 #pragma unroll 8
         for (int k = 0; k < T; ++k) row[k] = composite_step(row[k], cum, k == T - 1);
+        if (a.w_out)
+            for (int k = 0; k < T; ++k) a.w_out[(size_t)k * N + r0 + lane] = row[k];
         const float wsum = torch_row_sum(T, [&](int i) { return row[i] + 0.01f; });
         double c = 0.0;
         float wnext = row[0];
@@ -371,6 +375,7 @@ __global__ void __launch_bounds__(256) k_prop_pdf(PropArgs a) {
         float t = nan_to_num((u - g0) / (g1 - g0));
         t = fminf(fmaxf(t, 0.0f), 1.0f);
         a.bins_out[(size_t)j * N + r] = b0 + t * (b1 - b0);
+        if (a.inds_out) a.inds_out[(size_t)j * N + r] = i;    // torch.searchsorted(cdf, u, right=True)
     }
 }
 
@@ -480,6 +485,28 @@ __device__ float view_weight(const FinalArgs& a, int idx) {
     }
     const int r = (idx - kV3) >> 6;
     return i < 3 ? a.V2[i * 32 + rho(r) + 4 * h] : 0.0f;
+}
+
+// Exact-fp32 grid_mlp (head_mode 1) on v_mfma_f32_32x32x2_f32: one weight
+// per lane and k-step, A[i][k = h] for the lane (i, h), 128 k-steps:
+//   layer 1  step = ob*16 + kb*8 + m        (m: register of the gathered f[8])
+//   layer 2  step = 32 + ob*32 + t*16 + q   (q: register of accumulator tile t)
+//   layer 3  step = 96 + t*16 + q
+// Each MFMA is the fma chain of its two k terms in k order (exact fp32).
+constexpr int kXSteps = 128;
+
+__device__ float grid_weight_exact(const FinalArgs& a, int step, int lane) {
+    const int i = lane & 31, h = lane >> 5;
+    if (step < 32) {
+        const int ob = step >> 4, kb = (step >> 3) & 1, m = step & 7;
+        return a.G0[(ob * 32 + i) * 32 + 2 * final_level(kb, h, m >> 1) + (m & 1)];
+    }
+    if (step < 96) {
+        const int s = step - 32, ob = s >> 5, t = (s >> 4) & 1, q = s & 15;
+        return a.G1[(ob * 32 + i) * 64 + t * 32 + rho(q) + 4 * h];
+    }
+    const int s = step - 96, t = s >> 4, q = s & 15;
+    return i < 16 ? a.G2[i * 64 + t * 32 + rho(q) + 4 * h] : 0.0f;
 }
 
 __device__ __forceinline__ void split_pair(float x, float y, uint32_t& hi, uint32_t& lo) {
@@ -671,17 +698,26 @@ __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const Leve
 // final; per-slot partial sums of w, w*t and w*features are added at the end.
 // S > 1 only serves small N (one rank's share of a view): S-times more waves,
 // while a wave still gathers at adjacent samples of neighbouring rays.
-template <int T, int S, bool PF>
+template <int T, int S, bool PF, bool EXACT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_final(FinalArgs a) {
     static_assert(S == 1 || S == 2 || S == 4, "segments per ray");
+    static_assert(kXSteps * 64 == 2 * kFSlots * 64 * 4, "exact weights reuse the bf16x3 slots");
     constexpr int R = 32 / S, TS = T / S;
-    __shared__ uint4 Fh[kFSlots * 64], Fl[kFSlots * 64];
+    __shared__ uint4 Fbuf[2 * kFSlots * 64];          // bf16x3: hi | lo fragments; exact: fp32 steps
     __shared__ float Vl[kVTotal];
-    for (int idx = threadIdx.x; idx < kFSlots * 64; idx += 256) {
-        float v[8];
+    uint4* const Fh = Fbuf;
+    uint4* const Fl = Fbuf + kFSlots * 64;
+    float* const Fx = reinterpret_cast<float*>(Fbuf);
+    if constexpr (EXACT) {
+        for (int idx = threadIdx.x; idx < kXSteps * 64; idx += 256)
+            Fx[idx] = grid_weight_exact(a, idx >> 6, idx & 63);
+    } else {
+        for (int idx = threadIdx.x; idx < kFSlots * 64; idx += 256) {
+            float v[8];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) v[m] = grid_weight(a, idx >> 6, idx & 63, m);
-        split8(v, Fh[idx], Fl[idx]);
+            for (int m = 0; m < 8; ++m) v[m] = grid_weight(a, idx >> 6, idx & 63, m);
+            split8(v, Fh[idx], Fl[idx]);
+        }
     }
     for (int idx = threadIdx.x; idx < kVTotal; idx += 256) Vl[idx] = view_weight(a, idx);
     __syncthreads();
@@ -795,6 +831,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         asm volatile("" : "+v"(wo));
         const uint4* FH = Fh + wo;
         const uint4* FL = Fl + wo;
+        const float* FX = Fx + wo;
 
         floatx16 h1a = {}, h1b = {};
 #pragma unroll
@@ -808,10 +845,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
                 levels(kb, dl);
                 gather_levels_c2<4, S == 1>(emb, dl, ux, uy, uz, f, kinds(kb));
             }
-            uint4 bh, bl;
-            split8(f, bh, bl);
-            h1a = mfma3(FH[(kF1 + 2 * kb) * 64], FL[(kF1 + 2 * kb) * 64], bh, bl, h1a);
-            h1b = mfma3(FH[(kF1 + 2 * kb + 1) * 64], FL[(kF1 + 2 * kb + 1) * 64], bh, bl, h1b);
+            if constexpr (EXACT) {
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    h1a = MFMA32(FX[(kb * 8 + m) * 64], f[m], h1a);
+                    h1b = MFMA32(FX[(16 + kb * 8 + m) * 64], f[m], h1b);
+                }
+            } else {
+                uint4 bh, bl;
+                split8(f, bh, bl);
+                h1a = mfma3(FH[(kF1 + 2 * kb) * 64], FL[(kF1 + 2 * kb) * 64], bh, bl, h1a);
+                h1b = mfma3(FH[(kF1 + 2 * kb + 1) * 64], FL[(kF1 + 2 * kb + 1) * 64], bh, bl, h1b);
+            }
         }
         if constexpr (PF) {
             if (i + 1 < TS) {
@@ -828,16 +873,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
             h1b[i] = fmaxf(h1b[i], 0.0f);
         }
         floatx16 h2a = {}, h2b = {};
+        if constexpr (EXACT) {
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb) {
-            float v[8];
+            for (int t = 0; t < 2; ++t) {
 #pragma unroll
-            for (int m = 0; m < 8; ++m) v[m] = (kb >> 1) ? h1b[8 * (kb & 1) + m] : h1a[8 * (kb & 1) + m];
-            uint4 bh, bl;
-            split8(v, bh, bl);
-            h2a = mfma3(FH[(kF2 + 2 * kb) * 64], FL[(kF2 + 2 * kb) * 64], bh, bl, h2a);
-            h2b = mfma3(FH[(kF2 + 2 * kb + 1) * 64], FL[(kF2 + 2 * kb + 1) * 64], bh, bl, h2b);
-            __builtin_amdgcn_sched_barrier(0);
+                for (int q = 0; q < 16; ++q) {
+                    const float v = t ? h1b[q] : h1a[q];
+                    h2a = MFMA32(FX[(32 + t * 16 + q) * 64], v, h2a);
+                    h2b = MFMA32(FX[(64 + t * 16 + q) * 64], v, h2b);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb) {
+                float v[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) v[m] = (kb >> 1) ? h1b[8 * (kb & 1) + m] : h1a[8 * (kb & 1) + m];
+                uint4 bh, bl;
+                split8(v, bh, bl);
+                h2a = mfma3(FH[(kF2 + 2 * kb) * 64], FL[(kF2 + 2 * kb) * 64], bh, bl, h2a);
+                h2b = mfma3(FH[(kF2 + 2 * kb + 1) * 64], FL[(kF2 + 2 * kb + 1) * 64], bh, bl, h2b);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -845,15 +903,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
             h2b[i] = fmaxf(h2b[i], 0.0f);
         }
         floatx16 o3 = {};
+        if constexpr (EXACT) {
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb) {
-            float v[8];
+            for (int t = 0; t < 2; ++t) {
 #pragma unroll
-            for (int m = 0; m < 8; ++m) v[m] = (kb >> 1) ? h2b[8 * (kb & 1) + m] : h2a[8 * (kb & 1) + m];
-            uint4 bh, bl;
-            split8(v, bh, bl);
-            o3 = mfma3(FH[(kF3 + kb) * 64], FL[(kF3 + kb) * 64], bh, bl, o3);
-            __builtin_amdgcn_sched_barrier(0);
+                for (int q = 0; q < 16; ++q) o3 = MFMA32(FX[(96 + t * 16 + q) * 64], t ? h2b[q] : h2a[q], o3);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb) {
+                float v[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) v[m] = (kb >> 1) ? h2b[8 * (kb & 1) + m] : h2a[8 * (kb & 1) + m];
+                uint4 bh, bl;
+                split8(v, bh, bl);
+                o3 = mfma3(FH[(kF3 + kb) * 64], FL[(kF3 + kb) * 64], bh, bl, o3);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
 
         // sigma pre-activation = row 0, held by the lower half-wave
@@ -1309,6 +1376,9 @@ int lookup_mode() {
 
 thread_local hipEvent_t g_stage_events[8];
 thread_local uint32_t g_n_stage_events = 0;
+thread_local samnerf_taps g_taps = {};
+thread_local uint32_t g_taps_n = 0;
+thread_local bool g_taps_on = false;
 
 void mark_stage(uint32_t i, hipStream_t s) {
     if (i < g_n_stage_events && g_stage_events[i]) (void)hipEventRecord(g_stage_events[i], s);
@@ -1359,6 +1429,22 @@ void launch_prop_sigma(int look, uint32_t N, hipStream_t s, const PropArgs& pa) 
     else if (look == kLookBox4 && box4_ok(pa.grid))
         k_prop_sigma<T, FIRST, kLookBox4><<<nb, 256, 0, s>>>(pa);
     else k_prop_sigma<T, FIRST, kLookPacked><<<nb, 256, 0, s>>>(pa);
+}
+
+// k_final by ray-segment form S and prefetch; EXACT = the exact-fp32
+// grid_mlp of head_mode 1
+template <bool EXACT>
+void launch_final(int seg, bool pf, uint32_t N, hipStream_t s, const FinalArgs& fa) {
+    if (seg == 1) {
+        if (pf) k_final<32, 1, true, EXACT><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
+        else k_final<32, 1, false, EXACT><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
+    } else if (seg == 2) {
+        if (pf) k_final<32, 2, true, EXACT><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
+        else k_final<32, 2, false, EXACT><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
+    } else {
+        if (pf) k_final<32, 4, true, EXACT><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
+        else k_final<32, 4, false, EXACT><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
+    }
 }
 
 Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
@@ -1529,6 +1615,13 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.gs = make_grid_scale(m->grid_bound);
     pa.snf = w.snf;
     pa.wtmp = w.wtmp;
+    // parity taps (samnerf_set_taps): the stages write their intermediates to
+    // the caller's buffers instead of the workspace; the kernels are the same
+    if (g_taps_on && g_taps_n != N)
+        return fail(SAMNERF_EINVAL, "render: taps were set for %u rays, the call renders %u", g_taps_n, N);
+    const samnerf_taps tp = g_taps_on ? g_taps : samnerf_taps{};
+    float* const bins1 = tp.bins1 ? tp.bins1 : w.bins1;
+    float* const bins2 = tp.bins2 ? tp.bins2 : w.bins2;
 
     // stage 0: 128 uniform samples -> 65 bins (renderer.py:263-267, :274-275)
     pa.grid = gp0;
@@ -1537,7 +1630,10 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.bins0 = make_lin(0.0f, 1.0f, 129);
     pa.u = make_lin((float)(0.5 / 65), (float)(1.0 - 0.5 / 65), 65);
     pa.bins_in = nullptr;
-    pa.bins_out = w.bins1;
+    pa.bins_out = bins1;
+    pa.wtmp = tp.ds0 ? tp.ds0 : w.wtmp;
+    pa.inds_out = tp.inds1;
+    pa.w_out = tp.w0;
     const int look = lookup_mode();
     mark_stage(0, s);
     k_snf<<<div_up(N, 256), 256, 0, s>>>(pa);
@@ -1549,8 +1645,11 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.W0 = m->prop_mlp[1][0];
     pa.W1 = m->prop_mlp[1][1];
     pa.u = make_lin((float)(0.5 / 33), (float)(1.0 - 0.5 / 33), 33);
-    pa.bins_in = w.bins1;
-    pa.bins_out = w.bins2;
+    pa.bins_in = bins1;
+    pa.bins_out = bins2;
+    pa.wtmp = tp.ds1 ? tp.ds1 : w.wtmp;
+    pa.inds_out = tp.inds2;
+    pa.w_out = tp.w1;
     mark_stage(1, s);
     launch_prop_sigma<64, false>(look, N, s, pa);
     k_prop_pdf<64, 33, false><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
@@ -1570,7 +1669,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.V0 = m->view_mlp[0];
     fa.V1 = m->view_mlp[1];
     fa.V2 = m->view_mlp[2];
-    fa.bins_in = w.bins2;
+    fa.bins_in = bins2;
     fa.classes = final_classes();
     fa.snf = w.snf;
     fa.u_out = w.u_f;
@@ -1586,16 +1685,8 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     const char* fs = getenv("SAMNERF_FINAL_S");
     const int seg = fs ? atoi(fs) : (N >= 65536u ? 1 : N >= 32768u ? 2 : 4);
     const bool pf = final_prefetch(seg);
-    if (seg == 1) {
-        if (pf) k_final<32, 1, true><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
-        else k_final<32, 1, false><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
-    } else if (seg == 2) {
-        if (pf) k_final<32, 2, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
-        else k_final<32, 2, false><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
-    } else {
-        if (pf) k_final<32, 4, true><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
-        else k_final<32, 4, false><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
-    }
+    if (m->head_mode == 1) launch_final<true>(seg, pf, N, s, fa);
+    else launch_final<false>(seg, pf, N, s, fa);
 
     if (sam_rows) {
         SgridArgs sa{};
@@ -1627,6 +1718,13 @@ int samnerf_set_stage_events(void* const* events, uint32_t n) {
     g_n_stage_events = events ? n : 0u;
     for (uint32_t i = 0; i < g_n_stage_events; ++i)
         g_stage_events[i] = reinterpret_cast<hipEvent_t>(events[i]);
+    return SAMNERF_OK;
+}
+
+int samnerf_set_taps(const samnerf_taps* taps, uint32_t N) {
+    g_taps_on = taps != nullptr;
+    g_taps = taps ? *taps : samnerf_taps{};
+    g_taps_n = taps ? N : 0u;
     return SAMNERF_OK;
 }
 

@@ -66,7 +66,15 @@ _SIGS = {
     "samnerf_tile_encode": ([_vp, _vp, _vp, _vp, _u32, _vp, _vp], _int),
     "samnerf_tile_decode": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp], _int),
     "samnerf_set_stage_events": ([ctypes.POINTER(_vp), _u32], _int),
+    "samnerf_set_taps": ([ctypes.c_void_p, _u32], _int),
 }
+
+
+class SamnerfTaps(ctypes.Structure):
+    """samnerf_taps (include/samnerf_hip.h): parity-test taps of the render."""
+    _fields_ = [("ds0", _vp), ("ds1", _vp), ("w0", _vp), ("w1", _vp), ("bins1", _vp),
+                ("bins2", _vp), ("inds1", _vp), ("inds2", _vp)]
+
 
 EXPORTED = tuple(_SIGS)
 _lib = None

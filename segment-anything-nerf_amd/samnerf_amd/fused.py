@@ -12,7 +12,7 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import SamnerfGrid, SamnerfModel, check, lib
+from ._lib import SamnerfGrid, SamnerfModel, SamnerfTaps, check, lib
 from .ops import _ptr, _stream
 
 ROW = 164          # head-input row: f_sam 128 | f_image 31 | image 3 | depth 1 | pad
@@ -119,12 +119,16 @@ class FusedRenderer:
     # -------------------------------------------------------------- render --
     @torch.no_grad()
     def render(self, rays_o, rays_d, cam_near_far=None, bg_color=None, rows=None,
-               keep_workspace=False, feats=True):
+               keep_workspace=False, feats=True, taps=False):
         """rays_o, rays_d [N,3] (CUDA fp32) -> dict(image [N,3], depth [N],
         weights_sum [N], samvit [N,256] if with_sam and feats).  `rows`
         (optional [N,164] tensor) receives the head input cat(f_sam, f_image,
         image, depth).  feats=False skips the SAM-feature stages (the
-        reference computes and discards them when return_feats == 0)."""
+        reference computes and discards them when return_feats == 0).
+        taps=True (parity tests) adds the proposal stages' intermediates
+        (samnerf_set_taps): ds0 [N,128], ds1 [N,64], their weights w0, w1, bins1 [N,65],
+        bins2 [N,33] and their searchsorted indices inds1, inds2 (int32),
+        ray-major views of the kernels' sample-major buffers."""
         rays_o = rays_o.contiguous().float()
         rays_d = rays_d.contiguous().float()
         N = rays_o.shape[0]
@@ -150,11 +154,28 @@ class FusedRenderer:
             n_cnf = cnf.shape[0]
         if rows is not None:
             assert rows.shape == (N, ROW) and rows.is_contiguous()
-        check(lib().samnerf_render_forward(
-            ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, _ptr(cnf), n_cnf, bg, _ptr(image),
-            _ptr(depth), _ptr(wsum), _ptr(samvit), _ptr(rows), _ptr(ws), need, _stream(rays_o)),
-            "render_forward")
+        tap = None
+        if taps:
+            steps = [int(v) for v in m.num_steps]
+            tap = {"ds0": torch.empty(steps[0], N, device=dev), "ds1": torch.empty(steps[1], N, device=dev),
+                   "w0": torch.empty(steps[0], N, device=dev), "w1": torch.empty(steps[1], N, device=dev),
+                   "bins1": torch.empty(steps[1] + 1, N, device=dev),
+                   "bins2": torch.empty(steps[2] + 1, N, device=dev),
+                   "inds1": torch.empty(steps[1] + 1, N, device=dev, dtype=torch.int32),
+                   "inds2": torch.empty(steps[2] + 1, N, device=dev, dtype=torch.int32)}
+            st = SamnerfTaps(*[t.data_ptr() for t in tap.values()])
+            check(lib().samnerf_set_taps(ctypes.byref(st), N), "set_taps")
+        try:
+            check(lib().samnerf_render_forward(
+                ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, _ptr(cnf), n_cnf, bg, _ptr(image),
+                _ptr(depth), _ptr(wsum), _ptr(samvit), _ptr(rows), _ptr(ws), need, _stream(rays_o)),
+                "render_forward")
+        finally:
+            if taps:
+                lib().samnerf_set_taps(None, 0)
         out = {"image": image, "depth": depth, "weights_sum": wsum}
+        if tap is not None:
+            out.update({k: v.t() for k, v in tap.items()})
         if samvit is not None:
             out["samvit"] = samvit
         if keep_workspace:
