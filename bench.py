@@ -134,6 +134,8 @@ def parse():
                          "records, samvit as int16 with a per-ray power-of-two scale (|err| <= 2^-14 "
                          "of the ray's max, own band exact).  The other codec is timed after the "
                          "headline and reported beside it (unless --no-alt)")
+    ap.add_argument("--torch-adam", action="store_true",
+                    help="--mode train: torch.optim.Adam (foreach) instead of the one-pass HIP Adam")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -264,7 +266,10 @@ def train_main(args, dev):
     net.train()
     for k, p in net.named_parameters():
         p.requires_grad = k.startswith("s_grid") or k.startswith("samvit_mlp")
-    opt = torch.optim.Adam([p for p in net.parameters()], lr=1e-2, eps=1e-15)
+    from samnerf_amd.optim import FusedAdam
+    params_ = [p for p in net.parameters() if p.requires_grad]
+    opt = (torch.optim.Adam(params_, lr=1e-2, eps=1e-15) if args.torch_adam
+           else FusedAdam(params_, lr=1e-2, eps=1e-15))
     renderer = FusedRenderer(net)
     h = w = 64
     pose, intr = synth.gui_camera(w, h)
@@ -294,7 +299,9 @@ def train_main(args, dev):
            "value": args.steps / dt, "unit": "steps/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True,
            "rays_per_s": 4096 * args.steps / dt, "final_loss": float(loss),
-           "dtype": "fp32 (SAM head bf16x3 in the fused forward; head backward torch fp32)",
+           "optimizer": "torch.optim.Adam (foreach)" if args.torch_adam else
+                        "FusedAdam: one-pass HIP Adam (train_optim.hip), torch.optim.Adam semantics",
+           "dtype": "fp32 (fused forward: grid_mlp bf16x3 MFMA; SAM head forward + backward torch fp32)",
            "data": "synthetic (default-init weights, N(0,1) target)",
            "config": {"workload": "cfg5: 64x64 rays, with_sam, RGB frozen", "optimizer": "Adam lr 1e-2 eps 1e-15"},
            "vs_baseline": None}

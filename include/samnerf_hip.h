@@ -170,8 +170,10 @@ typedef struct {
     float grid_bound;             /* 2 under contract (renderer.py:152-153) */
     float min_near;               /* main.py:69 */
     uint32_t num_steps[3];        /* (128, 64, 32), main.py:79-80 */
-    int head_mode;                /* SAM head GEMMs: 0 = bf16x3 split precision on bf16
-                                     MFMA (~1e-5 relative, default), 1 = exact fp32 MFMA */
+    int head_mode;                /* precision of the GEMMs -- grid_mlp (per sample) and the
+                                     SAM head: 0 = bf16x3 split precision on bf16 MFMA with
+                                     fp32 accumulate (~1e-5 relative, default); 1 = exact
+                                     fp32 MFMA (v_mfma_f32_32x32x2_f32) for both */
 } samnerf_model;
 
 /* Bytes of device workspace samnerf_render_forward needs for N rays. */
@@ -207,6 +209,27 @@ int samnerf_render_forward(const samnerf_model* model, const float* rays_o,
 int samnerf_sgrid_backward(const samnerf_model* model, const float* grad_fsam, uint32_t N,
                            float* grad_embeddings, const void* workspace,
                            size_t workspace_bytes, samnerf_stream_t stream);
+
+/* ------------------------------------------------------------- training --
+ * One Adam step (torch.optim.Adam semantics, amsgrad off, maximize off) over
+ * every tensor of the table in one launch: param -= lr / (1 - beta1^step) *
+ * m / (sqrt(v) / sqrt(1 - beta2^step) + eps) after m, v absorb grad (+
+ * weight_decay * param).  The optimiser of the distillation step
+ * (nerf/utils.py:1831, Adam(lr 1e-2, eps 1e-15) of main.py:296).  Tensors
+ * with a NULL grad are skipped (torch skips parameters without .grad); step
+ * counts from 1 and is the same for every tensor of the call.  The scalars
+ * are doubles (Python floats): derived ones (1 - beta, bias corrections) are
+ * formed in double and rounded to float once, as torch does. */
+typedef struct {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    uint64_t n;                   /* elements */
+} samnerf_adam_tensor;
+int samnerf_adam_step(const samnerf_adam_tensor* tensors_host, uint32_t n_tensors, double lr,
+                      double beta1, double beta2, double eps, double weight_decay, uint32_t step,
+                      samnerf_stream_t stream);
 
 /* Transport record of the per-ray outputs for the all-gather of a
  * ray-sharded view (samnerf_amd/dist.py; no reference counterpart: the

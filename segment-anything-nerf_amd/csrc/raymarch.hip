@@ -33,6 +33,16 @@
 
 using namespace samnerf;
 
+// Diagnostic build knobs (tools/diag/build_variant.sh), defaults = product:
+// the k-block k_final prefetches across samples and whether that prefetch may
+// use the dense pair loads.
+#ifndef SAMNERF_DIAG_KPRE
+#define SAMNERF_DIAG_KPRE 1
+#endif
+#ifndef SAMNERF_DIAG_PF_PAIRS
+#define SAMNERF_DIAG_PF_PAIRS 0
+#endif
+
 namespace samnerf {
 int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, float* samvit,
                      float* packed, hipStream_t s);
@@ -387,7 +397,18 @@ struct FinalArgs {
     GridScale gs;
     float bg;
     const Tables* tab;
-    const float* grid_emb;  // == tab->grid.emb, as a kernel argument so gathers are global_load (not flat)
+    // The main grid's level descriptors by value (kernarg), copied into LDS
+    // at kernel start; each half-wave reads its slot's descriptor from there.
+    // Read through `tab` they were vector loads -- the kernel's stores may
+    // alias a global table, so the compiler cannot use the scalar cache --
+    // and the per-half-wave select became one 64-lane load per field: ~33
+    // extra VMEM instructions per wave and sample competing with the gathers
+    // for the texture-address path (profiles/r2b PMC: 90 VMEM reads per
+    // wave-sample).  Kernarg scalar loads + selects in the loop measured
+    // slower (1.23 vs 0.92 ms: SGPR-bound reloads, lgkmcnt waits).
+    GridDesc<16> grid;
+    uint32_t kdense[2], khashed[2];   // wave-uniform slot classes of k-blocks 0 / 1 (host-side)
+    const float* grid_emb;  // == grid.emb, as a kernel argument so gathers are global_load (not flat)
     const float* G0;   // grid_mlp [64,32]
     const float* G1;   // [64,64]
     const float* G2;   // [16,64]
@@ -402,7 +423,6 @@ struct FinalArgs {
     float* depth;      // [N]
     float* wsum;       // [N]
     float* rows;       // [N, kRow] or null
-    uint32_t classes;  // 1: k_final's uniform slot paths (SAMNERF_FINAL_CLASSES, default on)
 };
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -705,6 +725,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     constexpr int R = 32 / S, TS = T / S;
     __shared__ uint4 Fbuf[2 * kFSlots * 64];          // bf16x3: hi | lo fragments; exact: fp32 steps
     __shared__ float Vl[kVTotal];
+    __shared__ LevelDesc sLv[16];
+    if (threadIdx.x < 16) sLv[threadIdx.x] = a.grid.lv[threadIdx.x];
     uint4* const Fh = Fbuf;
     uint4* const Fl = Fbuf + kFSlots * 64;
     float* const Fx = reinterpret_cast<float*>(Fbuf);
@@ -734,7 +756,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     const bool sample_writer = live && hh == 0;          // u_out / w_out of this segment
     const bool writer = sample_writer && seg == 0;       // per-ray outputs
     const uint32_t N = a.N;
-    const GridDesc<16>* __restrict__ G = &a.tab->grid;
     const float2* __restrict__ emb = reinterpret_cast<const float2*>(a.grid_emb);
 
     float o[3], d[3];
@@ -752,26 +773,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 
     // PF: the first k-block's gathers of sample i + 1 are issued before the
     // layer-2/3 MFMAs of sample i, so their latency hides behind them
-    // level descriptors of k-block kb for this half-wave (scalar loads +
-    // selects, re-evaluated where used rather than held in VGPRs)
+    // level descriptors of k-block kb for this half-wave (LDS reads,
+    // re-evaluated where used rather than held in VGPRs)
     auto levels = [&](int kb, LevelDesc* dl) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            dl[q] = select_level(G->lv[final_level(kb, 0, q)], G->lv[final_level(kb, 1, q)], hh != 0);
+        for (int q = 0; q < 4; ++q) dl[q] = sLv[final_level(kb, hh, q)];
     };
-    // wave-uniform slot classes (scalar loads)
-    auto kinds = [&](int kb) {
-        SlotKinds k{0u, 0u};
-        if (!a.classes) return k;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const bool ha = G->lv[final_level(kb, 0, q)].flags & kHashed;
-            const bool hb = G->lv[final_level(kb, 1, q)].flags & kHashed;
-            k.dense |= (!ha && !hb) ? 1u << q : 0u;
-            k.hashed |= (ha && hb) ? 1u << q : 0u;
-        }
-        return k;
-    };
+    // wave-uniform slot classes (kernel arguments)
+    auto kinds = [&](int kb) { return SlotKinds{a.kdense[kb], a.khashed[kb]}; };
     // PF prefetches k-block kPre = 1 (levels 8-15: hashed in every grid of
     // the path) and gathers k-block 0 -- which holds the dense levels and
     // their pair loads -- inside the iteration.  Pair loads in the prefetched
@@ -779,10 +788,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     // run, tools/diag/final_determinism.py), so the prefetch never uses them.
     // Both forms accumulate layer 1 in the order kPre, 1 - kPre: PF on and off
     // give identical bits.
-    constexpr int kPre = 1;
+    constexpr int kPre = SAMNERF_DIAG_KPRE;
     auto pf_kinds = [&](int kb) {
         SlotKinds k = kinds(kb);
-        k.dense = 0u;
+        if (!SAMNERF_DIAG_PF_PAIRS) k.dense = 0u;
         return k;
     };
     // rb_prev of sample i is rb_next of sample i - 1 when S == 1 (same bits;
@@ -1662,7 +1671,19 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.gs = make_grid_scale(m->grid_bound);
     fa.bg = bg_color;
     fa.tab = w.tables;
+    fa.grid = gg;
     fa.grid_emb = gg.emb;
+    // slot q of k-block kb holds levels final_level(kb, 0 / 1, q): dense in
+    // both half-waves -> pair loads, hashed in both -> select-free rows
+    for (int kb = 0; kb < 2; ++kb) {
+        fa.kdense[kb] = fa.khashed[kb] = 0u;
+        for (int q = 0; q < 4 && final_classes(); ++q) {
+            const bool ha = gg.lv[final_level(kb, 0, q)].flags & kHashed;
+            const bool hb = gg.lv[final_level(kb, 1, q)].flags & kHashed;
+            fa.kdense[kb] |= (!ha && !hb) ? 1u << q : 0u;
+            fa.khashed[kb] |= (ha && hb) ? 1u << q : 0u;
+        }
+    }
     fa.G0 = m->grid_mlp[0];
     fa.G1 = m->grid_mlp[1];
     fa.G2 = m->grid_mlp[2];
@@ -1670,7 +1691,6 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.V1 = m->view_mlp[1];
     fa.V2 = m->view_mlp[2];
     fa.bins_in = bins2;
-    fa.classes = final_classes();
     fa.snf = w.snf;
     fa.u_out = w.u_f;
     fa.w_out = w.w_f;

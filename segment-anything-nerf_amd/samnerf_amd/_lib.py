@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("SAMNERF_LIB") or os.path.join(_HERE, "libsamnerf_hip.
 
 _u32 = ctypes.c_uint32
 _f32 = ctypes.c_float
+_f64 = ctypes.c_double
 _int = ctypes.c_int
 _vp = ctypes.c_void_p
 _sz = ctypes.c_size_t
@@ -67,7 +68,14 @@ _SIGS = {
     "samnerf_tile_decode": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp], _int),
     "samnerf_set_stage_events": ([ctypes.POINTER(_vp), _u32], _int),
     "samnerf_set_taps": ([ctypes.c_void_p, _u32], _int),
+    "samnerf_adam_step": ([ctypes.c_void_p, _u32, _f64, _f64, _f64, _f64, _f64, _u32, _vp], _int),
 }
+
+
+class SamnerfAdamTensor(ctypes.Structure):
+    """samnerf_adam_tensor (include/samnerf_hip.h)."""
+    _fields_ = [("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp),
+                ("n", ctypes.c_uint64)]
 
 
 class SamnerfTaps(ctypes.Structure):

@@ -119,7 +119,7 @@ class FusedRenderer:
     # -------------------------------------------------------------- render --
     @torch.no_grad()
     def render(self, rays_o, rays_d, cam_near_far=None, bg_color=None, rows=None,
-               keep_workspace=False, feats=True, taps=False):
+               keep_workspace=False, feats=True, taps=False, own_workspace=False):
         """rays_o, rays_d [N,3] (CUDA fp32) -> dict(image [N,3], depth [N],
         weights_sum [N], samvit [N,256] if with_sam and feats).  `rows`
         (optional [N,164] tensor) receives the head input cat(f_sam, f_image,
@@ -128,13 +128,20 @@ class FusedRenderer:
         taps=True (parity tests) adds the proposal stages' intermediates
         (samnerf_set_taps): ds0 [N,128], ds1 [N,64], their weights w0, w1, bins1 [N,65],
         bins2 [N,33] and their searchsorted indices inds1, inds2 (int32),
-        ray-major views of the kernels' sample-major buffers."""
+        ray-major views of the kernels' sample-major buffers.
+        own_workspace=True renders into a fresh workspace (from torch's
+        caching allocator) instead of the per-stream one, so a caller can
+        keep it (training: the backward reads its sample weights/positions)."""
         rays_o = rays_o.contiguous().float()
         rays_d = rays_d.contiguous().float()
         N = rays_o.shape[0]
         dev = rays_o.device
         m = self.model()
-        ws, need = self.workspace(m, N, dev)
+        if own_workspace:
+            need = lib().samnerf_render_workspace_size(ctypes.byref(m), N)
+            ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        else:
+            ws, need = self.workspace(m, N, dev)
         if bg_color is None:
             bg = 1.0
         elif torch.is_tensor(bg_color):
@@ -201,11 +208,12 @@ class _FusedSamRows(torch.autograd.Function):
     def forward(ctx, s_emb, renderer, rays_o, rays_d, cam_near_far, bg_color):
         N = rays_o.shape[0]
         rows = torch.empty(N, ROW, device=rays_o.device)
+        # feats=False: the head runs in torch below (it needs autograd), so the
+        # fused head is skipped; a private workspace keeps the sample weights
+        # and positions the s_grid scatter of the backward reads
         out = renderer.render(rays_o, rays_d, cam_near_far, bg_color, rows=rows,
-                              keep_workspace=True)
-        ws = out.pop("_workspace")
-        # own a private workspace copy: the renderer reuses its buffer
-        ctx.ws = (ws[0][:ws[1]].clone(), ws[1], ws[2])
+                              keep_workspace=True, feats=False, own_workspace=True)
+        ctx.ws = out.pop("_workspace")
         ctx.renderer = renderer
         ctx.keep = list(renderer._keep)
         ctx.emb_shape = s_emb.shape
