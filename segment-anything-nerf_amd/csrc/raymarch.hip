@@ -389,23 +389,23 @@ __global__ void __launch_bounds__(256) k_prop_pdf(PropArgs a) {
     }
 }
 
-struct Tables;
 struct FinalArgs {
     const float* rays_o;
     const float* rays_d;
     uint32_t N;
     GridScale gs;
     float bg;
-    const Tables* tab;
     // The main grid's level descriptors by value (kernarg), copied into LDS
     // at kernel start; each half-wave reads its slot's descriptor from there.
-    // Read through `tab` they were vector loads -- the kernel's stores may
-    // alias a global table, so the compiler cannot use the scalar cache --
-    // and the per-half-wave select became one 64-lane load per field: ~33
-    // extra VMEM instructions per wave and sample competing with the gathers
-    // for the texture-address path (profiles/r2b PMC: 90 VMEM reads per
-    // wave-sample).  Kernarg scalar loads + selects in the loop measured
-    // slower (1.23 vs 0.92 ms: SGPR-bound reloads, lgkmcnt waits).
+    // Round 1 read them from a copy in the workspace (written by a one-thread
+    // kernel before each render): the kernel's stores may alias that table,
+    // so the compiler could not use the scalar cache, and the per-half-wave
+    // select became one 64-lane 16-B load per descriptor -- ~33 extra VMEM
+    // instructions per wave and sample competing with the gathers for the
+    // texture-address path (profiles/r2b PMC: 90 VMEM reads per wave-sample),
+    // and the source of the prefetch nondeterminism.  Kernarg
+    // scalar loads + selects in the loop measured slower (1.23 vs 0.92 ms:
+    // SGPR-bound reloads, lgkmcnt waits); LDS: 0.82 ms.
     GridDesc<16> grid;
     uint32_t kdense[2], khashed[2];   // wave-uniform slot classes of k-blocks 0 / 1 (host-side)
     const float* grid_emb;  // == grid.emb, as a kernel argument so gathers are global_load (not flat)
@@ -426,17 +426,6 @@ struct FinalArgs {
 };
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-// Per-call grid geometry, copied into the workspace by k_put_tables so the
-// march kernels read it with scalar loads at a runtime level index (a
-// by-value kernel argument indexed dynamically would go through scratch).
-struct Tables {
-    GridDesc<16> grid, s_grid, prop0, prop1;
-};
-
-__global__ void k_put_tables(Tables t, Tables* __restrict__ dst) {
-    if (threadIdx.x == 0) *dst = t;
-}
 
 // ---- grid_mlp on bf16x3 MFMAs (v_mfma_f32_32x32x16_bf16, fp32 accumulate).
 // Transposed orientation: A = weights (rows = hidden units), B = activations
@@ -783,11 +772,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     auto kinds = [&](int kb) { return SlotKinds{a.kdense[kb], a.khashed[kb]}; };
     // PF prefetches k-block kPre = 1 (levels 8-15: hashed in every grid of
     // the path) and gathers k-block 0 -- which holds the dense levels and
-    // their pair loads -- inside the iteration.  Pair loads in the prefetched
-    // block made the PF form nondeterministic (16-ray groups differing run to
-    // run, tools/diag/final_determinism.py), so the prefetch never uses them.
-    // Both forms accumulate layer 1 in the order kPre, 1 - kPre: PF on and off
-    // give identical bits.
+    // their pair loads -- inside the iteration.  Both forms accumulate layer 1
+    // in the order kPre, 1 - kPre: PF on and off give identical bits.
+    // Prefetching k-block 0 with its pair loads (tools/diag/build_variant.sh
+    // -DSAMNERF_DIAG_KPRE=0 -DSAMNERF_DIAG_PF_PAIRS=1) was nondeterministic in
+    // round 1 while the level descriptors came from per-lane vector loads of
+    // a workspace table; with the descriptors in LDS it is deterministic and
+    // bit-identical to PF off, but 2.4 % slower (0.847 vs 0.827 ms), so
+    // kPre = 1 stays.
     constexpr int kPre = SAMNERF_DIAG_KPRE;
     auto pf_kinds = [&](int kb) {
         SlotKinds k = kinds(kb);
@@ -1365,7 +1357,6 @@ struct Workspace {
     float* w_f;
     float* rows;
     float* packed;
-    Tables* tables;
     size_t bytes;
 };
 
@@ -1474,7 +1465,6 @@ Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
     w.w_f = take((size_t)m->num_steps[2] * n);
     w.rows = take((size_t)kRow * n);
     w.packed = take(m->with_sam ? sam_head_packed_floats() : 0);
-    w.tables = reinterpret_cast<Tables*>(take((sizeof(Tables) + 3) / 4));
     w.bytes = off;
     return w;
 }
@@ -1607,12 +1597,6 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     if (m->with_sam && (rc = make_grid_desc(m->s_grid, 8, 16, gs, "s_grid"))) return rc;
 
     const uint32_t nb = div_up(N, 256);
-    Tables tabs;
-    tabs.grid = gg;
-    tabs.s_grid = m->with_sam ? gs : gg;
-    tabs.prop0 = gp0;
-    tabs.prop1 = gp1;
-    k_put_tables<<<1, 64, 0, s>>>(tabs, w.tables);
     PropArgs pa{};
     pa.rays_o = rays_o;
     pa.rays_d = rays_d;
@@ -1670,7 +1654,6 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.N = N;
     fa.gs = make_grid_scale(m->grid_bound);
     fa.bg = bg_color;
-    fa.tab = w.tables;
     fa.grid = gg;
     fa.grid_emb = gg.emb;
     // slot q of k-block kb holds levels final_level(kb, 0 / 1, q): dense in
