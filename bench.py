@@ -252,23 +252,23 @@ def reference_equivalent_gpu(net, ro, rd, n_rays, chunk=16384):
                     "encoders), chunks of 16384 rays, same view and weights"}
 
 
-def train_main(args, dev):
+def train_steps(dev, steps, warmup, torch_adam=False):
     """BASELINE config 5: one step = fused forward of 4096 rays
     (64x64, fovy 60) with grad, MSE vs a N(0,1) [1,256,64,64] target (seed 1)
     after the reference's bilinear resize, backward (HIP s_grid scatter +
-    torch head), Adam(lr 1e-2, eps 1e-15) over get_params-style groups with
-    the RGB parameters frozen (main.py:255-262, 296; utils.py:1072-1106)."""
+    torch head), Adam(lr 1e-2, eps 1e-15) with the RGB parameters frozen
+    (main.py:255-262, 296; utils.py:1072-1106).  Returns (ms per step, loss)."""
     import torch.nn.functional as F
     from samnerf_amd import ops
     from samnerf_amd.fused import FusedRenderer, render_sam_train
+    from samnerf_amd.optim import FusedAdam
     from samnerf_amd import synth
     net, spec, params = build_net(True, dev)
     net.train()
     for k, p in net.named_parameters():
         p.requires_grad = k.startswith("s_grid") or k.startswith("samvit_mlp")
-    from samnerf_amd.optim import FusedAdam
     params_ = [p for p in net.parameters() if p.requires_grad]
-    opt = (torch.optim.Adam(params_, lr=1e-2, eps=1e-15) if args.torch_adam
+    opt = (torch.optim.Adam(params_, lr=1e-2, eps=1e-15) if torch_adam
            else FusedAdam(params_, lr=1e-2, eps=1e-15))
     renderer = FusedRenderer(net)
     h = w = 64
@@ -287,24 +287,33 @@ def train_main(args, dev):
         opt.zero_grad(set_to_none=True)
         return loss
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         loss = step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    return dt * 1e3 / steps, float(loss)
+
+
+TRAIN_WHAT = {
+    "optimizer": "FusedAdam: one-pass HIP Adam (train_optim.hip), torch.optim.Adam semantics",
+    "dtype": "fp32 (fused forward: grid_mlp bf16x3 MFMA; SAM head forward + backward torch fp32)",
+    "data": "synthetic (default-init weights, N(0,1) target)",
+    "config": {"workload": "cfg5: 64x64 rays, with_sam, RGB frozen", "optimizer": "Adam lr 1e-2 eps 1e-15"},
+}
+
+
+def train_main(args, dev):
+    ms, loss = train_steps(dev, args.steps, args.warmup, args.torch_adam)
     rec = {"metric": "cfg5 SAM distillation train steps/s (4096 rays, fwd+bwd+Adam)",
-           "value": args.steps / dt, "unit": "steps/s", "n_gpus": 1, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True,
-           "rays_per_s": 4096 * args.steps / dt, "final_loss": float(loss),
-           "optimizer": "torch.optim.Adam (foreach)" if args.torch_adam else
-                        "FusedAdam: one-pass HIP Adam (train_optim.hip), torch.optim.Adam semantics",
-           "dtype": "fp32 (fused forward: grid_mlp bf16x3 MFMA; SAM head forward + backward torch fp32)",
-           "data": "synthetic (default-init weights, N(0,1) target)",
-           "config": {"workload": "cfg5: 64x64 rays, with_sam, RGB frozen", "optimizer": "Adam lr 1e-2 eps 1e-15"},
-           "vs_baseline": None}
+           "value": 1e3 / ms, "unit": "steps/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+           "rays_per_s": 4096 * 1e3 / ms, "final_loss": loss, **TRAIN_WHAT, "vs_baseline": None}
+    if args.torch_adam:
+        rec["optimizer"] = "torch.optim.Adam (foreach)"
     print(json.dumps(rec), flush=True)
 
 
@@ -586,6 +595,13 @@ def main():
             "max_abs_samvit_vs_headline": float((last3["samvit"] - last["samvit"]).abs().max())
             if with_sam else None,
             "max_abs_image_vs_headline": float((last3["image"] - last["image"]).abs().max())}
+
+    if not args.no_alt and world == 1 and args.rank_share <= 1 and with_sam:
+        # BASELINE config 5 beside the headline (`--mode train` runs it alone)
+        ms5, loss5 = train_steps(dev, 20, 5)
+        side["cfg5_train"] = {"ms_per_step": ms5, "steps_per_s": 1e3 / ms5,
+                              "rays_per_s": 4096 * 1e3 / ms5, "steps": 20, "warmup": 5,
+                              "final_loss": loss5, **TRAIN_WHAT}
 
     if rank == 0:
         rec = {

@@ -1203,22 +1203,52 @@ __global__ void __launch_bounds__(256) k_sgrid_box4(SgridArgs a) {
 
 // Backward of k_sgrid for the distillation step: grad_emb[row] += w_k *
 // corner_weight * g[ray, level*8 + c].  One thread per (ray, level, channel):
-// 8 adjacent lanes add to the 32 contiguous bytes of one corner row.
+// a wave is 8 neighbouring rays x 8 channels, so one atomic wave-instruction
+// adds 8 rows of 32 contiguous bytes.
+//
+// The global float atomics are the cost: they execute at the memory side at
+// roughly one wave-instruction per 50 ns per CU whatever the lanes hold
+// (MI355X_MICROARCH.md), and the round-1 form issued 8 per wave and sample (one
+// per corner, duplicates among the 8 rays merged by a butterfly).  Here the
+// wave first sums its 64 corner contributions per channel in LDS over the
+// exact box of corner cells the 8 rays touch (wave_box.h's idea, reversed),
+// then compacts the non-zero cells (ballot + prefix) and adds each distinct
+// cell row once: ceil(distinct rows / 8) atomics per wave and sample --
+// ~2.4x fewer over the 16 levels of a training view (distinct corner rows of
+// 8 rays: ~10 at the coarse levels, ~50 at level 15).  Boxes of more than 64
+// cells (scattered rays) take the per-corner form.  Measured on a cfg-5 step
+// the box form is SLOWER (0.70 vs 0.56 ms): the atomic instruction count is
+// not what binds the per-corner form; the box's six wave reductions, LDS
+// atomics and three wave syncs per sample cost more than the atomics they
+// save.  The per-corner form stays the default (max_cells = 0); the box form
+// is kept selectable (SAMNERF_SGRID_BWD=box) and tested against it.
+constexpr uint32_t kBwdBoxCells = 64;
+
 template <int T>
 __global__ void __launch_bounds__(256)
 k_sgrid_backward(uint32_t N, GridDesc<16> g, const float* __restrict__ u_in,
                  const float* __restrict__ w_in, const float* __restrict__ grad, uint32_t gstride,
-                 float* __restrict__ gemb) {
+                 float* __restrict__ gemb, uint32_t max_cells) {
+    __shared__ float box[4][kBwdBoxCells * 8];           // per wave: cell x channel sums
+    __shared__ uint32_t list[4][kBwdBoxCells];           // per wave: rows of the non-zero cells
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t r = (uint32_t)(t >> 3), ch = (uint32_t)(t & 7u), lane = threadIdx.x & 63u;
+    const uint32_t wv = threadIdx.x >> 6;
     const uint32_t level = blockIdx.y;
     if (((t & ~(uint64_t)63) >> 3) >= N) return;          // whole wave past the end
-    const bool live = r < N;                                // lanes stay for the shuffles
+    const bool live = r < N;                                // lanes stay for the reductions
     const uint32_t rr = live ? r : N - 1;
     const LevelDesc d = g.lv[level];
     const float gv = live ? grad[(size_t)rr * gstride + level * 8u + ch] : 0.0f;
     float* base = gemb + (size_t)d.off * 8u + ch;
-    for (int k = 0; k < T; ++k) {
+    float* slice = box[wv];
+    uint32_t* rows = list[wv];
+    const uint32_t top = d.res - 1u;
+    // blockIdx.z: this block's share of the samples (more waves in flight: the
+    // per-sample chain -- loads, box reductions, LDS sums, atomics -- is
+    // latency-bound at 8 rays per wave)
+    const int k0 = (int)(blockIdx.z * T / gridDim.z), k1 = (int)((blockIdx.z + 1) * T / gridDim.z);
+    for (int k = k0; k < k1; ++k) {
         const float ux = u_in[((size_t)k * 3 + 0) * N + rr];
         const float uy = u_in[((size_t)k * 3 + 1) * N + rr];
         const float uz = u_in[((size_t)k * 3 + 2) * N + rr];
@@ -1228,32 +1258,79 @@ k_sgrid_backward(uint32_t N, GridDesc<16> g, const float* __restrict__ u_in,
         locate_axis(ux, d, cx, fx);
         locate_axis(uy, d, cy, fy);
         locate_axis(uz, d, cz, fz);
-        const uint32_t top = d.res - 1u;
         const uint32_t nx = min(cx + 1u, top), ny = min(cy + 1u, top), nz = min(cz + 1u, top);
+        // the wave's box of corner cells (cells are never negative: int order)
+        const uint32_t x0 = (uint32_t)wave_imin((int)cx), x1 = (uint32_t)wave_imax((int)nx);
+        const uint32_t y0 = (uint32_t)wave_imin((int)cy), y1 = (uint32_t)wave_imax((int)ny);
+        const uint32_t z0 = (uint32_t)wave_imin((int)cz), z1 = (uint32_t)wave_imax((int)nz);
+        const uint32_t ex = x1 - x0 + 1u, ey = y1 - y0 + 1u, ez = z1 - z0 + 1u;
+        const uint32_t cells = ex * ey * ez;                 // wave-uniform
+        if (cells <= max_cells) {
+            // 1. zero the slice (lane = cell), 2. LDS-add the corners
+            reinterpret_cast<float4*>(slice + lane * 8u)[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            reinterpret_cast<float4*>(slice + lane * 8u)[1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            wave_lds_sync();
+            const uint32_t X[2] = {cx - x0, nx - x0};
+            const uint32_t Y[2] = {(cy - y0) * ex, (ny - y0) * ex};
+            const uint32_t Z[2] = {(cz - z0) * ex * ey, (nz - z0) * ex * ey};
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const float wx = (c & 1) ? fx : 1.0f - fx;
-            const float wy = (c & 2) ? fy : 1.0f - fy;
-            const float wz = (c & 4) ? fz : 1.0f - fz;
-            const uint32_t row = dense_or_hash_row((c & 1) ? nx : cx, (c & 2) ? ny : cy,
-                                                   (c & 4) ? nz : cz, d);
-            float val = ((wx * wy) * wz) * wg;
-            // The wave's 8 rays (neighbouring pixels) often hit the same corner
-            // row: merge equal rows over a 3-level butterfly so one lane per
-            // row and channel issues the atomic (the atomics run at the memory
-            // side, so fewer and fuller requests are what pays).
-            bool alive = live;
-#pragma unroll
-            for (int sd = 8; sd < 64; sd <<= 1) {
-                const uint32_t orow = __shfl_xor(row, sd);
-                const float oval = __shfl_xor(val, sd);
-                const int oalive = __shfl_xor((int)alive, sd);
-                if (alive && oalive && orow == row) {
-                    if (lane & sd) alive = false;
-                    else val += oval;
+            for (int c = 0; c < 8; ++c) {
+                const float wx = (c & 1) ? fx : 1.0f - fx;
+                const float wy = (c & 2) ? fy : 1.0f - fy;
+                const float wz = (c & 4) ? fz : 1.0f - fz;
+                const uint32_t cell = X[c & 1] + Y[(c >> 1) & 1] + Z[c >> 2];
+                atomicAdd(slice + cell * 8u + ch, ((wx * wy) * wz) * wg);
+            }
+            wave_lds_sync();
+            // 3. compact the non-zero cells (lane = cell): ballot + prefix
+            const float4 va = reinterpret_cast<const float4*>(slice + lane * 8u)[0];
+            const float4 vb = reinterpret_cast<const float4*>(slice + lane * 8u)[1];
+            const bool nzc = lane < cells && (va.x != 0.0f || va.y != 0.0f || va.z != 0.0f ||
+                                              va.w != 0.0f || vb.x != 0.0f || vb.y != 0.0f ||
+                                              vb.z != 0.0f || vb.w != 0.0f);
+            const uint64_t mask = __builtin_amdgcn_ballot_w64(nzc);
+            const uint32_t n = (uint32_t)__builtin_popcountll(mask);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+            if (nzc) {
+                const uint32_t bx = lane % ex, by = (lane / ex) % ey, bz = lane / (ex * ey);
+                rows[rank] = (dense_or_hash_row(x0 + bx, y0 + by, z0 + bz, d) << 6) | lane;
+            }
+            wave_lds_sync();
+            // 4. one global atomic per distinct cell row and channel, 8 cells
+            //    (x 8 channels) per wave-instruction
+            for (uint32_t j = 0; j < n; j += 8u) {
+                const uint32_t idx = j + (lane >> 3);
+                if (idx < n) {
+                    const uint32_t e = rows[idx];
+                    atomicAdd(base + (size_t)(e >> 6) * 8u, slice[(e & 63u) * 8u + ch]);
                 }
             }
-            if (alive) atomicAdd(base + (size_t)row * 8u, val);
+            wave_lds_sync();                                  // reads done before the next zeroing
+        } else {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float wx = (c & 1) ? fx : 1.0f - fx;
+                const float wy = (c & 2) ? fy : 1.0f - fy;
+                const float wz = (c & 4) ? fz : 1.0f - fz;
+                const uint32_t row = dense_or_hash_row((c & 1) ? nx : cx, (c & 2) ? ny : cy,
+                                                       (c & 4) ? nz : cz, d);
+                float val = ((wx * wy) * wz) * wg;
+                // merge equal rows of the wave's 8 rays over a 3-level butterfly
+                // so one lane per row and channel issues the atomic
+                bool alive = live;
+#pragma unroll
+                for (int sd = 8; sd < 64; sd <<= 1) {
+                    const uint32_t orow = __shfl_xor(row, sd);
+                    const float oval = __shfl_xor(val, sd);
+                    const int oalive = __shfl_xor((int)alive, sd);
+                    if (alive && oalive && orow == row) {
+                        if (lane & sd) alive = false;
+                        else val += oval;
+                    }
+                }
+                if (alive) atomicAdd(base + (size_t)row * 8u, val);
+            }
         }
     }
 }
@@ -1744,9 +1821,20 @@ int samnerf_sgrid_backward(const samnerf_model* m, const float* grad_fsam, uint3
     GridDesc<16> gs;
     int rc = make_grid_desc(m->s_grid, 8, 16, gs, "s_grid");
     if (rc) return rc;
-    k_sgrid_backward<32><<<dim3(div_up((uint64_t)N * 8, 256), 16), 256, 0,
+    for (int l = 0; l < 16; ++l)       // box cells carry row << 6 | cell in 32 bits
+        if (gs.lv[l].size > (1u << 26))
+            return fail(SAMNERF_EINVAL, "sgrid_backward: level %d has more than 2^26 rows", l);
+    // SAMNERF_SGRID_BWD=box: the LDS-box aggregation (A/B and tests; measured
+    // slower than the per-corner atomics, 0.70 vs 0.56 ms per cfg-5 step, so
+    // not the default); SAMNERF_SGRID_BWD_SPLIT: sample groups per ray
+    // (blockIdx.z; 1 = the round-1 form, 4-16 measured no faster)
+    const char* mode = getenv("SAMNERF_SGRID_BWD");
+    const uint32_t max_cells = (mode && !strcmp(mode, "box")) ? kBwdBoxCells : 0u;
+    const char* sp = getenv("SAMNERF_SGRID_BWD_SPLIT");
+    const uint32_t split = sp ? (uint32_t)std::max(1, std::min(32, atoi(sp))) : 1u;
+    k_sgrid_backward<32><<<dim3(div_up((uint64_t)N * 8, 256), 16, split), 256, 0,
                            reinterpret_cast<hipStream_t>(stream)>>>(N, gs, w.u_f, w.w_f, grad_fsam,
-                                                                     kRow, grad_embeddings);
+                                                                     kRow, grad_embeddings, max_cells);
     return check_launch("sgrid_backward");
 }
 
