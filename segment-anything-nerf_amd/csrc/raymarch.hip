@@ -707,8 +707,20 @@ __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const Leve
 // final; per-slot partial sums of w, w*t and w*features are added at the end.
 // S > 1 only serves small N (one rank's share of a view): S-times more waves,
 // while a wave still gathers at adjacent samples of neighbouring rays.
+// Occupancy: the S = 1 form without the cross-sample prefetch runs at 3 waves
+// per SIMD (168 VGPRs, 10 spilled): more waves hide the gather latency better
+// than the prefetch did at 2 (0.797 vs 0.826 ms per view); the S = 2 / 4 forms
+// spill 20+ registers at 3 waves and stay at 2 (0.139 vs 0.158 ms at 32K rays).
+#ifndef SAMNERF_DIAG_FINAL_WAVES
+#define SAMNERF_DIAG_FINAL_WAVES 3
+#endif
+template <int S_, bool PF_>
+constexpr int final_waves() { return (S_ == 1 && !PF_) ? SAMNERF_DIAG_FINAL_WAVES : 2; }
+
 template <int T, int S, bool PF, bool EXACT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_final(FinalArgs a) {
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(final_waves<S, PF>(), final_waves<S, PF>())))
+k_final(FinalArgs a) {
     static_assert(S == 1 || S == 2 || S == 4, "segments per ray");
     static_assert(kXSteps * 64 == 2 * kFSlots * 64 * 4, "exact weights reuse the bf16x3 slots");
     constexpr int R = 32 / S, TS = T / S;
@@ -1107,8 +1119,19 @@ __global__ void __launch_bounds__(256) k_sgrid(SgridArgs a) {
 // bits are identical.
 constexpr uint32_t kBoxSlots = 256;          // 32 B slots per wave (8 KiB)
 
+// 4 waves per SIMD (128 VGPRs, 7 spilled) instead of the 3 the compiler's
+// default 142 VGPRs allow: the VALU-bound box gathers hide their LDS and
+// staging latency better -- 0.835 -> 0.72 ms per view, 0.126 -> 0.112 ms at
+// one rank's 32K rays (round 2)
+#ifndef SAMNERF_DIAG_SGRID_WAVES
+#define SAMNERF_DIAG_SGRID_WAVES 4
+#endif
 template <int T>
-__global__ void __launch_bounds__(256) k_sgrid_box4(SgridArgs a) {
+__global__ void __launch_bounds__(256)
+#if SAMNERF_DIAG_SGRID_WAVES
+__attribute__((amdgpu_waves_per_eu(SAMNERF_DIAG_SGRID_WAVES, SAMNERF_DIAG_SGRID_WAVES)))
+#endif
+k_sgrid_box4(SgridArgs a) {
     constexpr int TQ = T / 4;
     __shared__ float4 smem[4][kBoxSlots * 2];          // per wave: the box slice
     const uint32_t lane = threadIdx.x & 63u, q = threadIdx.x >> 6;
@@ -1469,11 +1492,12 @@ void mark_stage(uint32_t i, hipStream_t s) {
 // Below 32,768 rays (not measured) the direct form stays.
 constexpr uint32_t kBox4MinRays = 32768;
 
-// k_final's cross-sample prefetch of one k-block's gathers: on for S = 1
-// (a full view: 1.01 -> 0.99 ms), off for S = 2 / 4 (one rank's share), whose
-// prefetching forms spill once the slot-class paths are in: at 32,768 rays
-// 0.260 ms without it vs 0.288 with it (0.303 for the earlier default, PF
-// without slot classes).  SAMNERF_FINAL_PF = 0 | 1 forces it off / on.
+// k_final's cross-sample prefetch of one k-block's gathers: off by default
+// since round 2 -- for S = 1 three waves per SIMD without it beat two with it
+// (0.797 vs 0.826 ms per view, see final_waves); for S = 2 / 4 (one rank's
+// share) the prefetching forms spill once the slot-class paths are in (at
+// 32,768 rays 0.260 ms without it vs 0.288 with it).  SAMNERF_FINAL_PF = 0 | 1
+// forces it off / on (the bit-identity tests run both).
 // k_final's wave-uniform slot paths (dense pair loads, select-free hashed
 // rows): on by default; SAMNERF_FINAL_CLASSES=0 takes the lane-varying form
 // everywhere (same bits: the A/B parity test).
@@ -1484,7 +1508,7 @@ uint32_t final_classes() {
 
 bool final_prefetch(int seg) {
     const char* v = getenv("SAMNERF_FINAL_PF");
-    return v ? atoi(v) != 0 : seg == 1;
+    return v ? atoi(v) != 0 : false;
 }
 
 // k_sgrid_box4 packs cell indices and extents into 10 bits
