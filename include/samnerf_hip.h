@@ -231,6 +231,26 @@ int samnerf_adam_step(const samnerf_adam_tensor* tensors_host, uint32_t n_tensor
                       double beta1, double beta2, double eps, double weight_decay, uint32_t step,
                       samnerf_stream_t stream);
 
+/* The SAM head of the distillation step with its backward (nerf/network.py:
+ * 36-75, :120-123 under nerf/utils.py:1098-1106), exact fp32 on MFMA.
+ * forward: rows [N,164] (the head input rows of samnerf_render_forward's
+ * feature_rows) -> samvit [N,256]; saves the activations in `workspace`
+ * (samnerf_head_train_workspace_size(N) bytes), which the backward of the
+ * same rows reads.  backward: grad_samvit [N,256] -> grad_rows [N,164]
+ * (columns 0..162 written; the caller zeroes it), and ACCUMULATES into
+ * grad_w[5] ([256,163], [256,256], [256,419], [256,256], [256,256]),
+ * grad_b[5] ([256] each), grad_ln_w, grad_ln_b ([256]).  The weights are the
+ * model's sam_w / sam_b / ln_w / ln_b. */
+size_t samnerf_head_train_workspace_size(uint32_t N);
+int samnerf_head_train_forward(const samnerf_model* model, const float* rows, uint32_t N,
+                               float* samvit, void* workspace, size_t workspace_bytes,
+                               samnerf_stream_t stream);
+int samnerf_head_train_backward(const samnerf_model* model, const float* rows,
+                                const float* grad_samvit, uint32_t N, float* grad_rows,
+                                float* const* grad_w, float* const* grad_b, float* grad_ln_w,
+                                float* grad_ln_b, void* workspace, size_t workspace_bytes,
+                                samnerf_stream_t stream);
+
 /* Transport record of the per-ray outputs for the all-gather of a
  * ray-sharded view (samnerf_amd/dist.py; no reference counterpart: the
  * reference renders on one GPU, nerf/renderer.py:185-219).  One record of

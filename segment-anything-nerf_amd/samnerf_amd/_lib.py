@@ -69,6 +69,11 @@ _SIGS = {
     "samnerf_set_stage_events": ([ctypes.POINTER(_vp), _u32], _int),
     "samnerf_set_taps": ([ctypes.c_void_p, _u32], _int),
     "samnerf_adam_step": ([ctypes.c_void_p, _u32, _f64, _f64, _f64, _f64, _f64, _u32, _vp], _int),
+    "samnerf_head_train_workspace_size": ([_u32], _sz),
+    "samnerf_head_train_forward": ([ctypes.POINTER(SamnerfModel), _vp, _u32, _vp, _vp, _sz, _vp], _int),
+    "samnerf_head_train_backward": ([ctypes.POINTER(SamnerfModel), _vp, _vp, _u32, _vp,
+                                     ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp, _vp, _sz,
+                                     _vp], _int),
 }
 
 

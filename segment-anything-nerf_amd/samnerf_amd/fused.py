@@ -229,12 +229,62 @@ class _FusedSamRows(torch.autograd.Function):
         return grad, None, None, None, None, None
 
 
-def render_sam_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None):
+def _head_params(net):
+    skip, ln = net.samvit_mlp[0], net.samvit_mlp[1]
+    return ([skip.net[i].weight for i in range(5)] + [skip.net[i].bias for i in range(5)]
+            + [ln.weight, ln.bias])
+
+
+class _SamHeadTrain(torch.autograd.Function):
+    """samvit_mlp (SkipConnMLP 163->256 x5 + LayerNorm, network.py:36-75,
+    :120-123) on the head-input rows, forward and backward as HIP kernels
+    (sam_head_train.hip, exact fp32 MFMA): gradients w.r.t. the rows and the
+    12 head tensors, the same values torch's autograd computes for
+    net.samvit_mlp(rows[:, :163]) up to summation order."""
+
+    @staticmethod
+    def forward(ctx, rows, renderer, *params):
+        rows = rows.contiguous()
+        N = rows.shape[0]
+        m = renderer.model()
+        need = lib().samnerf_head_train_workspace_size(N)
+        ws = torch.empty(max(need, 1), dtype=torch.uint8, device=rows.device)
+        samvit = torch.empty(N, 256, device=rows.device)
+        check(lib().samnerf_head_train_forward(ctypes.byref(m), _ptr(rows), N, _ptr(samvit), _ptr(ws),
+                                               need, _stream(rows)), "head_train_forward")
+        ctx.save_for_backward(rows)
+        ctx.ws, ctx.need, ctx.m, ctx.keep = ws, need, m, list(renderer._keep)
+        ctx.shapes = [p.shape for p in params]
+        return samvit
+
+    @staticmethod
+    def backward(ctx, g):
+        (rows,) = ctx.saved_tensors
+        g = g.contiguous().float()
+        dev = rows.device
+        grows = torch.zeros_like(rows)
+        grads = [torch.zeros(sh, device=dev) for sh in ctx.shapes]
+        gw = (ctypes.c_void_p * 5)(*[t.data_ptr() for t in grads[:5]])
+        gb = (ctypes.c_void_p * 5)(*[t.data_ptr() for t in grads[5:10]])
+        check(lib().samnerf_head_train_backward(
+            ctypes.byref(ctx.m), _ptr(rows), _ptr(g), rows.shape[0], _ptr(grows), gw, gb,
+            _ptr(grads[10]), _ptr(grads[11]), _ptr(ctx.ws), ctx.need, _stream(g)), "head_train_backward")
+        return (grows, None, *grads)
+
+
+def render_sam_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None, head=None):
     """Differentiable SAM-feature render for the distillation step
     (nerf/utils.py:1098-1099): returns samvit [N,256] with autograd to
-    s_grid.embeddings (HIP scatter) and samvit_mlp (torch)."""
+    s_grid.embeddings (HIP scatter) and samvit_mlp (HIP head forward +
+    backward, sam_head_train.hip; head="torch" or SAMNERF_TRAIN_HEAD=torch runs
+    the head as torch ops instead, for comparison)."""
+    import os
     net = renderer.net
     rows, image, depth, wsum = _FusedSamRows.apply(net.s_grid.embeddings, renderer, rays_o,
                                                     rays_d, cam_near_far, bg_color)
-    samvit = net.samvit_mlp(rows[:, :163])
+    head = head or os.environ.get("SAMNERF_TRAIN_HEAD", "hip")
+    if head == "torch":
+        samvit = net.samvit_mlp(rows[:, :163])
+    else:
+        samvit = _SamHeadTrain.apply(rows, renderer, *_head_params(net))
     return {"samvit": samvit, "image": image, "depth": depth, "weights_sum": wsum}

@@ -131,6 +131,41 @@ def test_sgrid_backward_box_matches_per_corner(hip_lib, cuda, monkeypatch):
     assert rel < 1e-5 and mx < 1e-5, (rel, mx)
 
 
+@pytest.mark.parametrize("n", [4096, 1000, 37])
+def test_head_train_kernels_match_torch_autograd(hip_lib, cuda, n):
+    """sam_head_train.hip (forward with saved activations, LayerNorm and
+    leaky_relu backward, dX chain, dW over all rays) against torch autograd of
+    net.samvit_mlp on the same rows, fp32: outputs and every gradient (the rows
+    and the 12 head tensors) to summation-order rounding; ragged ray counts
+    (partial workgroups, padded ray chunks)."""
+    from samnerf_amd.fused import FusedRenderer, _SamHeadTrain, _head_params
+    spec = synth.ModelSpec(with_sam=True, grid_log2=12, s_grid_log2=11, prop_log2=10)
+    net = make_net(spec, synth.make_params(spec, seed=15, emb_scale=0.5, ln_jitter=0.3), cuda)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    rows = (torch.randn(n, 164, generator=g) * torch.rand(1, 164, generator=g) * 3).to(cuda)
+    rows[:, 163] = 0.0
+    G = torch.randn(n, 256, generator=g).to(cuda)
+    params = _head_params(net)
+    r1 = rows.clone().requires_grad_(True)
+    out1 = _SamHeadTrain.apply(r1, FusedRenderer(net), *params)
+    (out1 * G).sum().backward()
+    g1 = [p.grad.clone() for p in params]
+    for p in params:
+        p.grad = None
+    r2 = rows.clone().requires_grad_(True)
+    out2 = net.samvit_mlp(r2[:, :163])
+    (out2 * G).sum().backward()
+    g2 = [p.grad.clone() for p in params]
+    assert (out1 - out2).abs().max().item() < 2e-5
+    gr1, gr2 = r1.grad[:, :163], r2.grad[:, :163]
+    assert ((gr1 - gr2).norm() / gr2.norm()).item() < 1e-5
+    assert r1.grad[:, 163].abs().max().item() == 0.0
+    names = [f"net.{i}.weight" for i in range(5)] + [f"net.{i}.bias" for i in range(5)] + ["ln.w", "ln.b"]
+    errs = {nm: ((a - b).norm() / b.norm().clamp_min(1e-12)).item() for nm, a, b in zip(names, g1, g2)}
+    print("head train grads", n, errs)
+    assert max(errs.values()) < 1e-5, errs
+
+
 def test_distillation_steps_reduce_loss(hip_lib, cuda):
     from samnerf_amd import ops
     from samnerf_amd.fused import FusedRenderer, render_sam_train
