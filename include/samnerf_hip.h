@@ -237,10 +237,11 @@ int samnerf_adam_step(const samnerf_adam_tensor* tensors_host, uint32_t n_tensor
  * feature_rows) -> samvit [N,256]; saves the activations in `workspace`
  * (samnerf_head_train_workspace_size(N) bytes), which the backward of the
  * same rows reads.  backward: grad_samvit [N,256] -> grad_rows [N,164]
- * (columns 0..162 written; the caller zeroes it), and ACCUMULATES into
- * grad_w[5] ([256,163], [256,256], [256,419], [256,256], [256,256]),
- * grad_b[5] ([256] each), grad_ln_w, grad_ln_b ([256]).  The weights are the
- * model's sam_w / sam_b / ln_w / ln_b. */
+ * (every column written, column 163 -- depth's padding -- as 0), and
+ * OVERWRITES grad_w[5] ([256,163], [256,256], [256,419], [256,256],
+ * [256,256]), grad_b[5] ([256] each), grad_ln_w, grad_ln_b ([256]); no
+ * buffer needs zeroing by the caller.  The weights are the model's sam_w /
+ * sam_b / ln_w / ln_b. */
 size_t samnerf_head_train_workspace_size(uint32_t N);
 int samnerf_head_train_forward(const samnerf_model* model, const float* rows, uint32_t N,
                                float* samvit, void* workspace, size_t workspace_bytes,

@@ -13,11 +13,16 @@
 //   k_ht_fwd   16 rays per workgroup, all 5 layers + LayerNorm, activations
 //              kept in LDS and saved for the backward;
 //   k_ht_bwd   LayerNorm backward, then dX = W^T G through the 5 layers with
-//              the leaky_relu derivative, bias / LN-parameter gradients;
-//              writes the gradient of the head input (its f_sam part feeds the
-//              s_grid scatter);
+//              the leaky_relu derivative; writes the gradient of the head
+//              input (its f_sam part feeds the s_grid scatter), per-workgroup
+//              LN-parameter partials, and zeroes the parameter gradients;
 //   k_ht_dw    dW_l = G_l^T X_l over all rays: one 32x32 output tile x 256
-//              rays per wave, float atomics into the weight gradients.
+//              rays per wave, float atomics into the weight gradients; the
+//              bias gradients (row sums of G_l) and the LN partials per
+//              256-ray chunk.  No address takes more than one atomic per
+//              chunk: the first version summed the bias gradients with one
+//              atomic per workgroup and address in k_ht_bwd (256 same-address
+//              atomics each at 4,096 rays), which made k_ht_bwd 436 us.
 // Every product is v_mfma_f32_16x16x4_f32 / v_mfma_f32_32x32x2_f32: exact fp32
 // (an fma chain in k order, cdna_hip_programming.md "FP32-input MFMA"), so
 // the gradients match torch's fp32 autograd to summation-order rounding.
@@ -92,6 +97,54 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ float leaky(float x) { return x >= 0.0f ? x : x * 0.01f; }
 
+// acc[m] += sum over KS k-steps s of A_m(s) B(s), 16x16x4 fp32 MFMA: the A
+// fragment of tile m at step s is Ap[m][s * 64] (L2-resident weight pack),
+// B(s) = bl[s * 64] (LDS).  The A loads of the next U steps are issued before
+// the MFMAs of the current U (register double buffer), so a wave waits for L2
+// once per chain instead of once per step: the first version, one load then
+// its MFMA, left k_ht_bwd at ~380 us of L2 latency for 4,096 rays.
+template <int MT, int U>
+__device__ __forceinline__ void chain_load(float (&buf)[U][MT], const float* const (&Ap)[MT], int g) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) buf[u][m] = Ap[m][(g * U + u) * 64];
+    // keep the whole group's loads ahead of the MFMAs that follow (the
+    // scheduler otherwise sinks them between the MFMAs and reuses registers,
+    // leaving ~2 steps of loads in flight)
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int MT, int U>
+__device__ __forceinline__ void chain_mfma(f32x4 (&acc)[MT], const float (&buf)[U][MT], const float* bl, int g) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const float b = bl[(g * U + u) * 64];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m] = mfma16(buf[u][m], b, acc[m]);
+    }
+}
+
+// Two register buffers in ping-pong, no copies between them (a rotating
+// cur = nxt copy made the compiler wait for the fresh loads right after
+// issuing them).  Past the last group the load repeats it (unused).
+template <int MT, int KS, int U>
+__device__ __forceinline__ void mfma_chain(f32x4 (&acc)[MT], const float* const (&Ap)[MT], const float* bl) {
+    static_assert(KS % U == 0, "k-steps must split into groups of U");
+    constexpr int G = KS / U;
+    float b0[U][MT], b1[U][MT];
+    chain_load<MT, U>(b0, Ap, 0);
+#pragma unroll 1
+    for (int g = 0; g < G; g += 2) {
+        chain_load<MT, U>(b1, Ap, min(g + 1, G - 1));
+        chain_mfma<MT, U>(acc, b0, bl, g);
+        if (g + 1 < G) {
+            chain_load<MT, U>(b0, Ap, min(g + 2, G - 1));
+            chain_mfma<MT, U>(acc, b1, bl, g + 1);
+        }
+    }
+}
+
 struct FwdArgs {
     HeadW hw;
     const float* rows;     // [N][164]
@@ -109,16 +162,14 @@ __device__ __forceinline__ void fwd_layer(const FwdArgs& a, const float* in, flo
                                           uint32_t ray0) {
     constexpr int S = kKp[L] / 4;
     const int j = lane & 15, k = lane >> 4;
-    const float* A = a.wf + fwd_base(L) + (size_t)(4 * w) * S * 64 + lane;
     f32x4 acc[4];
+    const float* Ap[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 4
-    for (int s = 0; s < S; ++s) {
-        const float b = in[(4 * s + k) * kRays + j];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = mfma16(A[((size_t)t * S + s) * 64], b, acc[t]);
+    for (int t = 0; t < 4; ++t) {
+        acc[t] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        Ap[t] = a.wf + fwd_base(L) + (size_t)(4 * w + t) * S * 64 + lane;
     }
+    mfma_chain<4, S, 4>(acc, Ap, in + k * kRays + j);
     const bool live = ray0 + (uint32_t)j < a.N;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -204,23 +255,22 @@ struct BwdArgs {
     const float* stats;     // [Np][2]
     uint32_t N, Np;
     float* G;               // [5][256][Np] d loss / d z_l (pre-activation), for k_ht_dw
-    float* grows;           // [N][164]: d loss / d head input (columns 0..162 written)
-    float* gb[5];           // bias gradients (accumulated)
-    float* gln_w;
-    float* gln_b;
+    float* grows;           // [N][164]: d loss / d head input (column 163 written 0)
+    float* lnpart;          // [blocks][512]: per-workgroup sums of g * yhat (LN weight), g (LN bias)
+    float* zero[12];        // parameter gradients, zeroed here and accumulated by k_ht_dw
+    uint32_t zero_n[12];
 };
 
-// sum over the 16 lanes of one lane group (lane bits 0..3)
-__device__ __forceinline__ float sum16(float v) {
-    v += __shfl_xor(v, 1);
-    v += __shfl_xor(v, 2);
-    v += __shfl_xor(v, 4);
-    v += __shfl_xor(v, 8);
-    return v;
+// zero the parameter gradients (k_ht_dw, stream-ordered after this kernel,
+// accumulates into them)
+__device__ __forceinline__ void zero_grads(const BwdArgs& a) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (int t = 0; t < 12; ++t)
+        for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < a.zero_n[t]; e += stride) a.zero[t][e] = 0.0f;
 }
 
 // dX[Kp x 16] = W_l^T G[256 x 16]: output tiles t = w, w + 4, .. of Kp/16.
-// MODE 0: the next G = dX * leaky'(h_{l-1}) into out (+ save, + bias grad)
+// MODE 0: the next G = dX * leaky'(h_{l-1}) into out (+ save for k_ht_dw)
 // MODE 1 (layer 2): rows < 256 as MODE 0, rows >= 256 raw into out (skip)
 // MODE 2 (layer 0): grows = dX + skip (out holds the skip rows at 256 + c)
 template <int L, int MODE>
@@ -232,18 +282,16 @@ __device__ __forceinline__ void bwd_layer(const BwdArgs& a, const float* in, flo
     const uint32_t ray = ray0 + (uint32_t)j;
     const bool live = ray < a.N;
     f32x4 acc[MT];
+    const float* Ap[MT];
 #pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-    const float* A = a.wb + fwd_base(L) + lane;
-#pragma unroll 2
-    for (int s = 0; s < 64; ++s) {
-        const float b = in[(4 * s + k) * kRays + j];
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-            const int t = w + 4 * m;
-            if (t < NT) acc[m] = mfma16(A[((size_t)t * 64 + s) * 64], b, acc[m]);
-        }
+    for (int m = 0; m < MT; ++m) {
+        acc[m] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        // tiles past NT (layers 0 and 2: 11 and 27 tiles over 4 waves) repeat
+        // the last tile and are dropped below: the chain stays branch-free
+        const int t = min(w + 4 * m, NT - 1);
+        Ap[m] = a.wb + fwd_base(L) + (size_t)t * 64 * 64 + lane;
     }
+    mfma_chain<MT, 64, 4>(acc, Ap, in + k * kRays + j);
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
         const int t = w + 4 * m;
@@ -254,6 +302,7 @@ __device__ __forceinline__ void bwd_layer(const BwdArgs& a, const float* in, flo
             const float dx = acc[m][r];
             if (MODE == 2) {
                 if (v < kIn && live) a.grows[(size_t)ray * kRowIn + v] = dx + out[(256 + v) * kRays + j];
+                if (v == kIn && live) a.grows[(size_t)ray * kRowIn + v] = 0.0f;
                 continue;
             }
             if (MODE == 1 && v >= 256) {                    // d / d x through the skip
@@ -265,8 +314,6 @@ __device__ __forceinline__ void bwd_layer(const BwdArgs& a, const float* in, flo
             const float gz = live ? (h > 0.0f ? dx : dx * 0.01f) : 0.0f;
             out[v * kRays + j] = gz;
             a.G[((size_t)(L - 1) * 256 + v) * a.Np + ray] = gz;
-            const float sb = sum16(gz);
-            if (j == 0) atomicAdd(a.gb[L - 1] + v, sb);
         }
     }
 }
@@ -277,6 +324,7 @@ __global__ void __launch_bounds__(256) k_ht_bwd(BwdArgs a) {
     __shared__ float red[2][4][kRays];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t ray0 = blockIdx.x * kRays;
+    zero_grads(a);
     // LayerNorm backward: thread u holds unit u of the 16 rays
     {
         const int u = tid;
@@ -294,8 +342,8 @@ __global__ void __launch_bounds__(256) k_ht_bwd(BwdArgs a) {
             dgw += g * yh[jj];
             dgb += g;
         }
-        atomicAdd(a.gln_w + u, dgw);
-        atomicAdd(a.gln_b + u, dgb);
+        a.lnpart[(size_t)blockIdx.x * 512 + u] = dgw;
+        a.lnpart[(size_t)blockIdx.x * 512 + 256 + u] = dgb;
         // per ray: sums over the 256 units of gyh and gyh * yh (wave, then 4 waves)
 #pragma unroll
         for (int jj = 0; jj < kRays; ++jj) {
@@ -311,7 +359,6 @@ __global__ void __launch_bounds__(256) k_ht_bwd(BwdArgs a) {
             }
         }
         __syncthreads();
-        float db = 0.0f;
 #pragma unroll
         for (int jj = 0; jj < kRays; ++jj) {
             const uint32_t ray = ray0 + jj;
@@ -321,9 +368,7 @@ __global__ void __launch_bounds__(256) k_ht_bwd(BwdArgs a) {
             const float gy = rstd * (gyh[jj] - m1 - yh[jj] * m2);
             P[u * kRays + jj] = gy;
             a.G[((size_t)4 * 256 + u) * a.Np + ray] = gy;
-            db += gy;
         }
-        atomicAdd(a.gb[4] + u, db);
     }
     __syncthreads();
     bwd_layer<4, 0>(a, P, Q, w, lane, ray0);      // -> G3
@@ -341,8 +386,13 @@ struct DwArgs {
     const float* G;         // [5][256][Np]
     const float* hsave;     // [5][256][Np]
     const float* rows;      // [N][164]
+    const float* lnpart;    // [blocks][512] from k_ht_bwd
     uint32_t N, Np, chunks; // chunks of 256 rays
+    uint32_t blocks;        // k_ht_bwd workgroups
     float* gw[5];           // weight gradients [256][K_l] (accumulated)
+    float* gb[5];           // bias gradients (accumulated)
+    float* gln_w;
+    float* gln_b;
 };
 
 constexpr int kDwTilesK[5] = {6, 8, 14, 8, 8};          // 32-wide column tiles of Kp_l
@@ -356,11 +406,22 @@ constexpr int kDwTiles = dw_items_before(5);              // 352 output tiles of
 // dW_l[u][k] += sum over a chunk of 256 rays of G_l[u][r] X_l[k][r]; one wave
 // per (output tile, chunk).  The sum runs over rays, so the rays of an
 // MFMA's k pair can be any two: lane half h of group m takes rays
-// c0 + 8m + 4h .. +3 over four MFMAs, one 16-B load per operand.
+// c0 + 8m + 4h .. +3 over four MFMAs, one 16-B load per operand.  The waves
+// of the first column tile (kt 0) also sum their G rows: the bias gradient.
+// After the tiles, 8 waves per chunk add the chunk's 16 LN partials.
 __global__ void __launch_bounds__(256) k_ht_dw(DwArgs a) {
     const uint32_t item = blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (item >= (uint32_t)kDwTiles * a.chunks) return;
     const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+    if (item >= (uint32_t)kDwTiles * a.chunks) {
+        const uint32_t e = item - (uint32_t)kDwTiles * a.chunks;
+        if (e >= 8u * a.chunks) return;
+        const uint32_t chunk = e >> 3, v = ((e & 7u) << 6) + (uint32_t)lane;       // v: 0..511
+        const uint32_t b0 = chunk * (256u / kRays), b1 = min(b0 + 256u / kRays, a.blocks);
+        float sum = 0.0f;
+        for (uint32_t b = b0; b < b1; ++b) sum += a.lnpart[(size_t)b * 512 + v];
+        atomicAdd(v < 256u ? a.gln_w + v : a.gln_b + (v - 256u), sum);
+        return;
+    }
     const uint32_t tile = item % kDwTiles, chunk = item / kDwTiles;
     int l = 0;
     while (l < 4 && (int)tile >= dw_items_before(l + 1)) ++l;
@@ -376,8 +437,10 @@ __global__ void __launch_bounds__(256) k_ht_dw(DwArgs a) {
     const float* Hb = (l == 0 || from_x) ? nullptr
                                          : a.hsave + ((size_t)(l - 1) * 256 + kk) * a.Np + c0 + 4 * h;
     f32x16 acc = {};
+    float bsum = 0.0f;
     for (int m = 0; m < 32; ++m) {
         const float4 ga = *reinterpret_cast<const float4*>(Ga + 8 * m);
+        if (kt == 0) bsum += (ga.x + ga.y) + (ga.z + ga.w);
         float xb[4];
         if (from_x) {
 #pragma unroll
@@ -393,6 +456,10 @@ __global__ void __launch_bounds__(256) k_ht_dw(DwArgs a) {
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.y, xb[1], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.z, xb[2], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.w, xb[3], acc, 0, 0, 0);
+    }
+    if (kt == 0) {
+        bsum += __shfl_xor(bsum, 32);
+        if (h == 0) atomicAdd(a.gb[l] + u, bsum);
     }
     // acc register q of lane (col i, half h) = dW[32ut + (q & 3) + 8 (q >> 2) + 4h][32kt + i]
     const int col = 32 * kt + i;
@@ -410,6 +477,7 @@ struct Layout {
     float* hsave;
     float* stats;
     float* G;
+    float* lnpart;
     uint32_t Np;
     size_t bytes;
 };
@@ -431,6 +499,7 @@ Layout carve(uint32_t N, void* base) {
     L.hsave = take((size_t)5 * 256 * L.Np);
     L.stats = take((size_t)2 * L.Np);
     L.G = take((size_t)5 * 256 * L.Np);
+    L.lnpart = take((size_t)512 * div_up(N, kRays));
     L.bytes = off;
     return L;
 }
@@ -506,10 +575,18 @@ int samnerf_head_train_backward(const samnerf_model* m, const float* rows, const
     b.Np = L.Np;
     b.G = L.G;
     b.grows = grad_rows;
-    for (int i = 0; i < 5; ++i) b.gb[i] = grad_b[i];
-    b.gln_w = grad_ln_w;
-    b.gln_b = grad_ln_b;
-    k_ht_bwd<<<div_up(N, kRays), 256, 0, s>>>(b);
+    b.lnpart = L.lnpart;
+    for (int i = 0; i < 5; ++i) {
+        b.zero[i] = grad_w[i];
+        b.zero_n[i] = 256u * (uint32_t)kKl[i];
+        b.zero[5 + i] = grad_b[i];
+        b.zero_n[5 + i] = 256u;
+    }
+    b.zero[10] = grad_ln_w;
+    b.zero[11] = grad_ln_b;
+    b.zero_n[10] = b.zero_n[11] = 256u;
+    const uint32_t blocks = div_up(N, kRays);
+    k_ht_bwd<<<blocks, 256, 0, s>>>(b);
     if ((rc = check_launch("head_train_backward"))) return rc;
     DwArgs d{};
     d.G = L.G;
@@ -518,8 +595,15 @@ int samnerf_head_train_backward(const samnerf_model* m, const float* rows, const
     d.N = N;
     d.Np = L.Np;
     d.chunks = L.Np / 256u;
-    for (int i = 0; i < 5; ++i) d.gw[i] = grad_w[i];
-    k_ht_dw<<<div_up((uint64_t)kDwTiles * d.chunks, 4), 256, 0, s>>>(d);
+    d.lnpart = L.lnpart;
+    d.blocks = blocks;
+    for (int i = 0; i < 5; ++i) {
+        d.gw[i] = grad_w[i];
+        d.gb[i] = grad_b[i];
+    }
+    d.gln_w = grad_ln_w;
+    d.gln_b = grad_ln_b;
+    k_ht_dw<<<div_up((uint64_t)(kDwTiles + 8) * d.chunks, 4), 256, 0, s>>>(d);
     return check_launch("head_train_backward (dW)");
 }
 

@@ -262,8 +262,8 @@ class _SamHeadTrain(torch.autograd.Function):
         (rows,) = ctx.saved_tensors
         g = g.contiguous().float()
         dev = rows.device
-        grows = torch.zeros_like(rows)
-        grads = [torch.zeros(sh, device=dev) for sh in ctx.shapes]
+        grows = torch.empty_like(rows)                     # all written by the kernels
+        grads = [torch.empty(sh, device=dev) for sh in ctx.shapes]
         gw = (ctypes.c_void_p * 5)(*[t.data_ptr() for t in grads[:5]])
         gb = (ctypes.c_void_p * 5)(*[t.data_ptr() for t in grads[5:10]])
         check(lib().samnerf_head_train_backward(

@@ -152,6 +152,15 @@ def test_head_train_kernels_match_torch_autograd(hip_lib, cuda, n):
     g1 = [p.grad.clone() for p in params]
     for p in params:
         p.grad = None
+    # the backward overwrites its (torch.empty) gradient buffers: a second
+    # pass, whose buffers come back from the allocator holding the first
+    # pass's values, gives the same gradients, not their double
+    r1b = rows.clone().requires_grad_(True)
+    (_SamHeadTrain.apply(r1b, FusedRenderer(net), *params) * G).sum().backward()
+    for p, a in zip(params, g1):
+        assert ((p.grad - a).norm() / a.norm().clamp_min(1e-12)).item() < 1e-5
+        p.grad = None
+    assert ((r1b.grad - r1.grad).norm() / r1.grad.norm()).item() < 1e-5
     r2 = rows.clone().requires_grad_(True)
     out2 = net.samvit_mlp(r2[:, :163])
     (out2 * G).sum().backward()
