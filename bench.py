@@ -183,14 +183,18 @@ def setup_dist(args):
     return rank, world, torch.device("cuda", 0)
 
 
-def build_net(with_sam, device, seed=0, emb_scale=1e-4):
+def build_net(with_sam, device, seed=0, emb_scale=1e-4, surface=False):
     """NeRFNetwork with synthesised weights: the bench's default-init scene
-    (embeddings U(+-1e-4) as grid.py:144-146) or, with emb_scale 0.5, the
-    parity-weight scene of the tests."""
+    (embeddings U(+-1e-4) as grid.py:144-146), with emb_scale 0.5 the
+    parity-weight scene of the tests, with surface=True the
+    opaque-sphere scene of the N1 line (synth.make_surface_params)."""
     from nerf.network import NeRFNetwork, default_opt
     from samnerf_amd import synth
     spec = synth.ModelSpec(with_sam=with_sam)
-    params = synth.make_params(spec, seed=seed, emb_scale=emb_scale, ln_jitter=0.0)
+    if surface:
+        params = synth.make_surface_params(spec, seed=seed)
+    else:
+        params = synth.make_params(spec, seed=seed, emb_scale=emb_scale, ln_jitter=0.0)
     net = NeRFNetwork(default_opt(with_sam=with_sam))
     net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
     return net.to(device).eval(), spec, params
@@ -300,7 +304,8 @@ def train_steps(dev, steps, warmup, torch_adam=False):
 
 TRAIN_WHAT = {
     "optimizer": "FusedAdam: one-pass HIP Adam (train_optim.hip), torch.optim.Adam semantics",
-    "dtype": "fp32 (fused forward: grid_mlp bf16x3 MFMA; SAM head forward + backward torch fp32)",
+    "dtype": "fp32 (fused render forward: grid_mlp bf16x3 MFMA; SAM head forward + backward on exact "
+             "fp32 MFMA, sam_head_train.hip; s_grid scatter fp32 atomics)",
     "data": "synthetic (default-init weights, N(0,1) target)",
     "config": {"workload": "cfg5: 64x64 rays, with_sam, RGB frozen", "optimizer": "Adam lr 1e-2 eps 1e-15"},
 }
@@ -314,6 +319,8 @@ def train_main(args, dev):
            "rays_per_s": 4096 * 1e3 / ms, "final_loss": loss, **TRAIN_WHAT, "vs_baseline": None}
     if args.torch_adam:
         rec["optimizer"] = "torch.optim.Adam (foreach)"
+    if os.environ.get("SAMNERF_TRAIN_HEAD", "hip") == "torch":
+        rec["dtype"] = "fp32 (fused render forward: grid_mlp bf16x3 MFMA; SAM head torch autograd)"
     print(json.dumps(rec), flush=True)
 
 
@@ -595,6 +602,31 @@ def main():
             "max_abs_samvit_vs_headline": float((last3["samvit"] - last["samvit"]).abs().max())
             if with_sam else None,
             "max_abs_image_vs_headline": float((last3["image"] - last["image"]).abs().max())}
+
+    if not args.no_alt and world == 1 and args.rank_share <= 1:
+        # N1, the flagged non-parity early exit (samnerf_model.t_thresh), on a
+        # scene whose rays saturate (random weights never do); timed against
+        # the default mode on the same scene and view
+        snet, _, _ = build_net(with_sam, dev, seed=3, surface=True)
+        k = max(3, args.steps // 2)
+        n1 = {}
+        for t in (0.0, 1e-4):
+            rn = ViewRunner(args, FusedRenderer(snet, head_mode=args.head_mode, t_thresh=t), 1, dev,
+                            H, W, pose, intr, r0, r1, codec)
+            dtn, lastn, stn, _ = rn.run(k, 2)
+            n1[t] = (dtn, lastn, stn)
+        base, fast = n1[0.0], n1[1e-4]
+        side["n1_early_exit"] = {
+            "value": n_total * k / fast[0], "unit": "rays/s", "ms_per_step": fast[0] * 1e3 / k,
+            "default_mode_ms_per_step": base[0] * 1e3 / k, "speedup": base[0] / fast[0],
+            "t_thresh": 1e-4, "stage_ms": fast[2], "default_mode_stage_ms": base[2],
+            "max_weights_sum_drop": float((base[1]["weights_sum"] - fast[1]["weights_sum"]).max()),
+            "max_abs_image_vs_default": float((base[1]["image"] - fast[1]["image"]).abs().max()),
+            **({"max_abs_samvit_vs_default": float((base[1]["samvit"] - fast[1]["samvit"]).abs().max())}
+               if with_sam else {}),
+            "what": "FLAGGED NON-PARITY mode (SURVEY H6), never the default: a wave of 32 rays stops the "
+                    "final stage once every ray's transmittance < t_thresh; opaque-sphere scene "
+                    "(synth.make_surface_params), same view"}
 
     if not args.no_alt and world == 1 and args.rank_share <= 1 and with_sam:
         # BASELINE config 5 beside the headline (`--mode train` runs it alone)

@@ -174,6 +174,12 @@ typedef struct {
                                      SAM head: 0 = bf16x3 split precision on bf16 MFMA with
                                      fp32 accumulate (~1e-5 relative, default); 1 = exact
                                      fp32 MFMA (v_mfma_f32_32x32x2_f32) for both */
+    float t_thresh;               /* N1, a flagged NON-PARITY mode: 0 = off (the
+                                     reference's semantics, default); t in (0, 1): a wave of 32
+                                     rays stops marching the final stage once every ray's
+                                     transmittance is below t -- the dropped samples' weights
+                                     (their sum <= t per ray) become 0, so weights_sum, depth,
+                                     colour and features change by at most t x their range */
 } samnerf_model;
 
 /* Bytes of device workspace samnerf_render_forward needs for N rays. */

@@ -423,6 +423,10 @@ struct FinalArgs {
     float* depth;      // [N]
     float* wsum;       // [N]
     float* rows;       // [N, kRow] or null
+    // N1 (flagged, non-parity; samnerf_model.t_thresh): optical depth
+    // -ln(t_thresh) past which a ray is opaque; a wave whose rays all are
+    // stops marching.  INFINITY: off (the default, the reference's semantics).
+    float exit_depth;
 };
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -714,12 +718,16 @@ __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const Leve
 #ifndef SAMNERF_DIAG_FINAL_WAVES
 #define SAMNERF_DIAG_FINAL_WAVES 3
 #endif
-template <int S_, bool PF_>
-constexpr int final_waves() { return (S_ == 1 && !PF_) ? SAMNERF_DIAG_FINAL_WAVES : 2; }
+template <int S_, bool PF_, bool EXIT_ = false>
+constexpr int final_waves() { return (S_ == 1 && !PF_ && !EXIT_) ? SAMNERF_DIAG_FINAL_WAVES : 2; }
 
-template <int T, int S, bool PF, bool EXACT>
+// EXIT: the N1 early-exit form, its own instantiation at 2 waves per SIMD:
+// the exit in the sample loop raised the 3-wave form's spills from 10 to 22
+// VGPRs (and cost the default kernel 0.80 -> 0.92 ms per view while it was a
+// run-time check in the one instantiation)
+template <int T, int S, bool PF, bool EXACT, bool EXIT = false>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(final_waves<S, PF>(), final_waves<S, PF>())))
+__attribute__((amdgpu_waves_per_eu(final_waves<S, PF, EXIT>(), final_waves<S, PF, EXIT>())))
 k_final(FinalArgs a) {
     static_assert(S == 1 || S == 2 || S == 4, "segments per ray");
     static_assert(kXSteps * 64 == 2 * kFSlots * 64 * 4, "exact weights reuse the bf16x3 slots");
@@ -825,6 +833,7 @@ k_final(FinalArgs a) {
         gather_issue_c2<4>(emb, dl, p_ux, p_uy, p_uz, pre, pf_kinds(kPre));
     }
 
+    int exit_at = TS;                                     // EXIT: first dropped step
     for (int i = 0; i < TS; ++i) {
         const int k = i * S + seg;
         float rb_next, ux, uy, uz;
@@ -957,6 +966,29 @@ k_final(FinalArgs a) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) fg[q] = fg[q] + w * o3[q];
         rb_prev = rb_next;
+        // N1 early exit: once the transmittance of every ray of the wave is
+        // below t_thresh, the samples left (whose weights sum to that
+        // transmittance, the last one absorbing the rest) are dropped: their
+        // weights are stored as 0 (k_sgrid skips all-zero samples) and their
+        // positions as the grid centre (in range for any gather).  Nothing of
+        // the sample is held past its MFMAs for this (holding the position
+        // spilled 16 more VGPRs at 3 waves per SIMD).
+        if (EXIT && i + 1 < TS) {
+            const bool open = live && !(cum > (double)a.exit_depth);
+            if (__builtin_amdgcn_ballot_w64(open) == 0) {
+                exit_at = i + 1;
+                break;
+            }
+        }
+    }
+    if (EXIT && sample_writer) {
+        for (int i2 = exit_at; i2 < TS; ++i2) {
+            const int k2 = i2 * S + seg;
+            a.w_out[(size_t)k2 * N + r] = 0.0f;
+            a.u_out[((size_t)k2 * 3 + 0) * N + r] = 0.5f;
+            a.u_out[((size_t)k2 * 3 + 1) * N + r] = 0.5f;
+            a.u_out[((size_t)k2 * 3 + 2) * N + r] = 0.5f;
+        }
     }
 
     if constexpr (S > 1) {                               // add the slots' partial sums
@@ -1075,7 +1107,10 @@ __global__ void __launch_bounds__(256) k_sgrid(SgridArgs a) {
         const float nz = a.u_in[((size_t)kn * 3 + 2) * N + rr];
         const float nw = a.w_in[(size_t)kn * N + rr];
         float f[8];
-        if constexpr (MODE == kLookRef) {
+        // a sample with weight 0 on every ray of the wave adds nothing (N1's
+        // dropped samples; acc + 0 * f == acc for the finite features)
+        if (__builtin_amdgcn_ballot_w64(w != 0.0f) == 0) {
+        } else if constexpr (MODE == kLookRef) {
             lookup_level3_ref<8>(a.grid.emb, lv, ux, uy, uz, f);
 #pragma unroll
             for (int c = 0; c < 8; ++c) acc[c] = acc[c] + w * f[c];
@@ -1166,31 +1201,34 @@ k_sgrid_box4(SgridArgs a) {
         const float ny = a.u_in[((size_t)kn * 3 + 1) * N + rr];
         const float nz = a.u_in[((size_t)kn * 3 + 2) * N + rr];
         const float nw = a.w_in[(size_t)kn * N + rr];
-        const URange ur = wave_urange(ux, uy, uz);
-        const bool ordered = wave_positions_ordered(ux, uy, uz);
-        uint32_t p0, p1, p2;
-        pbox_lane(mine, ur, p0, p1, p2);
-        const f2v wv = {w, w};
+        // samples with weight 0 on all 64 rays (N1's dropped samples) add nothing
+        if (__builtin_amdgcn_ballot_w64(w != 0.0f) != 0) {
+            const URange ur = wave_urange(ux, uy, uz);
+            const bool ordered = wave_positions_ordered(ux, uy, uz);
+            uint32_t p0, p1, p2;
+            pbox_lane(mine, ur, p0, p1, p2);
+            const f2v wv = {w, w};
 #pragma unroll
-        for (int l = 0; l < 4; ++l) {
-            const PBox b = pbox_read(p0, p1, p2, l);
-            float f[8];
-            if (b.slots <= kBoxSlots) {
-                wave_lds_sync();                        // previous level's reads done
-                stage_pbox<8>(base, L[l], b, slice, lane);
-                wave_lds_sync();
-                if (ordered)
-                    lookup_level3_pbox<8, false>(a.grid.emb, L[l], b, slice, ux, uy, uz, f);
-                else
-                    lookup_level3_pbox<8, true>(a.grid.emb, L[l], b, slice, ux, uy, uz, f);
-            } else {
-                lookup_level3<8>(a.grid.emb, L[l], ux, uy, uz, f);
-            }
+            for (int l = 0; l < 4; ++l) {
+                const PBox b = pbox_read(p0, p1, p2, l);
+                float f[8];
+                if (b.slots <= kBoxSlots) {
+                    wave_lds_sync();                        // previous level's reads done
+                    stage_pbox<8>(base, L[l], b, slice, lane);
+                    wave_lds_sync();
+                    if (ordered)
+                        lookup_level3_pbox<8, false>(a.grid.emb, L[l], b, slice, ux, uy, uz, f);
+                    else
+                        lookup_level3_pbox<8, true>(a.grid.emb, L[l], b, slice, ux, uy, uz, f);
+                } else {
+                    lookup_level3<8>(a.grid.emb, L[l], ux, uy, uz, f);
+                }
 #pragma unroll
-            for (int c = 0; c < 8; c += 2) {
-                const f2v s2 = f2v{acc[l][c], acc[l][c + 1]} + wv * f2v{f[c], f[c + 1]};
-                acc[l][c] = s2.x;
-                acc[l][c + 1] = s2.y;
+                for (int c = 0; c < 8; c += 2) {
+                    const f2v s2 = f2v{acc[l][c], acc[l][c + 1]} + wv * f2v{f[c], f[c + 1]};
+                    acc[l][c] = s2.x;
+                    acc[l][c + 1] = s2.y;
+                }
             }
         }
         ux = nx;
@@ -1275,7 +1313,9 @@ k_sgrid_backward(uint32_t N, GridDesc<16> g, const float* __restrict__ u_in,
         const float ux = u_in[((size_t)k * 3 + 0) * N + rr];
         const float uy = u_in[((size_t)k * 3 + 1) * N + rr];
         const float uz = u_in[((size_t)k * 3 + 2) * N + rr];
-        const float wg = w_in[(size_t)k * N + rr] * gv;
+        const float wk = w_in[(size_t)k * N + rr];
+        if (__builtin_amdgcn_ballot_w64(wk != 0.0f) == 0) continue;   // N1's dropped samples
+        const float wg = wk * gv;
         uint32_t cx, cy, cz;
         float fx, fy, fz;
         locate_axis(ux, d, cx, fx);
@@ -1536,6 +1576,12 @@ void launch_prop_sigma(int look, uint32_t N, hipStream_t s, const PropArgs& pa) 
 // grid_mlp of head_mode 1
 template <bool EXACT>
 void launch_final(int seg, bool pf, uint32_t N, hipStream_t s, const FinalArgs& fa) {
+    if (fa.exit_depth < INFINITY) {                      // N1 (no prefetch form)
+        if (seg == 1) k_final<32, 1, false, EXACT, true><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
+        else if (seg == 2) k_final<32, 2, false, EXACT, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
+        else k_final<32, 4, false, EXACT, true><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
+        return;
+    }
     if (seg == 1) {
         if (pf) k_final<32, 1, true, EXACT><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
         else k_final<32, 1, false, EXACT><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
@@ -1781,6 +1827,9 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.image = image;
     fa.depth = depth;
     fa.wsum = weights_sum;
+    if (!(m->t_thresh >= 0.0f && m->t_thresh < 1.0f))
+        return fail(SAMNERF_EINVAL, "render_forward: t_thresh %g outside [0, 1)", (double)m->t_thresh);
+    fa.exit_depth = m->t_thresh > 0.0f ? -logf(m->t_thresh) : INFINITY;
     const bool sam_rows = m->with_sam && (samvit || feature_rows);
     fa.rows = sam_rows || feature_rows ? rows : nullptr;
     mark_stage(2, s);

@@ -25,9 +25,13 @@ def _param(t, name):
 
 
 class FusedRenderer:
-    """head_mode: 0 = bf16x3 split-precision SAM head (default), 1 = exact fp32."""
+    """head_mode: 0 = bf16x3 split precision for grid_mlp and the SAM head
+    (default), 1 = exact fp32.  t_thresh: 0 (default) = the reference's
+    semantics; > 0 = the flagged non-parity early-exit mode N1 (a wave stops
+    marching once every ray's transmittance is below t_thresh; include/
+    samnerf_hip.h), also from SAMNERF_T_THRESH."""
 
-    def __init__(self, net, head_mode=None):
+    def __init__(self, net, head_mode=None, t_thresh=None):
         import os
         self.net = net
         self._ws = None
@@ -35,6 +39,9 @@ class FusedRenderer:
         self._model = None
         self._model_key_cached = None
         self.head_mode = int(os.environ.get("SAMNERF_HEAD_MODE", "0")) if head_mode is None else head_mode
+        self.t_thresh = float(os.environ.get("SAMNERF_T_THRESH", "0")) if t_thresh is None else float(t_thresh)
+        if not 0.0 <= self.t_thresh < 1.0:
+            raise ValueError(f"t_thresh {self.t_thresh} outside [0, 1)")
 
     # --------------------------------------------------------------- model --
     def _grid(self, enc, name):
@@ -55,7 +62,7 @@ class FusedRenderer:
         the by-value fields (aabb, bounds, steps)."""
         n = self.net
         aabb = n.aabb_train if n.training else n.aabb_infer
-        return (n.training, self.head_mode, aabb.data_ptr(), aabb._version,
+        return (n.training, self.head_mode, self.t_thresh, aabb.data_ptr(), aabb._version,
                 tuple(p.data_ptr() for p in n.parameters()), tuple(n.opt.num_steps),
                 float(n.opt.min_near), float(n.bound), bool(n.opt.with_sam))
 
@@ -101,6 +108,7 @@ class FusedRenderer:
         for i, v in enumerate(opt.num_steps):
             m.num_steps[i] = int(v)
         m.head_mode = int(self.head_mode)
+        m.t_thresh = float(self.t_thresh)
         return m
 
     def workspace(self, m, N, device):

@@ -216,3 +216,68 @@ def random_rotation(seed):
     if np.linalg.det(q) < 0:
         q[:, 0] = -q[:, 0]
     return q.astype(np.float32)
+
+
+def _level_resolutions(g: GridSpec):
+    """Indexing resolution per level (float32 formula of gridencoder.cu:133)."""
+    S32 = np.float32(g.S)
+    return [int(np.ceil(np.float32(np.exp2(np.float32(l) * S32)) * np.float32(g.base_resolution)))
+            for l in range(g.num_levels)]
+
+
+def _sphere_channel(g: GridSpec, table, bound, radius, amp):
+    """Channel 0 of the dense levels of `table` = +amp at the vertices inside a
+    sphere of `radius` (contracted units, at the origin), -amp outside; hashed
+    levels' channel 0 = 0.  Returns the dense level indices."""
+    offs = g.offsets()
+    dense = []
+    for l, res in enumerate(_level_resolutions(g)):
+        n = int(offs[l + 1] - offs[l])
+        if res ** 3 > n:                                  # hashed level (gridencoder.cu:61-79)
+            table[offs[l]:offs[l + 1], 0] = 0.0
+            continue
+        dense.append(l)
+        i = np.arange(res, dtype=np.float64)
+        x = ((i + 0.5) / res) * 2 * bound - bound          # vertex i sits at u = (i + 0.5) / res
+        X, Y, Z = np.meshgrid(x, x, x, indexing="ij")      # row = ix + iy res + iz res^2
+        inside = (X * X + Y * Y + Z * Z) < radius * radius
+        ch = np.where(inside, amp, -amp).astype(np.float32).transpose(2, 1, 0).reshape(-1)
+        table[offs[l]:offs[l] + res ** 3, 0] = ch
+    return dense
+
+
+def make_surface_params(spec: ModelSpec, seed=0, radius=0.3, amp=1.5, emb_scale=0.5, ln_jitter=0.1):
+    """make_params plus an opaque sphere: a scene whose rays saturate (the
+    trained-scene regime random weights never reach: there the transmittance
+    stays above 1e-2 until the last sample).  The density grid's and the
+    proposal grids' dense levels carry +-amp in channel 0 (inside / outside
+    the sphere), and the first rows of grid_mlp / prop_mlp route that channel
+    to the density output (two ReLU units for the positive and negative parts,
+    so the raw density is +amp * levels inside and -amp * levels outside).
+    Used by the flagged early-exit mode's tests and bench line (N1)."""
+    P = make_params(spec, seed=seed, emb_scale=emb_scale, ln_jitter=ln_jitter)
+    b = spec.grid_bound
+
+    def route(w0, w1, w2, dense, C):
+        cols = [l * C for l in dense]
+        w0[0, :] = 0.0
+        w0[1, :] = 0.0
+        w0[0, cols] = 1.0
+        w0[1, cols] = -1.0
+        if w2 is None:                                     # prop_mlp: 2 layers, 1 output
+            w1[0, :] = 0.0
+            w1[0, 0], w1[0, 1] = 1.0, -1.0
+            return
+        w1[0:2, :] = 0.0
+        w1[0, 0] = 1.0
+        w1[1, 1] = 1.0
+        w2[0, :] = 0.0
+        w2[0, 0], w2[0, 1] = 1.0, -1.0
+
+    d = _sphere_channel(spec.grid, P["grid.embeddings"], b, radius, amp)
+    route(P["grid_mlp.net.0.weight"], P["grid_mlp.net.1.weight"], P["grid_mlp.net.2.weight"], d,
+          spec.grid.level_dim)
+    for i, g in enumerate(spec.prop):
+        d = _sphere_channel(g, P[f"prop_encoders.{i}.embeddings"], b, radius, amp)
+        route(P[f"prop_mlp.{i}.net.0.weight"], P[f"prop_mlp.{i}.net.1.weight"], None, d, g.level_dim)
+    return P

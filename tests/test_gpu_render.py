@@ -396,3 +396,37 @@ def test_final_slot_classes_bit_identical(hip_lib, cuda, monkeypatch, n):
             outs.append(o)
         for k in outs[0]:
             assert torch.equal(outs[0][k], outs[1][k]), (pf, k)
+
+
+def test_fused_render_from_reference_layout_checkpoint(hip_lib, cuda, tmp_path):
+    """SURVEY 8f-1 on the device: a model-only checkpoint in the reference's
+    layout (utils.py:2046-2074; save_checkpoint writes {epoch, global_step,
+    stats, model}) of the golden scene's weights, loaded (weights_only=True)
+    into a CUDA network that has already rendered with other weights, renders
+    the reference's golden view through the fused kernels; the EMA shadow
+    (utils.py:1684-1686) is honoured the same way."""
+    from samnerf_amd import checkpoint as ck
+    fx = np.load(os.path.join(GOLDEN, "render_small_sam.npz"))
+    spec = spec_from_fixture(fx)
+    params = synth.make_params(spec, seed=int(fx["seed"]), emb_scale=float(fx["emb_scale"]),
+                               ln_jitter=float(fx["ln_jitter"]))
+    src = make_net(spec, params, "cpu")
+    path = tmp_path / "ngp_ep0003.pth"
+    ck.save_checkpoint(src, path, epoch=3, global_step=300)
+    other = synth.make_params(spec, seed=int(fx["seed"]) + 1, emb_scale=0.5, ln_jitter=0.2)
+    net = make_net(spec, other, cuda)
+    ro = torch.from_numpy(fx["rays_o"]).to(cuda)
+    rd = torch.from_numpy(fx["rays_d"]).to(cuda)
+    H, W = int(fx["H"]), int(fx["W"])
+    ref = {k: torch.from_numpy(fx[k]) for k in ("image", "depth", "weights_sum", "samvit")}
+    before = net.render(ro, rd, staged=False, return_feats=1, H=H, W=W)
+    assert max_abs(before["samvit"].reshape(-1, 256), ref["samvit"].reshape(-1, 256)) > 1e-2
+    info = ck.load_checkpoint(net, ck.latest_checkpoint(tmp_path), map_location=cuda)
+    assert info["epoch"] == 3 and info["missing"] == [] and info["unexpected"] == []
+    out = net.render(ro, rd, staged=False, return_feats=1, H=H, W=W)
+    _check_outputs(out, ref)
+    # the EMA shadow replaces the weights it covers
+    ck.save_checkpoint(make_net(spec, other, "cpu"), tmp_path / "ngp_ep0004.pth", epoch=4,
+                       ema_shadow=[p.detach().clone() for p in src.parameters()])
+    ck.load_checkpoint(net, str(tmp_path / "ngp_ep0004.pth"), use_ema=True, map_location=cuda)
+    _check_outputs(net.render(ro, rd, staged=False, return_feats=1, H=H, W=W), ref)
