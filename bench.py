@@ -136,6 +136,12 @@ def parse():
                          "headline and reported beside it (unless --no-alt)")
     ap.add_argument("--torch-adam", action="store_true",
                     help="--mode train: torch.optim.Adam (foreach) instead of the one-pass HIP Adam")
+    ap.add_argument("--scene", choices=["default", "surface"], default="default",
+                    help="weights of the timed view: default-init (the headline, embeddings U(+-1e-4) as "
+                         "the reference initialises them) or the opaque-sphere scene "
+                         "(synth.make_surface_params: rays saturate at a surface, as in a trained scene)")
+    ap.add_argument("--no-tiles", dest="tiles", action="store_false",
+                    help="row-major ray waves instead of 8x4 pixel tiles (samnerf_model.view_width = 0)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -282,7 +288,7 @@ def train_steps(dev, steps, warmup, torch_adam=False):
     gt = torch.randn(1, 256, 64, 64, generator=g).to(dev)
 
     def step():
-        out = render_sam_train(renderer, ro, rd)
+        out = render_sam_train(renderer, ro, rd, view_width=w)
         pred = out["samvit"].reshape(1, h, w, 256).permute(0, 3, 1, 2).contiguous()
         pred = F.interpolate(pred, gt.shape[2:], mode="bilinear")
         loss = F.mse_loss(pred, gt)
@@ -342,9 +348,9 @@ def gui_main(args, dev):
 
     def frame():
         ro, rd = ops.get_rays(pose, intr, H, W, device=dev)
-        img = r.render(ro, rd, feats=False)
+        img = r.render(ro, rd, feats=False, view_width=W)
         ro2, rd2 = ops.get_rays(pose_lr, intr_lr, 64, 64, device=dev)
-        return img, r.render(ro2, rd2)
+        return img, r.render(ro2, rd2, view_width=64)
 
     for _ in range(args.warmup):
         frame()
@@ -398,7 +404,7 @@ class ViewRunner:
         def render_fn(ro, rd):
             raw = next(it, None)
             lib().samnerf_set_stage_events(raw, 6 if raw is not None else 0)
-            return self.renderer.render(ro, rd)
+            return self.renderer.render(ro, rd, view_width=W if self.args.tiles else 0)
 
         if self.world > 1 and self.args.chunks > 0:
             return render_view_sharded(render_fn, ray_fn, H, W, chunks=self.chunks)
@@ -556,7 +562,8 @@ def main():
     from samnerf_amd import synth
 
     with_sam = not args.no_sam
-    net, spec, params = build_net(with_sam, dev)
+    net, spec, params = build_net(with_sam, dev, seed=3 if args.scene == "surface" else 0,
+                                  surface=args.scene == "surface")
     renderer = FusedRenderer(net, head_mode=args.head_mode)
     H, W = args.H, args.W
     pose, intr = synth.gui_camera(W, H)
@@ -642,7 +649,9 @@ def main():
             "streams": len(runner.streams),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": DTYPE[args.head_mode],
-            "data": "synthetic (random-init weights of the reference architecture, GUI camera)",
+            "data": ("synthetic (random-init weights of the reference architecture, GUI camera)"
+                     if args.scene == "default" else
+                     "synthetic opaque-sphere scene (synth.make_surface_params), GUI camera"),
             "config": {"workload": ("cfg3: 512x512 view, RGB + 256-d SAM feature per ray" if with_sam
                                     else "cfg2: 512x512 view, RGB only") if (H, W) == (512, 512)
                        else f"{H}x{W} view", **({"rank_share": f"rows {r0}-{r1} of {args.rank_share} bands"}

@@ -180,6 +180,12 @@ typedef struct {
                                      transmittance is below t -- the dropped samples' weights
                                      (their sum <= t per ray) become 0, so weights_sum, depth,
                                      colour and features change by at most t x their range */
+    uint32_t view_width;          /* layout hint of the ray batch, not a weight: the rays are a
+                                     row-major image this many pixels wide (0 = unknown).  When W
+                                     is a multiple of 8 and N of 4 W, the kernels group rays into
+                                     8 x 4 pixel tiles (compact wave footprints, better gather
+                                     locality); outputs stay in ray order and are bit-identical.
+                                     samnerf_sgrid_backward must see the value of the forward. */
 } samnerf_model;
 
 /* Bytes of device workspace samnerf_render_forward needs for N rays. */

@@ -106,6 +106,39 @@ GridScale make_grid_scale(float bound) {
     return g;
 }
 
+// Ray tiling (samnerf_model.view_width).  The kernels work on ray SLOTS: a
+// wave of the proposal / s_grid kernels is 64 consecutive slots, a k_final
+// wave 32.  With the view's width W known, slot s is the ray of pixel
+// (x, y) of an 8 x 4 tile -- tile s / 32 in row-major tile order, pixel s % 32
+// row-major inside it -- so a wave's samples cover a compact patch of the
+// scene instead of a 32- or 64-pixel row segment: at fine levels the corner
+// boxes shrink and more gathers hit rows a neighbour already brought into L1
+// (tools/diag/tile_probe.py: 3.14 -> 2.97 ms per default-init view, final
+// 1.41 -> 1.20 ms on the opaque-sphere scene).  Per-sample intermediates
+// (near/far, bins, ds, u_f, w_f) live in slot order; the rays are read and the
+// per-ray outputs (image, depth, weights_sum, head rows) written at ray_of(s),
+// so callers see ray order.  w == 0: identity (W not a multiple of 8, or N not
+// a multiple of 4 W rows).
+struct RayTiles {
+    uint32_t w;      // view width in pixels (0: identity)
+    uint32_t tpr;    // tiles per tile row = w / 8
+    __device__ __forceinline__ uint32_t operator()(uint32_t s) const {
+        if (w == 0u) return s;
+        const uint32_t tile = s >> 5, in = s & 31u;
+        const uint32_t trow = tile / tpr, tcol = tile - trow * tpr;
+        return (trow * 4u + (in >> 3)) * w + tcol * 8u + (in & 7u);
+    }
+};
+
+RayTiles make_ray_tiles(uint32_t N, uint32_t W) {
+    RayTiles t{0u, 0u};
+    if (W >= 8u && W % 8u == 0u && N % (4u * W) == 0u) {
+        t.w = W;
+        t.tpr = W / 8u;
+    }
+    return t;
+}
+
 // MLP layer y = W x (torch layout W[out][in]), fma chain in input order.
 template <int OUT, int IN, bool RELU>
 __device__ __forceinline__ void dense(const float* __restrict__ W, const float* x, float* y) {
@@ -157,6 +190,7 @@ struct PropArgs {
     const float* rays_d;
     const float* cnf;
     uint32_t N, n_cnf;
+    RayTiles tiles;        // slot -> ray (rays_o / rays_d / cnf are in ray order)
     float aabb[6];
     float min_near;
     GridScale gs;
@@ -209,13 +243,13 @@ __global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
     // the end recompute ray N - 1 and store nothing)
     if (LOOK != kLookBox4 && r0 >= a.N) return;
     const bool live = r0 < a.N;
-    const uint32_t r = live ? r0 : a.N - 1u;
-    const uint32_t N = a.N;
+    const uint32_t r = live ? r0 : a.N - 1u;              // slot
+    const uint32_t N = a.N, ray = a.tiles(r);
     float o[3], d[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        o[c] = a.rays_o[(size_t)r * 3 + c];
-        d[c] = a.rays_d[(size_t)r * 3 + c];
+        o[c] = a.rays_o[(size_t)ray * 3 + c];
+        d[c] = a.rays_d[(size_t)ray * 3 + c];
     }
     const float sn = a.snf[r], sf = a.snf[N + r];           // k_snf (stage 0) / stage 0 (stage 1)
     float b0, b1;
@@ -283,18 +317,19 @@ __global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
 // Stage 0 ray setup, one thread per ray: near/far from the AABB slab test
 // (renderer.py:122-139, 229-236) and their spacing (renderer.py:250-253).
 __global__ void __launch_bounds__(256) k_snf(PropArgs a) {
-    const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t r = blockIdx.x * 256u + threadIdx.x;  // slot
     if (r >= a.N) return;
+    const uint32_t ray = a.tiles(r);
     float o[3], d[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        o[c] = a.rays_o[(size_t)r * 3 + c];
-        d[c] = a.rays_d[(size_t)r * 3 + c];
+        o[c] = a.rays_o[(size_t)ray * 3 + c];
+        d[c] = a.rays_d[(size_t)ray * 3 + c];
     }
     float near, far;
     near_far_aabb(o, d, a.aabb, a.min_near, near, far);
     if (a.cnf) {  // renderer.py:234-236
-        const uint32_t q = a.n_cnf == 1 ? 0u : r;
+        const uint32_t q = a.n_cnf == 1 ? 0u : ray;
         const float cn = a.cnf[q * 2], cf = a.cnf[q * 2 + 1];
         near = (isnan(near) || isnan(cn)) ? NAN : fmaxf(near, cn);
         far = (isnan(far) || isnan(cf)) ? NAN : fminf(far, cf);
@@ -423,6 +458,7 @@ struct FinalArgs {
     float* depth;      // [N]
     float* wsum;       // [N]
     float* rows;       // [N, kRow] or null
+    RayTiles tiles;    // slot -> ray: rays_o / rays_d and the per-ray outputs are in ray order
     // N1 (flagged, non-parity; samnerf_model.t_thresh): optical depth
     // -ln(t_thresh) past which a ray is opaque; a wave whose rays all are
     // stops marching.  INFINITY: off (the default, the reference's semantics).
@@ -768,10 +804,13 @@ k_final(FinalArgs a) {
     const float2* __restrict__ emb = reinterpret_cast<const float2*>(a.grid_emb);
 
     float o[3], d[3];
+    {
+        const uint32_t ray = a.tiles(rr);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        o[c] = a.rays_o[(size_t)rr * 3 + c];
-        d[c] = a.rays_d[(size_t)rr * 3 + c];
+        for (int c = 0; c < 3; ++c) {
+            o[c] = a.rays_o[(size_t)ray * 3 + c];
+            d[c] = a.rays_d[(size_t)ray * 3 + c];
+        }
     }
     const float sn = a.snf[rr], sf = a.snf[N + rr];
     float rb_prev = real_bin(sn, sf, a.bins_in[(size_t)seg * N + rr]);
@@ -1037,7 +1076,8 @@ k_final(FinalArgs a) {
     for (int q = 0; q < 16; ++q) v3 = MFMA32(Vl[kV3 + q * 64 + lane], v2[q], v3);
 
     if (!live || seg != 0) return;
-    float* row = a.rows ? a.rows + (size_t)r * kRow : nullptr;
+    const uint32_t ray = a.tiles(r);                     // per-ray outputs in ray order
+    float* row = a.rows ? a.rows + (size_t)ray * kRow : nullptr;
     if (row) {                                 // geo units owned by this half-wave
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -1050,10 +1090,10 @@ k_final(FinalArgs a) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {                // rows 0..2 of v3 = registers 0..2, lower half
         img[c] = sigmoidf(v3[c]) + (1.0f - ws) * a.bg;
-        a.image[(size_t)r * 3 + c] = img[c];
+        a.image[(size_t)ray * 3 + c] = img[c];
     }
-    a.depth[r] = dp;
-    a.wsum[r] = ws;
+    a.depth[ray] = dp;
+    a.wsum[ray] = ws;
     if (row) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) row[143 + i] = sh[i] * ws;
@@ -1067,6 +1107,7 @@ k_final(FinalArgs a) {
 
 struct SgridArgs {
     uint32_t N;
+    RayTiles tiles;      // slot -> ray of the rows
     GridDesc<16> grid;
     const float* u_in;   // [T][3][N]
     const float* w_in;   // [T][N]
@@ -1137,7 +1178,7 @@ __global__ void __launch_bounds__(256) k_sgrid(SgridArgs a) {
     if (q > 0 || !live) return;
 #pragma unroll
     for (int c = 0; c < 8; ++c) acc[c] = ((acc[c] + part[0][c][lane]) + part[1][c][lane]) + part[2][c][lane];
-    float4* dst = reinterpret_cast<float4*>(a.rows + (size_t)r * kRow + level * 8u);
+    float4* dst = reinterpret_cast<float4*>(a.rows + (size_t)a.tiles(r) * kRow + level * 8u);
     dst[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
     dst[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
 }
@@ -1247,7 +1288,7 @@ k_sgrid_box4(SgridArgs a) {
     }
     __syncthreads();
     if (q > 0 || !live) return;
-    float* dst = a.rows + (size_t)r * kRow + g * 32u;
+    float* dst = a.rows + (size_t)a.tiles(r) * kRow + g * 32u;
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
         float v[8];
@@ -1287,7 +1328,7 @@ constexpr uint32_t kBwdBoxCells = 64;
 
 template <int T>
 __global__ void __launch_bounds__(256)
-k_sgrid_backward(uint32_t N, GridDesc<16> g, const float* __restrict__ u_in,
+k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __restrict__ u_in,
                  const float* __restrict__ w_in, const float* __restrict__ grad, uint32_t gstride,
                  float* __restrict__ gemb, uint32_t max_cells) {
     __shared__ float box[4][kBwdBoxCells * 8];           // per wave: cell x channel sums
@@ -1300,7 +1341,7 @@ k_sgrid_backward(uint32_t N, GridDesc<16> g, const float* __restrict__ u_in,
     const bool live = r < N;                                // lanes stay for the reductions
     const uint32_t rr = live ? r : N - 1;
     const LevelDesc d = g.lv[level];
-    const float gv = live ? grad[(size_t)rr * gstride + level * 8u + ch] : 0.0f;
+    const float gv = live ? grad[(size_t)tiles(rr) * gstride + level * 8u + ch] : 0.0f;
     float* base = gemb + (size_t)d.off * 8u + ch;
     float* slice = box[wv];
     uint32_t* rows = list[wv];
@@ -1744,11 +1785,15 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     if (m->with_sam && (rc = make_grid_desc(m->s_grid, 8, 16, gs, "s_grid"))) return rc;
 
     const uint32_t nb = div_up(N, 256);
+    // parity taps expose slot-ordered intermediates as ray-major views: the
+    // identity map while they are set
+    const RayTiles tiles = g_taps_on ? RayTiles{0u, 0u} : make_ray_tiles(N, m->view_width);
     PropArgs pa{};
     pa.rays_o = rays_o;
     pa.rays_d = rays_d;
     pa.cnf = cam_near_far;
     pa.N = N;
+    pa.tiles = tiles;
     pa.n_cnf = n_cnf;
     for (int i = 0; i < 6; ++i) pa.aabb[i] = m->aabb[i];
     pa.min_near = m->min_near;
@@ -1799,6 +1844,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.rays_o = rays_o;
     fa.rays_d = rays_d;
     fa.N = N;
+    fa.tiles = tiles;
     fa.gs = make_grid_scale(m->grid_bound);
     fa.bg = bg_color;
     fa.grid = gg;
@@ -1844,6 +1890,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     if (sam_rows) {
         SgridArgs sa{};
         sa.N = N;
+        sa.tiles = tiles;
         sa.grid = gs;
         sa.u_in = w.u_f;
         sa.w_in = w.w_f;
@@ -1906,7 +1953,8 @@ int samnerf_sgrid_backward(const samnerf_model* m, const float* grad_fsam, uint3
     const char* sp = getenv("SAMNERF_SGRID_BWD_SPLIT");
     const uint32_t split = sp ? (uint32_t)std::max(1, std::min(32, atoi(sp))) : 1u;
     k_sgrid_backward<32><<<dim3(div_up((uint64_t)N * 8, 256), 16, split), 256, 0,
-                           reinterpret_cast<hipStream_t>(stream)>>>(N, gs, w.u_f, w.w_f, grad_fsam,
+                           reinterpret_cast<hipStream_t>(stream)>>>(N, make_ray_tiles(N, m->view_width),
+                                                                     gs, w.u_f, w.w_f, grad_fsam,
                                                                      kRow, grad_embeddings, max_cells);
     return check_launch("sgrid_backward");
 }

@@ -152,7 +152,10 @@ class NeRFRenderer(nn.Module):
             cnf = cam_near_far
             if cnf is not None and cnf.shape[0] != 1:
                 cnf = cnf[head:tail]
-            part = self.run(rays_o[head:tail], rays_d[head:tail], cam_near_far=cnf, **kwargs)
+            # chunks of whole image rows keep the ray-tiling hint (W only: the
+            # chunk's samvit stays flat)
+            wk = W if (W is not None and step % W == 0) else None
+            part = self.run(rays_o[head:tail], rays_d[head:tail], cam_near_far=cnf, W=wk, **kwargs)
             for k, v in part.items():
                 if v is None:
                     continue
@@ -180,8 +183,10 @@ class NeRFRenderer(nn.Module):
             from samnerf_amd.fused import FusedRenderer
             if self._fused is None or self._fused.net is not self:
                 self._fused = FusedRenderer(self)
+            n = rays_o.shape[0]
+            vw = W if (W is not None and n % W == 0) else 0      # a whole number of image rows
             out = self._fused.render(rays_o, rays_d, cam_near_far, bg_color,
-                                     feats=return_feats > 0)
+                                     feats=return_feats > 0, view_width=vw)
             samvit = out.pop("samvit", None)
             if return_feats > 0 and samvit is not None:
                 out["samvit"] = samvit.view(H, W, -1) if H is not None else samvit

@@ -35,7 +35,7 @@ class SamnerfModel(ctypes.Structure):
                 ("sam_w", _vp * 5), ("sam_b", _vp * 5), ("ln_w", _vp), ("ln_b", _vp),
                 ("with_sam", _int), ("aabb", _f32 * 6), ("grid_bound", _f32),
                 ("min_near", _f32), ("num_steps", _u32 * 3), ("head_mode", _int),
-                ("t_thresh", _f32)]
+                ("t_thresh", _f32), ("view_width", _u32)]
 
 
 _SIGS = {

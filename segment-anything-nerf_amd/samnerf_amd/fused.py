@@ -127,7 +127,7 @@ class FusedRenderer:
     # -------------------------------------------------------------- render --
     @torch.no_grad()
     def render(self, rays_o, rays_d, cam_near_far=None, bg_color=None, rows=None,
-               keep_workspace=False, feats=True, taps=False, own_workspace=False):
+               keep_workspace=False, feats=True, taps=False, own_workspace=False, view_width=0):
         """rays_o, rays_d [N,3] (CUDA fp32) -> dict(image [N,3], depth [N],
         weights_sum [N], samvit [N,256] if with_sam and feats).  `rows`
         (optional [N,164] tensor) receives the head input cat(f_sam, f_image,
@@ -139,12 +139,16 @@ class FusedRenderer:
         ray-major views of the kernels' sample-major buffers.
         own_workspace=True renders into a fresh workspace (from torch's
         caching allocator) instead of the per-stream one, so a caller can
-        keep it (training: the backward reads its sample weights/positions)."""
+        keep it (training: the backward reads its sample weights/positions).
+        view_width: the rays are a row-major image of this width (a layout
+        hint, samnerf_model.view_width): the kernels then run 8 x 4 pixel
+        tiles per wave, same outputs bit for bit, faster gathers."""
         rays_o = rays_o.contiguous().float()
         rays_d = rays_d.contiguous().float()
         N = rays_o.shape[0]
         dev = rays_o.device
         m = self.model()
+        m.view_width = 0 if taps else int(view_width or 0)
         if own_workspace:
             need = lib().samnerf_render_workspace_size(ctypes.byref(m), N)
             ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
@@ -194,11 +198,12 @@ class FusedRenderer:
         if samvit is not None:
             out["samvit"] = samvit
         if keep_workspace:
-            out["_workspace"] = (ws, need, m)
+            out["_workspace"] = (ws, need, m, int(m.view_width))
         return out
 
     def sgrid_backward(self, grad_rows, workspace, grad_embeddings):
-        ws, need, m = workspace
+        ws, need, m, view_width = workspace
+        m.view_width = view_width                 # the forward's slot order of the workspace
         N = grad_rows.shape[0]
         grad_rows = grad_rows.contiguous()
         assert grad_rows.shape[1] == ROW
@@ -213,14 +218,15 @@ class _FusedSamRows(torch.autograd.Function):
     cut by sample_pdf(...).detach(), renderer.py:274-275)."""
 
     @staticmethod
-    def forward(ctx, s_emb, renderer, rays_o, rays_d, cam_near_far, bg_color):
+    def forward(ctx, s_emb, renderer, rays_o, rays_d, cam_near_far, bg_color, view_width):
         N = rays_o.shape[0]
         rows = torch.empty(N, ROW, device=rays_o.device)
         # feats=False: the head runs in torch below (it needs autograd), so the
         # fused head is skipped; a private workspace keeps the sample weights
         # and positions the s_grid scatter of the backward reads
         out = renderer.render(rays_o, rays_d, cam_near_far, bg_color, rows=rows,
-                              keep_workspace=True, feats=False, own_workspace=True)
+                              keep_workspace=True, feats=False, own_workspace=True,
+                              view_width=view_width)
         ctx.ws = out.pop("_workspace")
         ctx.renderer = renderer
         ctx.keep = list(renderer._keep)
@@ -234,7 +240,7 @@ class _FusedSamRows(torch.autograd.Function):
         if ctx.needs_input_grad[0] and g_rows is not None:
             grad = torch.zeros(ctx.emb_shape, device=g_rows.device)
             ctx.renderer.sgrid_backward(g_rows, ctx.ws, grad)
-        return grad, None, None, None, None, None
+        return grad, None, None, None, None, None, None
 
 
 def _head_params(net):
@@ -280,7 +286,8 @@ class _SamHeadTrain(torch.autograd.Function):
         return (grows, None, *grads)
 
 
-def render_sam_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None, head=None):
+def render_sam_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None, head=None,
+                     view_width=0):
     """Differentiable SAM-feature render for the distillation step
     (nerf/utils.py:1098-1099): returns samvit [N,256] with autograd to
     s_grid.embeddings (HIP scatter) and samvit_mlp (HIP head forward +
@@ -289,7 +296,7 @@ def render_sam_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None,
     import os
     net = renderer.net
     rows, image, depth, wsum = _FusedSamRows.apply(net.s_grid.embeddings, renderer, rays_o,
-                                                    rays_d, cam_near_far, bg_color)
+                                                    rays_d, cam_near_far, bg_color, view_width)
     head = head or os.environ.get("SAMNERF_TRAIN_HEAD", "hip")
     if head == "torch":
         samvit = net.samvit_mlp(rows[:, :163])

@@ -430,3 +430,30 @@ def test_fused_render_from_reference_layout_checkpoint(hip_lib, cuda, tmp_path):
                        ema_shadow=[p.detach().clone() for p in src.parameters()])
     ck.load_checkpoint(net, str(tmp_path / "ngp_ep0004.pth"), use_ema=True, map_location=cuda)
     _check_outputs(net.render(ro, rd, staged=False, return_feats=1, H=H, W=W), ref)
+
+
+@pytest.mark.parametrize("surface", [False, True])
+def test_ray_tiling_bit_identical(hip_lib, cuda, surface):
+    """samnerf_model.view_width (8 x 4 pixel tiles per wave) only changes which
+    rays share a wave: every output, the head-input rows included, equals the
+    row-major render bit for bit; a width the tiling cannot use (N not a
+    multiple of 4 rows) falls back to row-major order."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer
+    spec = synth.ModelSpec(with_sam=True)
+    params = (synth.make_surface_params(spec, seed=3) if surface
+              else synth.make_params(spec, seed=21, emb_scale=0.5, ln_jitter=0.1))
+    net = make_net(spec, params, cuda)
+    H, W = 96, 128
+    pose, intr = synth.gui_camera(W, H, rot=synth.random_rotation(4))
+    ro, rd = ops.get_rays(pose, intr, H, W, device=cuda)
+    fr = FusedRenderer(net)
+    outs = []
+    for vw, n in ((0, H * W), (W, H * W), (W, H * W - 2 * W)):
+        rows = torch.empty(n, 164, device=cuda)
+        o = fr.render(ro[:n], rd[:n], rows=rows, view_width=vw)
+        o["rows"] = rows
+        outs.append({k: v.cpu() for k, v in o.items()})
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+        assert torch.equal(outs[0][k][:H * W - 2 * W], outs[2][k]), k

@@ -314,3 +314,28 @@ def test_fused_adam_matches_torch_adam(hip_lib, cuda, wd):
             assert (x - y).abs().max().item() <= 1e-5 * y.abs().max().item(), k
         assert int(o1.state[a]["step"]) == int(o2.state[b]["step"])
 
+
+
+def test_distillation_step_with_ray_tiles(hip_lib, cuda):
+    """render_sam_train over a 64 x 64 feature view with view_width = 64 (8 x 4
+    ray tiles; the s_grid scatter reads the forward's slot-ordered samples and
+    the ray-ordered row gradients): the same samvit bits and the same
+    gradients (to float-atomic order) as row-major waves."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer, render_sam_train
+    net = _frozen_net(cuda, seed=7)
+    net.train()
+    pose, intr = synth.gui_camera(64, 64, rot=synth.random_rotation(2))
+    ro, rd = ops.get_rays(pose, intr, 64, 64, device=cuda)
+    g = torch.randn(4096, 256, generator=torch.Generator().manual_seed(3)).to(cuda)
+    params = [p for p in net.parameters() if p.requires_grad]
+    res = []
+    for vw in (0, 64):
+        for p in params:
+            p.grad = None
+        out = render_sam_train(FusedRenderer(net), ro, rd, view_width=vw)["samvit"]
+        (out * g).sum().backward()
+        res.append((out.detach().cpu(), [p.grad.detach().cpu().clone() for p in params]))
+    assert torch.equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert ((a - b).norm() / b.norm().clamp_min(1e-12)).item() < 1e-5

@@ -11,6 +11,7 @@ GROUPS_=(
   "TA_BUSY_avr TA_BUSY_max SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
   "FETCH_SIZE"
   "WRITE_SIZE"
+  "TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE"
 )
 i=0
 for g in "${GROUPS_[@]}"; do
