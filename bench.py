@@ -81,9 +81,10 @@ BF16_MFMA_PEAK_TFS = 2500.0    # MI355X_MICROARCH.md: dense BF16 ~2.5 PF
 F32_MFMA_PEAK_TFS = 157.3      # MI355X_MICROARCH.md: F32 matrix = vector peak
 DTYPE = {0: "fp32 in the reference's op order for everything that decides a discrete result "
             "(near/far, bins, proposal grids + MLPs, compositing, sample_pdf); grid_mlp "
-            "(32->64->64->16 per sample) and the SAM head (163->256x5) on bf16x3 split-precision "
-            "MFMA with fp32 accumulate (~1e-5 relative); view_mlp on fp32 MFMA",
-         1: "fp32 throughout: grid_mlp, view_mlp and the SAM head on fp32 MFMA "
+            "(32->64->64->16 per sample), the SAM head (163->256x5) and the mask head (143->256->256->K "
+            "per sample) on bf16x3 split-precision MFMA with fp32 accumulate (~1e-5 relative); "
+            "view_mlp on fp32 MFMA",
+         1: "fp32 throughout: grid_mlp, view_mlp, the SAM head and the mask head on fp32 MFMA "
             "(v_mfma_f32_32x32x2_f32), the rest in the reference's op order"}
 
 
@@ -260,6 +261,55 @@ def reference_equivalent_gpu(net, ro, rd, n_rays, chunk=16384):
     return {"value": n / dt, "unit": "rays/s", "rays": n,
             "what": "NeRFRenderer.run_torch (the reference's unfused torch op sequence, drop-in HIP "
                     "encoders), chunks of 16384 rays, same view and weights"}
+
+
+def mask_view(dev, steps, warmup, head_mode=0, ref_rays=32768):
+    """--with_mask rendering (mask_mlp_type 'default', n_inst 2, RGB + instance
+    logits, no SAM; renderer.py:392-395, :451-452) of one 512 x 512 view:
+    the fused render + k_mask_head against the reference's unfused op
+    sequence (run_torch, return_mask=1) on the same GPU (`ref_rays` of the
+    view, chunks of 16384).  Returns the side-line dict."""
+    from nerf.network import NeRFNetwork, default_opt
+    from samnerf_amd import ops, synth
+    from samnerf_amd.fused import FusedRenderer
+    spec = synth.ModelSpec(with_sam=False, with_mask=True, mask_type="default", sum_after_mlp=False)
+    params = synth.make_params(spec, seed=0, emb_scale=1e-4)
+    net = NeRFNetwork(default_opt(with_sam=False, with_mask=True, mask_mlp_type="default", n_inst=2))
+    net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    net = net.to(dev).eval()
+    H = W = 512
+    pose, intr = synth.gui_camera(W, H)
+    fr = FusedRenderer(net, head_mode=head_mode)
+
+    def view():
+        ro, rd = ops.get_rays(pose, intr, H, W, device=dev)
+        return fr.render(ro, rd, mask=True, view_width=W)
+
+    for _ in range(warmup):
+        view()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = view()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    ro, rd = ops.get_rays(pose, intr, H, W, device=dev)
+    n, chunk = min(ref_rays, H * W), 16384
+    with torch.no_grad():
+        ref = net.run_torch(ro[:chunk], rd[:chunk], return_mask=1)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for h in range(0, n, chunk):
+            ref = net.run_torch(ro[h:h + chunk], rd[h:h + chunk], return_mask=1)
+        torch.cuda.synchronize()
+        dt_ref = (time.perf_counter() - t1) / n
+    err = (out["instance_mask_logits"][n - chunk:n] - ref["instance_mask_logits"]).abs().max().item()
+    return {"value": H * W / dt, "unit": "rays/s", "ms_per_step": dt * 1e3,
+            "reference_equivalent_gpu": {"value": 1.0 / dt_ref, "unit": "rays/s", "rays": n},
+            "speedup": (H * W / dt) * dt_ref,
+            "max_abs_logits_vs_unfused": err, "dtype": DTYPE[head_mode],
+            "what": "--with_mask 'default' head (m_grid L16C8 + SkipConnMLP 143->256->256->2 per sample, "
+                    "weighted sum): fused render + k_mask_head vs run_torch(return_mask=1), 512x512 view"}
 
 
 def train_steps(dev, steps, warmup, torch_adam=False):
@@ -634,6 +684,10 @@ def main():
             "what": "FLAGGED NON-PARITY mode (SURVEY H6), never the default: a wave of 32 rays stops the "
                     "final stage once every ray's transmittance < t_thresh; opaque-sphere scene "
                     "(synth.make_surface_params), same view"}
+
+    if not args.no_alt and world == 1 and args.rank_share <= 1:
+        # the --with_mask instance head on the fused kernels
+        side["mask_default_head"] = mask_view(dev, max(3, args.steps // 2), 2, args.head_mode)
 
     if not args.no_alt and world == 1 and args.rank_share <= 1 and with_sam:
         # BASELINE config 5 beside the headline (`--mode train` runs it alone)

@@ -186,6 +186,14 @@ typedef struct {
                                      8 x 4 pixel tiles (compact wave footprints, better gather
                                      locality); outputs stay in ray order and are bit-identical.
                                      samnerf_sgrid_backward must see the value of the forward. */
+    /* --with_mask, mask_mlp_type 'default' (network.py:125-133, renderer.py:392-395,
+     * :451-452): m_grid L16 C8 and SkipConnMLP(143 -> 256 -> 256 -> mask_out, bias=False,
+     * leaky_relu); with_mask = 0 when the model has no such head.  Rendered by
+     * samnerf_mask_forward after samnerf_render_forward. */
+    int with_mask;
+    samnerf_grid m_grid;
+    const float* mask_w[3];       /* [256,143] [256,256] [mask_out,256] */
+    uint32_t mask_out;            /* n_inst + redundant_instance, 1..32 */
 } samnerf_model;
 
 /* Bytes of device workspace samnerf_render_forward needs for N rays. */
@@ -211,6 +219,15 @@ int samnerf_render_forward(const samnerf_model* model, const float* rays_o,
                            uint32_t n_cnf, float bg_color, float* image, float* depth,
                            float* weights_sum, float* samvit, float* feature_rows,
                            void* workspace, size_t workspace_bytes, samnerf_stream_t stream);
+
+/* instance_mask_logits [N, mask_out] (renderer.py:392-395, :451-452):
+ * sum_k w_k * mask_mlp(cat(m_grid(x_k), geo_feat_k)) over the final samples, the
+ * weights and positions those of the samnerf_render_forward call that last used
+ * `workspace` (same model, N and view_width; it stores each sample's geo_feat
+ * when model->with_mask).  Precision follows head_mode (bf16x3 / exact fp32 MFMA).
+ * Replaces the reference's per-chunk torch ops of that branch. */
+int samnerf_mask_forward(const samnerf_model* model, uint32_t N, float* instance_mask_logits,
+                         const void* workspace, size_t workspace_bytes, samnerf_stream_t stream);
 
 /* Backward of the s_grid feature composite for the SAM-distillation step
  * (nerf/utils.py:1098-1106 training branch): given the per-ray gradient of

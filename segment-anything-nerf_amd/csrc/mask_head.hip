@@ -1,0 +1,350 @@
+// mask_head.hip -- the --with_mask instance head (mask_mlp_type 'default') on
+// gfx950 matrix cores, fused after the ray march.
+//
+// Reference (nerf/network.py:125-133, nerf/renderer.py:322-323, :392-395,
+// :451-452): per final sample k of a ray
+//     point_mask_k = SkipConnMLP(143 -> 256 -> 256 -> K, bias=False, leaky_relu)
+//                        (cat(m_grid(x_k) [16 levels x 8 channels], geo_feat_k [15]))
+//     instance_mask_logits = sum_k weights_k.detach() * point_mask_k
+// The head is non-linear, so the sum cannot move in front of it: it runs on
+// all 32 samples of every ray (~6.5 MFLOP per ray, 3x the SAM head's GEMM
+// work per ray x 32 samples / 10).  The reference materialises [N, 32, 143]
+// and [N, 32, 256] twice per 16K-ray chunk; here nothing per sample leaves
+// the registers except the weight stream.
+//
+// One workgroup = 128 ray slots (4 waves x 32), looping over the 32 samples.
+// Per sample a wave gathers its 32 rays' m_grid features straight into the
+// B operands of layer 0 (lane half h of k-block kb < 8 = level 2 kb + h, its 8
+// channels = one 32-B corner row per corner: lookup_level3<8>), k-block 8 =
+// geo_feat (k_final stores it per sample when the model has a mask head).
+// Orientation and weight stream are k_sam_head_bf3's (sam_head.hip):
+// out^T[256 units x 32 rays] = W . act^T, 8 accumulator tiles per wave whose
+// registers are the next layer's B operands, weights in 16 KiB steps through
+// a 3-deep LDS ring by direct DMA, shared by the 4 waves.  27 steps per sample:
+// layer 0 (9 k-blocks x 8 tiles), layer 1 (16 x 8), layer 2 (16 k-blocks x
+// the one output tile, 8 per step).  The weighted sum over samples stays in
+// the output tile's registers.
+//
+// Precision (head_mode): 0 = bf16x3 split precision (3 bf16 MFMAs per 16-deep
+// k-block, ~1e-5 relative); 1 = exact fp32 (8 v_mfma_f32_32x32x2_f32 per
+// k-block, the step holds the fp32 weights in the same 32 B per lane and
+// tile).
+#include <algorithm>
+
+#include "samnerf_common.h"
+
+using namespace samnerf;
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+
+constexpr int kMIn = 143;                     // 128 m_grid features + 15 geo
+constexpr int kL0kb = 9;                      // 8 level pairs + geo (15 + 1 pad)
+constexpr int kHkb = 16;                      // 256 -> 16 k-blocks
+constexpr int kStepsPerSample = kL0kb + kHkb + 2;   // 27
+constexpr int kStepVec = 2 * 8 * 64;          // uint4 per step
+constexpr int kSlots = 128;                   // ray slots per workgroup
+constexpr int kT = 32;                        // final samples per ray
+
+__device__ __forceinline__ int rho(int q) { return (q & 3) + 8 * (q >> 2); }
+__device__ __forceinline__ int hidden_unit(int kb, int h, int m) {
+    return 32 * (kb >> 1) + rho(8 * (kb & 1) + m) + 4 * h;
+}
+
+__device__ __forceinline__ void split_pair(float x, float y, uint32_t& hi, uint32_t& lo) {
+    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v){x, y}, bf16x2v));
+    const float hx = __uint_as_float(hi << 16), hy = __uint_as_float(hi & 0xffff0000u);
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v){x - hx, y - hy}, bf16x2v));
+}
+
+// 8 values of one lane's k-block as the B operand pair: bf16x3 hi / lo, or
+// (EXACT) the fp32 values themselves, 4 in each uint4
+template <bool EXACT>
+__device__ __forceinline__ void to_operand(const float* v, uint4& a, uint4& b) {
+    if constexpr (EXACT) {
+        a = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
+        b = make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7]));
+    } else {
+        split_pair(v[0], v[1], a.x, b.x);
+        split_pair(v[2], v[3], a.y, b.y);
+        split_pair(v[4], v[5], a.z, b.z);
+        split_pair(v[6], v[7], a.w, b.w);
+    }
+}
+
+__device__ __forceinline__ float u4f(const uint4& u, int i) {
+    return __uint_as_float(i == 0 ? u.x : i == 1 ? u.y : i == 2 ? u.z : u.w);
+}
+
+// acc += A . B over one 16-deep k-block
+template <bool EXACT>
+__device__ __forceinline__ floatx16 kblock(uint4 a0, uint4 a1, uint4 b0, uint4 b1, floatx16 c) {
+    if constexpr (EXACT) {
+        // instruction s: lane (i, h) A = W[i][input (kb, h, s)], B = x[input (kb, h, s)]
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(s < 4 ? u4f(a0, s) : u4f(a1, s - 4),
+                                                    s < 4 ? u4f(b0, s) : u4f(b1, s - 4), c, 0, 0, 0);
+        return c;
+    } else {
+        const bf16x8 Ah = __builtin_bit_cast(bf16x8, a0), Al = __builtin_bit_cast(bf16x8, a1);
+        const bf16x8 Bh = __builtin_bit_cast(bf16x8, b0), Bl = __builtin_bit_cast(bf16x8, b1);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Al, Bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Ah, Bl, c, 0, 0, 0);
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(Ah, Bh, c, 0, 0, 0);
+    }
+}
+
+// packed[step 27][part 2][slot 8][lane 64] uint4: steps 0-8 layer 0 (slot =
+// output tile), 9-24 layer 1 (slot = tile), 25-26 layer 2 (slot = k-block
+// 8 (step - 25) + slot of the single output tile).  Lane (i, h), 8 values m
+// of k-block kb: W[32 t + i][input (kb, h, m)], input = 16 kb + 8 h + m for
+// layer 0 (m_grid level 2 kb + h channel m; kb 8: geo 8 h + m at column 128 +
+// 8 h + m, column 143 = padding), hidden_unit(kb, h, m) for layers 1-2.
+template <bool EXACT>
+__global__ void __launch_bounds__(256)
+k_mask_pack(const float* __restrict__ w0, const float* __restrict__ w1, const float* __restrict__ w2,
+            uint32_t K, uint4* __restrict__ packed) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint32_t)kStepsPerSample * 8u * 64u) return;
+    const int lane = (int)(t & 63u), slot = (int)((t >> 6) & 7u), step = (int)(t >> 9);
+    const int i = lane & 31, h = lane >> 5;
+    float v[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        float w;
+        if (step < kL0kb) {                               // layer 0: tile = slot
+            const int col = 16 * step + 8 * h + m;
+            w = col < kMIn ? w0[(32 * slot + i) * kMIn + col] : 0.0f;
+        } else if (step < kL0kb + kHkb) {                 // layer 1
+            const int kb = step - kL0kb;
+            w = w1[(32 * slot + i) * 256 + hidden_unit(kb, h, m)];
+        } else {                                          // layer 2: one tile
+            const int kb = 8 * (step - kL0kb - kHkb) + slot;
+            w = (uint32_t)i < K ? w2[i * 256 + hidden_unit(kb, h, m)] : 0.0f;
+        }
+        v[m] = w;
+    }
+    uint4 a, b;
+    to_operand<EXACT>(v, a, b);
+    packed[(size_t)step * kStepVec + slot * 64 + lane] = a;
+    packed[(size_t)step * kStepVec + 512 + slot * 64 + lane] = b;
+}
+
+struct MaskArgs {
+    GridDesc<16> grid;       // m_grid
+    const float* u_in;       // [32][3][N] grid-space sample positions (slot order)
+    const float* w_in;       // [32][N] final weights
+    const float* geo_in;     // [32][16][N] grid_mlp output rows (row 0 = sigma, unused)
+    uint32_t N, K;
+    RayTiles tiles;
+    const uint4* packed;
+    float* out;              // [N][K] (ray order)
+};
+
+// The weight stream of sam_head.hip's HeadStepper (DMA from inline asm into a
+// 3-step LDS ring, two steps ahead, counted vmcnt): the gathers issued at the
+// start of each sample are ordinary loads younger or older than the DMAs, and
+// either way only make those counted waits wait longer.
+struct MaskStepper {
+    const uint4* __restrict__ packed;
+    uint4* Wb;
+    int wave, lane;
+    uint32_t step;                                        // global step (sample * 27 + s)
+    uint32_t total;
+
+    __device__ __forceinline__ void issue(uint32_t s) {
+        const uint4* src = packed + (size_t)(s % kStepsPerSample) * kStepVec + wave * 256 + lane;
+        const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(Wb + (s % 3u) * kStepVec + wave * 256);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t d = __builtin_amdgcn_readfirstlane(dst + c * 1024u);
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(src + c * 64), "s"(d)
+                : "memory");
+        }
+    }
+
+    __device__ __forceinline__ void finish() {
+        if (step + 2 < total) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // step + 1 landed
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        ++step;
+    }
+
+    // one k-block for all 8 output tiles
+    template <bool EXACT>
+    __device__ __forceinline__ void run8(floatx16 (&acc)[8], const uint4& b0, const uint4& b1) {
+        if (step + 2 < total) issue(step + 2);
+        const uint4* cur = Wb + (step % 3u) * kStepVec + lane;
+        uint4 f0[8], f1[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            f0[t] = cur[t * 64];
+            f1[t] = cur[512 + t * 64];
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = kblock<EXACT>(f0[t], f1[t], b0, b1, acc[t]);
+        finish();
+    }
+
+    // eight k-blocks of the one output tile
+    template <bool EXACT>
+    __device__ __forceinline__ void run1(floatx16& acc, const uint4* b0, const uint4* b1) {
+        if (step + 2 < total) issue(step + 2);
+        const uint4* cur = Wb + (step % 3u) * kStepVec + lane;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = kblock<EXACT>(cur[k * 64], cur[512 + k * 64], b0[k], b1[k], acc);
+        finish();
+    }
+};
+
+__device__ __forceinline__ float leaky(float x) { return x < 0.0f ? x * 0.01f : x; }
+
+// leaky_relu on the accumulators, then the next layer's B operands (k-block
+// kb = 2t + s <- registers 8s..8s+7 of tile t, hidden_unit order)
+template <bool EXACT>
+__device__ __forceinline__ void epilogue(const floatx16 (&acc)[8], uint4 (&a0)[kHkb], uint4 (&a1)[kHkb]) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = leaky(acc[t][q]);
+        to_operand<EXACT>(v, a0[2 * t], a1[2 * t]);
+        to_operand<EXACT>(v + 8, a0[2 * t + 1], a1[2 * t + 1]);
+    }
+}
+
+constexpr int kXVec = kL0kb * 2 * 64;          // uint4 per wave: layer-0 B operands [kb][part][lane]
+constexpr int kDescVec = (16 * (int)sizeof(LevelDesc) + 15) / 16;
+
+template <bool EXACT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_mask_head(MaskArgs a) {
+    // one LDS object: the 3-step weight ring | each wave's layer-0 B operands
+    // of the current sample (the gathers land there, not in 72 VGPRs that
+    // would live through layer 0 next to the accumulators, fragments and
+    // activations: with them the kernel spilled ~350 registers) | the m_grid
+    // level descriptors (read per lane: a select between two kernel-argument
+    // descriptors became per-lane loads from the kernarg segment)
+    __shared__ uint4 smem[3 * kStepVec + 4 * kXVec + kDescVec];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int j = lane & 31, h = lane >> 5;
+    const uint32_t slot = blockIdx.x * kSlots + wave * 32u + j;
+    const bool live = slot < a.N;
+    const uint32_t ss = live ? slot : a.N - 1u, N = a.N;
+    uint4* const Xw = smem + 3 * kStepVec + wave * kXVec;
+    LevelDesc* const sLv = reinterpret_cast<LevelDesc*>(smem + 3 * kStepVec + 4 * kXVec);
+    if (tid < 16) sLv[tid] = a.grid.lv[tid];
+
+    MaskStepper st{a.packed, smem, wave, lane, 0u, (uint32_t)kT * kStepsPerSample};
+    st.issue(0);
+    st.issue(1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");          // step 0 landed
+    __syncthreads();
+
+    floatx16 sum = {};                                       // sum_k w_k * logits_k
+    floatx16 acc[8];
+    uint4 a0[kHkb], a1[kHkb];
+#pragma unroll 1
+    for (int k = 0; k < kT; ++k) {
+        // inputs of sample k.  `ko` is opaque so that the per-sample addresses
+        // are formed here, not carried through the loop as 64-bit induction
+        // pointers
+        uint32_t ko = (uint32_t)k;
+        asm volatile("" : "+s"(ko));
+        const float* up = a.u_in + (size_t)ko * 3u * N + ss;
+        const float ux = up[0], uy = up[N], uz = up[2u * N];
+        const float w = live ? a.w_in[(size_t)ko * N + ss] : 0.0f;
+        // the m_grid gathers: lane half h of k-block kb = level 2 kb + h
+#pragma unroll
+        for (int kb = 0; kb < 8; ++kb) {
+            float f[8];
+            const LevelDesc d = sLv[2 * kb + h];
+            lookup_level3<8>(a.grid.emb, d, ux, uy, uz, f);
+            uint4 xa, xb;
+            to_operand<EXACT>(f, xa, xb);
+            Xw[(2 * kb) * 64 + lane] = xa;
+            Xw[(2 * kb + 1) * 64 + lane] = xb;
+        }
+        {
+            float g[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int gi = 8 * h + m;                    // geo_feat index; 15 = padding
+                g[m] = gi < 15 ? a.geo_in[((size_t)ko * 16u + gi + 1) * N + ss] : 0.0f;
+            }
+            uint4 xa, xb;
+            to_operand<EXACT>(g, xa, xb);
+            Xw[16 * 64 + lane] = xa;
+            Xw[17 * 64 + lane] = xb;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = floatx16{};
+#pragma unroll
+        for (int kb = 0; kb < kL0kb; ++kb)
+            st.run8<EXACT>(acc, Xw[(2 * kb) * 64 + lane], Xw[(2 * kb + 1) * 64 + lane]);
+        epilogue<EXACT>(acc, a0, a1);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = floatx16{};
+#pragma unroll
+        for (int kb = 0; kb < kHkb; ++kb) st.run8<EXACT>(acc, a0[kb], a1[kb]);
+        epilogue<EXACT>(acc, a0, a1);
+        floatx16 o = {};
+        st.run1<EXACT>(o, a0, a1);
+        st.run1<EXACT>(o, a0 + 8, a1 + 8);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) sum[q] = __builtin_fmaf(w, o[q], sum[q]);
+    }
+    if (!live) return;
+    float* dst = a.out + (size_t)a.tiles(slot) * a.K;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const uint32_t u = (uint32_t)(rho(q) + 4 * h);
+        if (u < a.K) dst[u] = sum[q];
+    }
+}
+
+}  // namespace
+
+namespace samnerf {
+
+size_t mask_head_packed_floats() { return (size_t)kStepsPerSample * kStepVec * 4; }
+
+int mask_head_forward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
+                      const float* geo_f, uint32_t N, float* out, RayTiles tiles, float* packed,
+                      hipStream_t s) {
+    uint4* pk = reinterpret_cast<uint4*>(packed);
+    const uint32_t nfrag = (uint32_t)kStepsPerSample * 8u * 64u;
+    MaskArgs a;
+    a.grid = grid;
+    a.u_in = u_f;
+    a.w_in = w_f;
+    a.geo_in = geo_f;
+    a.N = N;
+    a.K = m->mask_out;
+    a.tiles = tiles;
+    a.packed = pk;
+    a.out = out;
+    if (m->head_mode == 1) {
+        k_mask_pack<true><<<div_up(nfrag, 256), 256, 0, s>>>(m->mask_w[0], m->mask_w[1], m->mask_w[2],
+                                                             m->mask_out, pk);
+        k_mask_head<true><<<div_up(N, (uint32_t)kSlots), 256, 0, s>>>(a);
+    } else {
+        k_mask_pack<false><<<div_up(nfrag, 256), 256, 0, s>>>(m->mask_w[0], m->mask_w[1], m->mask_w[2],
+                                                              m->mask_out, pk);
+        k_mask_head<false><<<div_up(N, (uint32_t)kSlots), 256, 0, s>>>(a);
+    }
+    return check_launch("mask_head");
+}
+
+}  // namespace samnerf

@@ -47,6 +47,10 @@ namespace samnerf {
 int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, float* samvit,
                      float* packed, hipStream_t s);
 size_t sam_head_packed_floats();
+int mask_head_forward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
+                      const float* geo_f, uint32_t N, float* out, RayTiles tiles, float* packed,
+                      hipStream_t s);
+size_t mask_head_packed_floats();
 }  // namespace samnerf
 
 namespace {
@@ -104,39 +108,6 @@ GridScale make_grid_scale(float bound) {
     const float m = std::frexp(g.b2, &e);                 // b2 = m * 2^e, m in [0.5, 1)
     g.inv_b2 = (m == 0.5f && std::isfinite(g.b2)) ? std::ldexp(1.0f, 1 - e) : 0.0f;
     return g;
-}
-
-// Ray tiling (samnerf_model.view_width).  The kernels work on ray SLOTS: a
-// wave of the proposal / s_grid kernels is 64 consecutive slots, a k_final
-// wave 32.  With the view's width W known, slot s is the ray of pixel
-// (x, y) of an 8 x 4 tile -- tile s / 32 in row-major tile order, pixel s % 32
-// row-major inside it -- so a wave's samples cover a compact patch of the
-// scene instead of a 32- or 64-pixel row segment: at fine levels the corner
-// boxes shrink and more gathers hit rows a neighbour already brought into L1
-// (tools/diag/tile_probe.py: 3.14 -> 2.97 ms per default-init view, final
-// 1.41 -> 1.20 ms on the opaque-sphere scene).  Per-sample intermediates
-// (near/far, bins, ds, u_f, w_f) live in slot order; the rays are read and the
-// per-ray outputs (image, depth, weights_sum, head rows) written at ray_of(s),
-// so callers see ray order.  w == 0: identity (W not a multiple of 8, or N not
-// a multiple of 4 W rows).
-struct RayTiles {
-    uint32_t w;      // view width in pixels (0: identity)
-    uint32_t tpr;    // tiles per tile row = w / 8
-    __device__ __forceinline__ uint32_t operator()(uint32_t s) const {
-        if (w == 0u) return s;
-        const uint32_t tile = s >> 5, in = s & 31u;
-        const uint32_t trow = tile / tpr, tcol = tile - trow * tpr;
-        return (trow * 4u + (in >> 3)) * w + tcol * 8u + (in & 7u);
-    }
-};
-
-RayTiles make_ray_tiles(uint32_t N, uint32_t W) {
-    RayTiles t{0u, 0u};
-    if (W >= 8u && W % 8u == 0u && N % (4u * W) == 0u) {
-        t.w = W;
-        t.tpr = W / 8u;
-    }
-    return t;
 }
 
 // MLP layer y = W x (torch layout W[out][in]), fma chain in input order.
@@ -463,6 +434,7 @@ struct FinalArgs {
     // -ln(t_thresh) past which a ray is opaque; a wave whose rays all are
     // stops marching.  INFINITY: off (the default, the reference's semantics).
     float exit_depth;
+    float* geo_out;    // GEO: [T][16][N] the grid_mlp output rows of every sample (mask head input)
 };
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -761,7 +733,9 @@ constexpr int final_waves() { return (S_ == 1 && !PF_ && !EXIT_) ? SAMNERF_DIAG_
 // the exit in the sample loop raised the 3-wave form's spills from 10 to 22
 // VGPRs (and cost the default kernel 0.80 -> 0.92 ms per view while it was a
 // run-time check in the one instantiation)
-template <int T, int S, bool PF, bool EXACT, bool EXIT = false>
+// GEO: also store every sample's grid_mlp output rows (geo_feat) for the
+// mask head (its own instantiation, only for renders of a mask model)
+template <int T, int S, bool PF, bool EXACT, bool EXIT = false, bool GEO = false>
 __global__ void __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(final_waves<S, PF, EXIT>(), final_waves<S, PF, EXIT>())))
 k_final(FinalArgs a) {
@@ -1004,6 +978,10 @@ k_final(FinalArgs a) {
         depth += (double)(w * t);
 #pragma unroll
         for (int q = 0; q < 8; ++q) fg[q] = fg[q] + w * o3[q];
+        if (GEO && live) {                               // rows rho(q) + 4 hh of this sample
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a.geo_out[((size_t)k * 16 + rho(q) + 4 * hh) * N + r] = o3[q];
+        }
         rb_prev = rb_next;
         // N1 early exit: once the transmittance of every ray of the wave is
         // below t_thresh, the samples left (whose weights sum to that
@@ -1538,6 +1516,8 @@ struct Workspace {
     float* w_f;
     float* rows;
     float* packed;
+    float* geo_f;      // [32][16][N] grid_mlp output rows per sample (with_mask)
+    float* mpacked;    // mask head weight stream (with_mask)
     size_t bytes;
 };
 
@@ -1617,6 +1597,12 @@ void launch_prop_sigma(int look, uint32_t N, hipStream_t s, const PropArgs& pa) 
 // grid_mlp of head_mode 1
 template <bool EXACT>
 void launch_final(int seg, bool pf, uint32_t N, hipStream_t s, const FinalArgs& fa) {
+    if (fa.geo_out) {                                    // mask model: geo_feat per sample
+        if (seg == 1) k_final<32, 1, false, EXACT, false, true><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
+        else if (seg == 2) k_final<32, 2, false, EXACT, false, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
+        else k_final<32, 4, false, EXACT, false, true><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
+        return;
+    }
     if (fa.exit_depth < INFINITY) {                      // N1 (no prefetch form)
         if (seg == 1) k_final<32, 1, false, EXACT, true><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
         else if (seg == 2) k_final<32, 2, false, EXACT, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
@@ -1653,6 +1639,8 @@ Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
     w.w_f = take((size_t)m->num_steps[2] * n);
     w.rows = take((size_t)kRow * n);
     w.packed = take(m->with_sam ? sam_head_packed_floats() : 0);
+    w.geo_f = take(m->with_mask ? (size_t)16 * m->num_steps[2] * n : 0);
+    w.mpacked = take(m->with_mask ? mask_head_packed_floats() : 0);
     w.bytes = off;
     return w;
 }
@@ -1876,6 +1864,11 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     if (!(m->t_thresh >= 0.0f && m->t_thresh < 1.0f))
         return fail(SAMNERF_EINVAL, "render_forward: t_thresh %g outside [0, 1)", (double)m->t_thresh);
     fa.exit_depth = m->t_thresh > 0.0f ? -logf(m->t_thresh) : INFINITY;
+    if (m->with_mask) {
+        if (m->t_thresh > 0.0f)
+            return fail(SAMNERF_EINVAL, "render_forward: the mask head and t_thresh do not combine");
+        fa.geo_out = w.geo_f;
+    }
     const bool sam_rows = m->with_sam && (samvit || feature_rows);
     fa.rows = sam_rows || feature_rows ? rows : nullptr;
     mark_stage(2, s);
@@ -1926,6 +1919,29 @@ int samnerf_set_taps(const samnerf_taps* taps, uint32_t N) {
     g_taps = taps ? *taps : samnerf_taps{};
     g_taps_n = taps ? N : 0u;
     return SAMNERF_OK;
+}
+
+int samnerf_mask_forward(const samnerf_model* m, uint32_t N, float* logits, const void* workspace,
+                         size_t workspace_bytes, samnerf_stream_t stream) {
+    if (!m) return fail(SAMNERF_EINVAL, "mask_forward: null model");
+    if (!m->with_mask) return fail(SAMNERF_EINVAL, "mask_forward: model has no mask head (with_mask = 0)");
+    if (N == 0) return SAMNERF_OK;
+    if (!logits || !workspace) return fail(SAMNERF_EINVAL, "mask_forward: null pointer");
+    if (m->mask_out < 1 || m->mask_out > 32)
+        return fail(SAMNERF_EINVAL, "mask_forward: mask_out %u outside 1..32", m->mask_out);
+    for (int i = 0; i < 3; ++i)
+        if (!m->mask_w[i]) return fail(SAMNERF_EINVAL, "mask_forward: null mask_mlp weight");
+    if (m->num_steps[2] != 32) return fail(SAMNERF_EINVAL, "mask_forward: fused path is built for 32 final samples");
+    Workspace w = carve(m, N, const_cast<void*>(workspace));
+    if (workspace_bytes < w.bytes)
+        return fail(SAMNERF_EWORKSPACE, "mask_forward: workspace needs %zu bytes, got %zu", w.bytes,
+                    workspace_bytes);
+    GridDesc<16> gm;
+    int rc = make_grid_desc(m->m_grid, 8, 16, gm, "m_grid");
+    if (rc) return rc;
+    const RayTiles tiles = g_taps_on ? RayTiles{0u, 0u} : make_ray_tiles(N, m->view_width);
+    return mask_head_forward(m, gm, w.u_f, w.w_f, w.geo_f, N, logits, tiles, w.mpacked,
+                             reinterpret_cast<hipStream_t>(stream));
 }
 
 int samnerf_sgrid_backward(const samnerf_model* m, const float* grad_fsam, uint32_t N,

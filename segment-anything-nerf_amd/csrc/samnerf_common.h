@@ -293,4 +293,37 @@ __device__ __forceinline__ void lookup_level3_ref(const float* __restrict__ emb,
     }
 }
 
+// Ray tiling (samnerf_model.view_width).  The kernels work on ray SLOTS: a
+// wave of the proposal / s_grid kernels is 64 consecutive slots, a k_final
+// wave 32.  With the view's width W known, slot s is the ray of pixel
+// (x, y) of an 8 x 4 tile -- tile s / 32 in row-major tile order, pixel s % 32
+// row-major inside it -- so a wave's samples cover a compact patch of the
+// scene instead of a 32- or 64-pixel row segment: at fine levels the corner
+// boxes shrink and more gathers hit rows a neighbour already brought into L1
+// (tools/diag/tile_probe.py: 3.14 -> 2.97 ms per default-init view, final
+// 1.41 -> 1.20 ms on the opaque-sphere scene).  Per-sample intermediates
+// (near/far, bins, ds, u_f, w_f) live in slot order; the rays are read and the
+// per-ray outputs (image, depth, weights_sum, head rows) written at ray_of(s),
+// so callers see ray order.  w == 0: identity (W not a multiple of 8, or N not
+// a multiple of 4 W rows).
+struct RayTiles {
+    uint32_t w;      // view width in pixels (0: identity)
+    uint32_t tpr;    // tiles per tile row = w / 8
+    __device__ __forceinline__ uint32_t operator()(uint32_t s) const {
+        if (w == 0u) return s;
+        const uint32_t tile = s >> 5, in = s & 31u;
+        const uint32_t trow = tile / tpr, tcol = tile - trow * tpr;
+        return (trow * 4u + (in >> 3)) * w + tcol * 8u + (in & 7u);
+    }
+};
+
+inline RayTiles make_ray_tiles(uint32_t N, uint32_t W) {
+    RayTiles t{0u, 0u};
+    if (W >= 8u && W % 8u == 0u && N % (4u * W) == 0u) {
+        t.w = W;
+        t.tpr = W / 8u;
+    }
+    return t;
+}
+
 }  // namespace samnerf

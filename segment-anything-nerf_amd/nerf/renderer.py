@@ -171,7 +171,11 @@ class NeRFRenderer(nn.Module):
         return results
 
     def _fused_ok(self, rays_o, perturb, return_mask, kwargs):
-        return (self.fused and rays_o.is_cuda and not perturb and not return_mask
+        if return_mask and not (getattr(self.opt, "with_mask", False)
+                                and self.opt.mask_mlp_type == "default"
+                                and self.mask_mlp[0].net[2].weight.shape[0] <= 32):
+            return False                     # the other mask heads: unfused path
+        return (self.fused and rays_o.is_cuda and not perturb
                 and not self.training and self.opt.background == "last_sample"
                 and not getattr(self.opt, "sum_after_mlp", False)
                 and list(self.opt.num_steps) == [128, 64, 32]
@@ -186,7 +190,7 @@ class NeRFRenderer(nn.Module):
             n = rays_o.shape[0]
             vw = W if (W is not None and n % W == 0) else 0      # a whole number of image rows
             out = self._fused.render(rays_o, rays_d, cam_near_far, bg_color,
-                                     feats=return_feats > 0, view_width=vw)
+                                     feats=return_feats > 0, view_width=vw, mask=return_mask > 0)
             samvit = out.pop("samvit", None)
             if return_feats > 0 and samvit is not None:
                 out["samvit"] = samvit.view(H, W, -1) if H is not None else samvit

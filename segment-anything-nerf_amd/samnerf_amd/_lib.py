@@ -35,7 +35,8 @@ class SamnerfModel(ctypes.Structure):
                 ("sam_w", _vp * 5), ("sam_b", _vp * 5), ("ln_w", _vp), ("ln_b", _vp),
                 ("with_sam", _int), ("aabb", _f32 * 6), ("grid_bound", _f32),
                 ("min_near", _f32), ("num_steps", _u32 * 3), ("head_mode", _int),
-                ("t_thresh", _f32), ("view_width", _u32)]
+                ("t_thresh", _f32), ("view_width", _u32),
+                ("with_mask", _int), ("m_grid", SamnerfGrid), ("mask_w", _vp * 3), ("mask_out", _u32)]
 
 
 _SIGS = {
@@ -64,6 +65,7 @@ _SIGS = {
                                 _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp], _int),
     "samnerf_sgrid_backward": ([ctypes.POINTER(SamnerfModel), _vp, _u32, _vp, _vp, _sz, _vp],
                                _int),
+    "samnerf_mask_forward": ([ctypes.POINTER(SamnerfModel), _u32, _vp, _vp, _sz, _vp], _int),
     "samnerf_tile_words": ([], _u32),
     "samnerf_tile_encode": ([_vp, _vp, _vp, _vp, _u32, _vp, _vp], _int),
     "samnerf_tile_decode": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp], _int),

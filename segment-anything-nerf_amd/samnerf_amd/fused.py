@@ -109,6 +109,13 @@ class FusedRenderer:
             m.num_steps[i] = int(v)
         m.head_mode = int(self.head_mode)
         m.t_thresh = float(self.t_thresh)
+        if self.fused_mask_ok():                        # --with_mask, mask_mlp_type 'default'
+            m.m_grid = self._grid(n.m_grid, "m_grid")
+            skip = n.mask_mlp[0]
+            for i in range(3):
+                m.mask_w[i] = _param(skip.net[i].weight, f"mask_mlp.0.net.{i}.weight")
+            m.mask_out = int(skip.net[2].weight.shape[0])
+        m.with_mask = 0                                 # set per call (render(mask=True))
         return m
 
     def workspace(self, m, N, device):
@@ -124,10 +131,19 @@ class FusedRenderer:
             ws = self._ws[key] = torch.empty(max(need, 1), dtype=torch.uint8, device=device)
         return ws, need
 
+    def fused_mask_ok(self):
+        """The mask heads the fused kernels run: mask_mlp_type 'default' (m_grid
+        L16C8 + SkipConnMLP 143->256->256->K) without sum_after_mlp, K <= 32."""
+        o = self.net.opt
+        return (getattr(o, "with_mask", False) and o.mask_mlp_type == "default"
+                and not getattr(o, "sum_after_mlp", False)
+                and self.net.mask_mlp[0].net[2].weight.shape[0] <= 32)
+
     # -------------------------------------------------------------- render --
     @torch.no_grad()
     def render(self, rays_o, rays_d, cam_near_far=None, bg_color=None, rows=None,
-               keep_workspace=False, feats=True, taps=False, own_workspace=False, view_width=0):
+               keep_workspace=False, feats=True, taps=False, own_workspace=False, view_width=0,
+               mask=False):
         """rays_o, rays_d [N,3] (CUDA fp32) -> dict(image [N,3], depth [N],
         weights_sum [N], samvit [N,256] if with_sam and feats).  `rows`
         (optional [N,164] tensor) receives the head input cat(f_sam, f_image,
@@ -142,13 +158,19 @@ class FusedRenderer:
         keep it (training: the backward reads its sample weights/positions).
         view_width: the rays are a row-major image of this width (a layout
         hint, samnerf_model.view_width): the kernels then run 8 x 4 pixel
-        tiles per wave, same outputs bit for bit, faster gathers."""
+        tiles per wave, same outputs bit for bit, faster gathers.
+        mask=True (a 'default' mask head, fused_mask_ok): also
+        instance_mask_logits [N, n_inst + redundant_instance]
+        (samnerf_mask_forward on the render's workspace)."""
         rays_o = rays_o.contiguous().float()
         rays_d = rays_d.contiguous().float()
         N = rays_o.shape[0]
         dev = rays_o.device
         m = self.model()
         m.view_width = 0 if taps else int(view_width or 0)
+        if mask and not self.fused_mask_ok():
+            raise NotImplementedError("fused render: only the 'default' mask head without sum_after_mlp")
+        m.with_mask = 1 if mask else 0
         if own_workspace:
             need = lib().samnerf_render_workspace_size(ctypes.byref(m), N)
             ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
@@ -189,10 +211,16 @@ class FusedRenderer:
                 ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, _ptr(cnf), n_cnf, bg, _ptr(image),
                 _ptr(depth), _ptr(wsum), _ptr(samvit), _ptr(rows), _ptr(ws), need, _stream(rays_o)),
                 "render_forward")
+            if mask:
+                logits = torch.empty(N, int(m.mask_out), device=dev)
+                check(lib().samnerf_mask_forward(ctypes.byref(m), N, _ptr(logits), _ptr(ws), need,
+                                                 _stream(rays_o)), "mask_forward")
         finally:
             if taps:
                 lib().samnerf_set_taps(None, 0)
         out = {"image": image, "depth": depth, "weights_sum": wsum}
+        if mask:
+            out["instance_mask_logits"] = logits
         if tap is not None:
             out.update({k: v.t() for k, v in tap.items()})
         if samvit is not None:
