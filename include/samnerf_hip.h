@@ -194,6 +194,9 @@ typedef struct {
     samnerf_grid m_grid;
     const float* mask_w[3];       /* [256,143] [256,256] [mask_out,256] */
     uint32_t mask_out;            /* n_inst + redundant_instance, 1..32 */
+    int sum_after_mlp;            /* --sum_after_mlp (renderer.py:339-342): image =
+                                     sigmoid(sum_k w_k view_mlp(colour_k)); RGB / mask models only
+                                     (with SAM features the reference crashes) */
 } samnerf_model;
 
 /* Bytes of device workspace samnerf_render_forward needs for N rays. */

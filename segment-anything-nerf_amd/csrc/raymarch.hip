@@ -726,18 +726,22 @@ __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const Leve
 #ifndef SAMNERF_DIAG_FINAL_WAVES
 #define SAMNERF_DIAG_FINAL_WAVES 3
 #endif
-template <int S_, bool PF_, bool EXIT_ = false>
-constexpr int final_waves() { return (S_ == 1 && !PF_ && !EXIT_) ? SAMNERF_DIAG_FINAL_WAVES : 2; }
+template <int S_, bool PF_, bool PLAIN_ = true>
+constexpr int final_waves() { return (S_ == 1 && !PF_ && PLAIN_) ? SAMNERF_DIAG_FINAL_WAVES : 2; }
 
 // EXIT: the N1 early-exit form, its own instantiation at 2 waves per SIMD:
 // the exit in the sample loop raised the 3-wave form's spills from 10 to 22
 // VGPRs (and cost the default kernel 0.80 -> 0.92 ms per view while it was a
 // run-time check in the one instantiation)
 // GEO: also store every sample's grid_mlp output rows (geo_feat) for the
-// mask head (its own instantiation, only for renders of a mask model)
-template <int T, int S, bool PF, bool EXACT, bool EXIT = false, bool GEO = false>
+// mask head (its own instantiation, only for renders of a mask model).
+// SA: --sum_after_mlp (renderer.py:339-342): the view MLP runs on every
+// sample's colour features, image = sigmoid(sum_k w_k view_mlp(colour_k)).
+// The EXIT / GEO / SA forms run at 2 waves per SIMD.
+template <int T, int S, bool PF, bool EXACT, bool EXIT = false, bool GEO = false, bool SA = false>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(final_waves<S, PF, EXIT>(), final_waves<S, PF, EXIT>())))
+__attribute__((amdgpu_waves_per_eu(final_waves<S, PF, !EXIT && !GEO && !SA>(),
+                                   final_waves<S, PF, !EXIT && !GEO && !SA>())))
 k_final(FinalArgs a) {
     static_assert(S == 1 || S == 2 || S == 4, "segments per ray");
     static_assert(kXSteps * 64 == 2 * kFSlots * 64 * 4, "exact weights reuse the bf16x3 slots");
@@ -792,6 +796,15 @@ k_final(FinalArgs a) {
     float fg[8];                                          // sum_k w_k * grid_mlp rows (acc layout)
 #pragma unroll
     for (int q = 0; q < 8; ++q) fg[q] = 0.0f;
+    float sh[16];                                         // SH(4) of the normalised direction
+    auto sh_of_ray = [&]() {
+        float dx = d[0], dy = d[1], dz = d[2];
+        normalize3(dx, dy, dz);
+        normalize3(dx, dy, dz);
+        sh_values<4>(dx, dy, dz, sh);
+    };
+    float rgb[3] = {0.0f, 0.0f, 0.0f};                    // SA: sum_k w_k * view_mlp(colour_k)
+    if constexpr (SA) sh_of_ray();
 
     // PF: the first k-block's gathers of sample i + 1 are issued before the
     // layer-2/3 MFMAs of sample i, so their latency hides behind them
@@ -982,6 +995,25 @@ k_final(FinalArgs a) {
 #pragma unroll
             for (int q = 0; q < 8; ++q) a.geo_out[((size_t)k * 16 + rho(q) + 4 * hh) * N + r] = o3[q];
         }
+        if constexpr (SA) {                              // view MLP on this sample's colour
+            floatx16 p1 = {};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) p1 = MFMA32(Vl[kV1 + q * 64 + lane], o3[q], p1);
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2) p1 = MFMA32(Vl[kV1 + (8 + s2) * 64 + lane], sh[2 * s2 + hh], p1);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) p1[q] = fmaxf(p1[q], 0.0f);
+            floatx16 p2 = {};
+#pragma unroll
+            for (int q = 0; q < 16; ++q) p2 = MFMA32(Vl[kV2 + q * 64 + lane], p1[q], p2);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) p2[q] = fmaxf(p2[q], 0.0f);
+            floatx16 p3 = {};
+#pragma unroll
+            for (int q = 0; q < 16; ++q) p3 = MFMA32(Vl[kV3 + q * 64 + lane], p2[q], p3);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) rgb[c] = rgb[c] + w * p3[c];   // rows 0..2, lower half
+        }
         rb_prev = rb_next;
         // N1 early exit: once the transmittance of every ray of the wave is
         // below t_thresh, the samples left (whose weights sum to that
@@ -1025,33 +1057,42 @@ k_final(FinalArgs a) {
         depth = pd;
 #pragma unroll
         for (int q = 0; q < 8; ++q) fg[q] = pf[q];
+        if constexpr (SA) {
+            float pr[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int s2 = 0; s2 < S; ++s2) {
+                const int src = (jj % R) + R * s2 + 32 * hh;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) pr[c] += __shfl(rgb[c], src);
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) rgb[c] = pr[c];
+        }
     }
 
     // view MLP on the accumulated colour features: rows 1..15 of fg are
     // f_image[0..14] (geo), f_image[15..30] = sh * sum(w) (colour = cat(geo, sh)
     // with sh constant along the ray, renderer.py:338; a rounding-level
     // reassociation of the reference's sum of products)
-    float dx = d[0], dy = d[1], dz = d[2];
-    normalize3(dx, dy, dz);
-    normalize3(dx, dy, dz);
-    float sh[16];
-    sh_values<4>(dx, dy, dz, sh);
+    if constexpr (!SA) sh_of_ray();
     const float ws = (float)wsum, dp = (float)depth;
-    floatx16 v1 = {};
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v1 = MFMA32(Vl[kV1 + q * 64 + lane], fg[q], v1);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) v1 = MFMA32(Vl[kV1 + (8 + s) * 64 + lane], sh[2 * s + hh] * ws, v1);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v1[i] = fmaxf(v1[i], 0.0f);
-    floatx16 v2 = {};
-#pragma unroll
-    for (int q = 0; q < 16; ++q) v2 = MFMA32(Vl[kV2 + q * 64 + lane], v1[q], v2);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v2[i] = fmaxf(v2[i], 0.0f);
     floatx16 v3 = {};
+    if constexpr (!SA) {
+        floatx16 v1 = {};
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v3 = MFMA32(Vl[kV3 + q * 64 + lane], v2[q], v3);
+        for (int q = 0; q < 8; ++q) v1 = MFMA32(Vl[kV1 + q * 64 + lane], fg[q], v1);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) v1 = MFMA32(Vl[kV1 + (8 + s) * 64 + lane], sh[2 * s + hh] * ws, v1);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v1[i] = fmaxf(v1[i], 0.0f);
+        floatx16 v2 = {};
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v2 = MFMA32(Vl[kV2 + q * 64 + lane], v1[q], v2);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v2[i] = fmaxf(v2[i], 0.0f);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v3 = MFMA32(Vl[kV3 + q * 64 + lane], v2[q], v3);
+    }
 
     if (!live || seg != 0) return;
     const uint32_t ray = a.tiles(r);                     // per-ray outputs in ray order
@@ -1067,7 +1108,7 @@ k_final(FinalArgs a) {
     float img[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {                // rows 0..2 of v3 = registers 0..2, lower half
-        img[c] = sigmoidf(v3[c]) + (1.0f - ws) * a.bg;
+        img[c] = sigmoidf(SA ? rgb[c] : v3[c]) + (1.0f - ws) * a.bg;
         a.image[(size_t)ray * 3 + c] = img[c];
     }
     a.depth[ray] = dp;
@@ -1594,19 +1635,27 @@ void launch_prop_sigma(int look, uint32_t N, hipStream_t s, const PropArgs& pa) 
 }
 
 // k_final by ray-segment form S and prefetch; EXACT = the exact-fp32
-// grid_mlp of head_mode 1
+// grid_mlp of head_mode 1.  The non-prefetching forms by segment count:
+template <bool EXACT, bool EXIT, bool GEO, bool SA>
+void launch_final_np(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa) {
+    if (seg == 1) k_final<32, 1, false, EXACT, EXIT, GEO, SA><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
+    else if (seg == 2) k_final<32, 2, false, EXACT, EXIT, GEO, SA><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
+    else k_final<32, 4, false, EXACT, EXIT, GEO, SA><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
+}
+
 template <bool EXACT>
-void launch_final(int seg, bool pf, uint32_t N, hipStream_t s, const FinalArgs& fa) {
+void launch_final(int seg, bool pf, uint32_t N, hipStream_t s, const FinalArgs& fa, bool sa) {
+    if (sa) {                                            // --sum_after_mlp (RGB / mask models)
+        if (fa.geo_out) launch_final_np<EXACT, false, true, true>(seg, N, s, fa);
+        else launch_final_np<EXACT, false, false, true>(seg, N, s, fa);
+        return;
+    }
     if (fa.geo_out) {                                    // mask model: geo_feat per sample
-        if (seg == 1) k_final<32, 1, false, EXACT, false, true><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
-        else if (seg == 2) k_final<32, 2, false, EXACT, false, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
-        else k_final<32, 4, false, EXACT, false, true><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
+        launch_final_np<EXACT, false, true, false>(seg, N, s, fa);
         return;
     }
     if (fa.exit_depth < INFINITY) {                      // N1 (no prefetch form)
-        if (seg == 1) k_final<32, 1, false, EXACT, true><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
-        else if (seg == 2) k_final<32, 2, false, EXACT, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
-        else k_final<32, 4, false, EXACT, true><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
+        launch_final_np<EXACT, true, false, false>(seg, N, s, fa);
         return;
     }
     if (seg == 1) {
@@ -1877,8 +1926,11 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     const char* fs = getenv("SAMNERF_FINAL_S");
     const int seg = fs ? atoi(fs) : (N >= 65536u ? 1 : N >= 32768u ? 2 : 4);
     const bool pf = final_prefetch(seg);
-    if (m->head_mode == 1) launch_final<true>(seg, pf, N, s, fa);
-    else launch_final<false>(seg, pf, N, s, fa);
+    if (m->sum_after_mlp && (m->t_thresh > 0.0f || sam_rows))
+        return fail(SAMNERF_EINVAL, "render_forward: sum_after_mlp renders RGB (+ mask) only: no SAM "
+                    "features (the reference's branch crashes, SURVEY 0.2) and no t_thresh");
+    if (m->head_mode == 1) launch_final<true>(seg, pf, N, s, fa, m->sum_after_mlp != 0);
+    else launch_final<false>(seg, pf, N, s, fa, m->sum_after_mlp != 0);
 
     if (sam_rows) {
         SgridArgs sa{};

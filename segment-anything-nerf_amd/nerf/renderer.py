@@ -177,7 +177,9 @@ class NeRFRenderer(nn.Module):
             return False                     # the other mask heads: unfused path
         return (self.fused and rays_o.is_cuda and not perturb
                 and not self.training and self.opt.background == "last_sample"
-                and not getattr(self.opt, "sum_after_mlp", False)
+                # sum_after_mlp: RGB (+ mask) models on the fused path; with SAM
+                # the reference's branch crashes and run_torch raises
+                and not (getattr(self.opt, "sum_after_mlp", False) and self.opt.with_sam)
                 and list(self.opt.num_steps) == [128, 64, 32]
                 and (not self.opt.with_sam or self.opt.sam_use_view_direction))
 

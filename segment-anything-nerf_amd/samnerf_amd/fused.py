@@ -116,6 +116,7 @@ class FusedRenderer:
                 m.mask_w[i] = _param(skip.net[i].weight, f"mask_mlp.0.net.{i}.weight")
             m.mask_out = int(skip.net[2].weight.shape[0])
         m.with_mask = 0                                 # set per call (render(mask=True))
+        m.sum_after_mlp = int(bool(getattr(opt, "sum_after_mlp", False)))
         return m
 
     def workspace(self, m, N, device):
@@ -133,10 +134,9 @@ class FusedRenderer:
 
     def fused_mask_ok(self):
         """The mask heads the fused kernels run: mask_mlp_type 'default' (m_grid
-        L16C8 + SkipConnMLP 143->256->256->K) without sum_after_mlp, K <= 32."""
+        L16C8 + SkipConnMLP 143->256->256->K), K <= 32."""
         o = self.net.opt
         return (getattr(o, "with_mask", False) and o.mask_mlp_type == "default"
-                and not getattr(o, "sum_after_mlp", False)
                 and self.net.mask_mlp[0].net[2].weight.shape[0] <= 32)
 
     # -------------------------------------------------------------- render --
@@ -169,7 +169,7 @@ class FusedRenderer:
         m = self.model()
         m.view_width = 0 if taps else int(view_width or 0)
         if mask and not self.fused_mask_ok():
-            raise NotImplementedError("fused render: only the 'default' mask head without sum_after_mlp")
+            raise NotImplementedError("fused render: only the 'default' mask head")
         m.with_mask = 1 if mask else 0
         if own_workspace:
             need = lib().samnerf_render_workspace_size(ctypes.byref(m), N)

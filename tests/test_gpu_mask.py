@@ -56,13 +56,15 @@ def test_mask_training_reduces_loss(hip_lib, cuda):
 
 
 @pytest.mark.parametrize("head_mode", [0, 1])
-def test_fused_mask_head_matches_reference_golden(hip_lib, cuda, monkeypatch, head_mode):
-    """The 'default' mask head (m_grid L16C8 + SkipConnMLP 143->256->256->K,
-    no sum_after_mlp) on the fused kernels: render(..., return_mask=1) takes
-    k_final<GEO> + k_mask_head (mask_head.hip) and matches the reference's own
-    golden within 1e-3, in both precision modes."""
+@pytest.mark.parametrize("name", ["render_mask_default_nosum", "render_mask_default"])
+def test_fused_mask_head_matches_reference_golden(hip_lib, cuda, monkeypatch, name, head_mode):
+    """The 'default' mask head (m_grid L16C8 + SkipConnMLP 143->256->256->K) on
+    the fused kernels: render(..., return_mask=1) takes k_final<GEO> (+ SA for
+    the sum_after_mlp fixture: the view MLP per sample) + k_mask_head
+    (mask_head.hip) and matches the reference's own golden within 1e-3, in
+    both precision modes."""
     monkeypatch.setenv("SAMNERF_HEAD_MODE", str(head_mode))
-    fx = np.load(os.path.join(GOLDEN, "render_mask_default_nosum.npz"))
+    fx = np.load(os.path.join(GOLDEN, name + ".npz"))
     spec = spec_from_fixture(fx)
     net = make_net(spec, fixture_params(fx, spec), cuda)
     ro = torch.from_numpy(fx["rays_o"]).to(cuda)
@@ -99,3 +101,23 @@ def test_fused_mask_head_matches_unfused_path(hip_lib, cuda, head_mode):
     assert got.shape == (64 * 64, 5)
     assert err < 1e-3 * max(1.0, scale), (err, scale)
     assert torch.equal(got, tiled)
+
+
+def test_fused_sum_after_mlp_rgb_matches_unfused(hip_lib, cuda, monkeypatch):
+    """--sum_after_mlp on an RGB model (image = sigmoid(sum_k w_k
+    view_mlp(colour_k)), renderer.py:339-342) on the fused k_final<SA> against
+    the unfused op sequence, all segment forms (S = 1 / 2 / 4 by ray count)."""
+    from samnerf_amd import ops
+    spec = synth.ModelSpec(with_sam=False, sum_after_mlp=True)
+    net = make_net(spec, synth.make_params(spec, seed=14, emb_scale=0.5), cuda)
+    pose, intr = synth.gui_camera(64, 64, rot=synth.random_rotation(5))
+    ro, rd = ops.get_rays(pose, intr, 64, 64, device=cuda)
+    with torch.no_grad():
+        ref = net.run_torch(ro, rd)
+        for seg, n in ((1, 4096), (2, 4096), (4, 1000)):
+            monkeypatch.setenv("SAMNERF_FINAL_S", str(seg))
+            out = net.run(ro[:n], rd[:n])
+            assert net._fused is not None
+            for k in ("image", "weights_sum"):
+                err = (out[k] - ref[k][:n]).abs().max().item()
+                assert err < 1e-3, (seg, n, k, err)
