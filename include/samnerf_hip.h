@@ -186,14 +186,20 @@ typedef struct {
                                      8 x 4 pixel tiles (compact wave footprints, better gather
                                      locality); outputs stay in ray order and are bit-identical.
                                      samnerf_sgrid_backward must see the value of the forward. */
-    /* --with_mask, mask_mlp_type 'default' (network.py:125-133, renderer.py:392-395,
-     * :451-452): m_grid L16 C8 and SkipConnMLP(143 -> 256 -> 256 -> mask_out, bias=False,
-     * leaky_relu); with_mask = 0 when the model has no such head.  Rendered by
-     * samnerf_mask_forward after samnerf_render_forward. */
+    /* --with_mask instance heads (network.py:125-203, renderer.py:392-452), rendered by
+     * samnerf_mask_forward after a samnerf_render_forward with with_mask = 1 (0: no mask
+     * outputs, nothing extra computed).  mask_kind 0 = 'default': m_grid L16 C8 and
+     * SkipConnMLP(143 -> 256 -> 256 -> mask_out, bias=False, leaky_relu), mask_w[0..2]
+     * = [256,143] [256,256] [mask_out,256]; 1 = 'adaptive' / 'density': six bias-free
+     * Linears on the grid_mlp intermediates, mask_w[0..5] = [96,32] [96,160] [96,160]
+     * [96,112] [96,96] [mask_out,96]; 2 = 'adaptive' / 'rgb' (needs sum_after_mlp):
+     * eight, also on the view_mlp intermediates, mask_w[0..7] = [96,32] [96,160]
+     * [96,160] [96,112] [96,128] [96,128] [96,96] [mask_out,96]. */
     int with_mask;
-    samnerf_grid m_grid;
-    const float* mask_w[3];       /* [256,143] [256,256] [mask_out,256] */
-    uint32_t mask_out;            /* n_inst + redundant_instance, 1..32 */
+    int mask_kind;
+    samnerf_grid m_grid;          /* mask_kind 0 */
+    const float* mask_w[8];
+    uint32_t mask_out;            /* n_inst (+ redundant_instance for 'default'), 1..32 */
     int sum_after_mlp;            /* --sum_after_mlp (renderer.py:339-342): image =
                                      sigmoid(sum_k w_k view_mlp(colour_k)); RGB / mask models only
                                      (with SAM features the reference crashes) */

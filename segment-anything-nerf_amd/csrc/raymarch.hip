@@ -435,7 +435,14 @@ struct FinalArgs {
     // stops marching.  INFINITY: off (the default, the reference's semantics).
     float exit_depth;
     float* geo_out;    // GEO: [T][16][N] the grid_mlp output rows of every sample (mask head input)
+    // AD (adaptive mask heads): the head is linear in the per-sample grid
+    // features and MLP intermediates, so sum_k w_k head(x_k) = E . sum_k w_k x_k
+    const float* aeff; // [K][240] E, blocks g 32 | h1 64 | h2 64 | o3 16 | v1 32 | v2 32 (k_mask_eff)
+    float* mlog;       // [N][K] instance_mask_logits (ray order)
+    uint32_t mask_out;
 };
+
+constexpr int kAeff = 240;          // columns of the adaptive heads' effective matrix
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -737,12 +744,20 @@ constexpr int final_waves() { return (S_ == 1 && !PF_ && PLAIN_) ? SAMNERF_DIAG_
 // mask head (its own instantiation, only for renders of a mask model).
 // SA: --sum_after_mlp (renderer.py:339-342): the view MLP runs on every
 // sample's colour features, image = sigmoid(sum_k w_k view_mlp(colour_k)).
-// The EXIT / GEO / SA forms run at 2 waves per SIMD.
-template <int T, int S, bool PF, bool EXACT, bool EXIT = false, bool GEO = false, bool SA = false>
+// AD: the adaptive mask heads (1 'density', 2 'rgb', S = 1 only): per-ray
+// weighted sums of the grid features and the grid_mlp (and, SA, view_mlp)
+// intermediates, then instance_mask_logits = E . sums (the head is linear).
+// The EXIT / GEO / SA forms run at 2 waves per SIMD, the AD forms at 1.
+template <int S_, bool PF_, bool PLAIN_, int AD_>
+constexpr int final_waves_of() { return AD_ ? 1 : final_waves<S_, PF_, PLAIN_>(); }
+
+template <int T, int S, bool PF, bool EXACT, bool EXIT = false, bool GEO = false, bool SA = false, int AD = 0>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(final_waves<S, PF, !EXIT && !GEO && !SA>(),
-                                   final_waves<S, PF, !EXIT && !GEO && !SA>())))
+__attribute__((amdgpu_waves_per_eu(final_waves_of<S, PF, !EXIT && !GEO && !SA, AD>(),
+                                   final_waves_of<S, PF, !EXIT && !GEO && !SA, AD>())))
 k_final(FinalArgs a) {
+    static_assert(AD == 0 || (S == 1 && !PF), "adaptive mask forms: one segment, no prefetch");
+    static_assert(AD != 2 || SA, "the 'rgb' adaptive head reads the per-sample view MLP (sum_after_mlp)");
     static_assert(S == 1 || S == 2 || S == 4, "segments per ray");
     static_assert(kXSteps * 64 == 2 * kFSlots * 64 * 4, "exact weights reuse the bf16x3 slots");
     constexpr int R = 32 / S, TS = T / S;
@@ -805,6 +820,19 @@ k_final(FinalArgs a) {
     };
     float rgb[3] = {0.0f, 0.0f, 0.0f};                    // SA: sum_k w_k * view_mlp(colour_k)
     if constexpr (SA) sh_of_ray();
+    // AD: sum_k w_k x_k of the adaptive heads' inputs, this lane's components
+    float gacc[AD ? 16 : 1], h1acc[AD ? 32 : 1], h2acc[AD ? 32 : 1], v1acc[AD == 2 ? 16 : 1],
+        v2acc[AD == 2 ? 16 : 1];
+    if constexpr (AD > 0) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) gacc[q] = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 32; ++q) h1acc[q] = h2acc[q] = 0.0f;
+    }
+    if constexpr (AD == 2) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v1acc[q] = v2acc[q] = 0.0f;
+    }
 
     // PF: the first k-block's gathers of sample i + 1 are issued before the
     // layer-2/3 MFMAs of sample i, so their latency hides behind them
@@ -882,6 +910,7 @@ k_final(FinalArgs a) {
         const float* FX = Fx + wo;
 
         floatx16 h1a = {}, h1b = {};
+        float fk[AD ? 16 : 1];                           // AD: this sample's grid features (by k-block)
 #pragma unroll
         for (int kbi = 0; kbi < 2; ++kbi) {
             const int kb = kbi == 0 ? kPre : 1 - kPre;
@@ -892,6 +921,10 @@ k_final(FinalArgs a) {
                 LevelDesc dl[4];
                 levels(kb, dl);
                 gather_levels_c2<4, S == 1>(emb, dl, ux, uy, uz, f, kinds(kb));
+            }
+            if constexpr (AD > 0) {
+#pragma unroll
+                for (int m = 0; m < 8; ++m) fk[kb * 8 + m] = f[m];
             }
             if constexpr (EXACT) {
 #pragma unroll
@@ -991,6 +1024,17 @@ k_final(FinalArgs a) {
         depth += (double)(w * t);
 #pragma unroll
         for (int q = 0; q < 8; ++q) fg[q] = fg[q] + w * o3[q];
+        if constexpr (AD > 0) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) gacc[m] = gacc[m] + w * fk[m];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                h1acc[q] = h1acc[q] + w * h1a[q];
+                h1acc[16 + q] = h1acc[16 + q] + w * h1b[q];
+                h2acc[q] = h2acc[q] + w * h2a[q];
+                h2acc[16 + q] = h2acc[16 + q] + w * h2b[q];
+            }
+        }
         if (GEO && live) {                               // rows rho(q) + 4 hh of this sample
 #pragma unroll
             for (int q = 0; q < 8; ++q) a.geo_out[((size_t)k * 16 + rho(q) + 4 * hh) * N + r] = o3[q];
@@ -1013,6 +1057,13 @@ k_final(FinalArgs a) {
             for (int q = 0; q < 16; ++q) p3 = MFMA32(Vl[kV3 + q * 64 + lane], p2[q], p3);
 #pragma unroll
             for (int c = 0; c < 3; ++c) rgb[c] = rgb[c] + w * p3[c];   // rows 0..2, lower half
+            if constexpr (AD == 2) {                     // view_mlp intermediates (post-ReLU)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    v1acc[q] = v1acc[q] + w * p1[q];
+                    v2acc[q] = v2acc[q] + w * p2[q];
+                }
+            }
         }
         rb_prev = rb_next;
         // N1 early exit: once the transmittance of every ray of the wave is
@@ -1094,6 +1145,29 @@ k_final(FinalArgs a) {
         for (int q = 0; q < 16; ++q) v3 = MFMA32(Vl[kV3 + q * 64 + lane], v2[q], v3);
     }
 
+    if constexpr (AD > 0) {
+        // instance_mask_logits[c] = E[c] . sums: this lane's components, then
+        // the other half-wave's (lane ^ 32 holds the ray's other rows)
+        const uint32_t K = a.mask_out;
+        for (uint32_t c = 0; c < K; ++c) {
+            const float* E = a.aeff + (size_t)c * kAeff;
+            float sacc = 0.0f;
+#pragma unroll
+            for (int m = 0; m < 16; ++m)
+                sacc += E[2 * final_level(m >> 3, hh, (m & 7) >> 1) + (m & 1)] * gacc[m];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int u = rho(q) + 4 * hh;
+                sacc += E[32 + u] * h1acc[q] + E[64 + u] * h1acc[16 + q];
+                sacc += E[96 + u] * h2acc[q] + E[128 + u] * h2acc[16 + q];
+                if constexpr (AD == 2) sacc += E[176 + u] * v1acc[q] + E[208 + u] * v2acc[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sacc += E[160 + rho(q) + 4 * hh] * fg[q];
+            sacc += __shfl_xor(sacc, 32);
+            if (live && hh == 0) a.mlog[(size_t)a.tiles(r) * K + c] = sacc;
+        }
+    }
     if (!live || seg != 0) return;
     const uint32_t ray = a.tiles(r);                     // per-ray outputs in ray order
     float* row = a.rows ? a.rows + (size_t)ray * kRow : nullptr;
@@ -1557,8 +1631,10 @@ struct Workspace {
     float* w_f;
     float* rows;
     float* packed;
-    float* geo_f;      // [32][16][N] grid_mlp output rows per sample (with_mask)
-    float* mpacked;    // mask head weight stream (with_mask)
+    float* geo_f;      // [32][16][N] grid_mlp output rows per sample (with_mask, kind 0)
+    float* mpacked;    // mask head weight stream (with_mask, kind 0)
+    float* aeff;       // [K][240] adaptive heads' effective matrix (with_mask, kinds 1-2)
+    float* mlog;       // [N][K] adaptive heads' logits (with_mask, kinds 1-2)
     size_t bytes;
 };
 
@@ -1634,6 +1710,61 @@ void launch_prop_sigma(int look, uint32_t N, hipStream_t s, const PropArgs& pa) 
     else k_prop_sigma<T, FIRST, kLookPacked><<<nb, 256, 0, s>>>(pa);
 }
 
+// The adaptive mask heads (network.py:143-191, renderer.py:399-434) are
+// chains of bias-free Linears on concatenations [intermediate ; m]: linear in
+// the per-sample inputs, so sum_k w_k head(x_k) = E . sum_k w_k x_k with E the
+// product of the chain, K x 240 (blocks g 32 | h1 64 | h2 64 | o3 16 | v1 32 |
+// v2 32).  One block multiplies it out from the output layer back:
+// P = W_last W_prev, then per concatenating layer [A | B]: E_block = P A,
+// P = P B.  (A reassociation of the reference's layer-by-layer products:
+// rounding-level differences.)
+struct EffArgs {
+    const float* w[8];
+    uint32_t K;
+    int kind;          // 1 density (6 layers), 2 rgb (8 layers)
+    float* aeff;
+};
+
+__global__ void __launch_bounds__(256) k_mask_eff(EffArgs a) {
+    __shared__ float P[2][32 * 96];
+    const int tid = threadIdx.x;
+    const int K = (int)a.K, nl = a.kind == 2 ? 8 : 6;
+    int cur = 0;
+    for (int e = tid; e < K * 96; e += 256) P[0][e] = a.w[nl - 1][e];
+    __syncthreads();
+    // out[r][c] = sum_i P[r][i] W[i][c0 + c] (W: 96 rows of `ld` columns)
+    auto mul = [&](const float* W, int ld, int c0, int nc, float* out, int out_ld) {
+        for (int e = tid; e < K * nc; e += 256) {
+            const int r = e / nc, c = e % nc;
+            float acc = 0.0f;
+            for (int i = 0; i < 96; ++i) acc = __builtin_fmaf(P[cur][r * 96 + i], W[i * ld + c0 + c], acc);
+            out[r * out_ld + c] = acc;
+        }
+        __syncthreads();
+    };
+    auto next = [&](const float* W, int ld, int c0) {
+        mul(W, ld, c0, 96, P[cur ^ 1], 96);
+        cur ^= 1;
+    };
+    float* E = a.aeff;
+    next(a.w[nl - 2], 96, 0);                            // P = W_last W_{last-1}
+    if (a.kind == 2) {
+        mul(a.w[5], 128, 0, 32, E + 208, kAeff);         // [v2 | m4]
+        next(a.w[5], 128, 32);
+        mul(a.w[4], 128, 0, 32, E + 176, kAeff);         // [v1 | m3]
+        next(a.w[4], 128, 32);
+    } else {
+        for (int e = tid; e < K * 64; e += 256) E[(e / 64) * kAeff + 176 + e % 64] = 0.0f;
+    }
+    mul(a.w[3], 112, 0, 16, E + 160, kAeff);             // [o3 | m2]
+    next(a.w[3], 112, 16);
+    mul(a.w[2], 160, 0, 64, E + 96, kAeff);              // [h2 | m1]
+    next(a.w[2], 160, 64);
+    mul(a.w[1], 160, 0, 64, E + 32, kAeff);              // [h1 | m0]
+    next(a.w[1], 160, 64);
+    mul(a.w[0], 32, 0, 32, E, kAeff);                    // m0 = W0 g
+}
+
 // k_final by ray-segment form S and prefetch; EXACT = the exact-fp32
 // grid_mlp of head_mode 1.  The non-prefetching forms by segment count:
 template <bool EXACT, bool EXIT, bool GEO, bool SA>
@@ -1644,7 +1775,14 @@ void launch_final_np(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa) {
 }
 
 template <bool EXACT>
-void launch_final(int seg, bool pf, uint32_t N, hipStream_t s, const FinalArgs& fa, bool sa) {
+void launch_final(int seg, bool pf, uint32_t N, hipStream_t s, const FinalArgs& fa, bool sa, int ad) {
+    if (ad) {                                            // adaptive mask heads: S = 1
+        const uint32_t nb = xcd_blocks(div_up(N, 128));
+        if (ad == 2) k_final<32, 1, false, EXACT, false, false, true, 2><<<nb, 256, 0, s>>>(fa);
+        else if (sa) k_final<32, 1, false, EXACT, false, false, true, 1><<<nb, 256, 0, s>>>(fa);
+        else k_final<32, 1, false, EXACT, false, false, false, 1><<<nb, 256, 0, s>>>(fa);
+        return;
+    }
     if (sa) {                                            // --sum_after_mlp (RGB / mask models)
         if (fa.geo_out) launch_final_np<EXACT, false, true, true>(seg, N, s, fa);
         else launch_final_np<EXACT, false, false, true>(seg, N, s, fa);
@@ -1688,8 +1826,11 @@ Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
     w.w_f = take((size_t)m->num_steps[2] * n);
     w.rows = take((size_t)kRow * n);
     w.packed = take(m->with_sam ? sam_head_packed_floats() : 0);
-    w.geo_f = take(m->with_mask ? (size_t)16 * m->num_steps[2] * n : 0);
-    w.mpacked = take(m->with_mask ? mask_head_packed_floats() : 0);
+    const bool mdef = m->with_mask && m->mask_kind == 0, madapt = m->with_mask && m->mask_kind > 0;
+    w.geo_f = take(mdef ? (size_t)16 * m->num_steps[2] * n : 0);
+    w.mpacked = take(mdef ? mask_head_packed_floats() : 0);
+    w.aeff = take(madapt ? (size_t)32 * kAeff : 0);
+    w.mlog = take(madapt ? (size_t)m->mask_out * n : 0);
     w.bytes = off;
     return w;
 }
@@ -1913,10 +2054,33 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     if (!(m->t_thresh >= 0.0f && m->t_thresh < 1.0f))
         return fail(SAMNERF_EINVAL, "render_forward: t_thresh %g outside [0, 1)", (double)m->t_thresh);
     fa.exit_depth = m->t_thresh > 0.0f ? -logf(m->t_thresh) : INFINITY;
+    int ad = 0;
     if (m->with_mask) {
         if (m->t_thresh > 0.0f)
             return fail(SAMNERF_EINVAL, "render_forward: the mask head and t_thresh do not combine");
-        fa.geo_out = w.geo_f;
+        if (m->mask_kind < 0 || m->mask_kind > 2)
+            return fail(SAMNERF_EINVAL, "render_forward: mask_kind %d", m->mask_kind);
+        if (m->mask_out < 1 || m->mask_out > 32)
+            return fail(SAMNERF_EINVAL, "render_forward: mask_out %u outside 1..32", m->mask_out);
+        const int nl = m->mask_kind == 0 ? 3 : m->mask_kind == 1 ? 6 : 8;
+        for (int i = 0; i < nl; ++i)
+            if (!m->mask_w[i]) return fail(SAMNERF_EINVAL, "render_forward: null mask_mlp weight %d", i);
+        if (m->mask_kind == 0) {
+            fa.geo_out = w.geo_f;
+        } else {
+            if (m->mask_kind == 2 && !m->sum_after_mlp)
+                return fail(SAMNERF_EINVAL, "render_forward: the adaptive 'rgb' head needs sum_after_mlp");
+            EffArgs ea{};
+            for (int i = 0; i < nl; ++i) ea.w[i] = m->mask_w[i];
+            ea.K = m->mask_out;
+            ea.kind = m->mask_kind;
+            ea.aeff = w.aeff;
+            k_mask_eff<<<1, 256, 0, s>>>(ea);
+            fa.aeff = w.aeff;
+            fa.mlog = w.mlog;
+            fa.mask_out = m->mask_out;
+            ad = m->mask_kind;
+        }
     }
     const bool sam_rows = m->with_sam && (samvit || feature_rows);
     fa.rows = sam_rows || feature_rows ? rows : nullptr;
@@ -1929,8 +2093,8 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     if (m->sum_after_mlp && (m->t_thresh > 0.0f || sam_rows))
         return fail(SAMNERF_EINVAL, "render_forward: sum_after_mlp renders RGB (+ mask) only: no SAM "
                     "features (the reference's branch crashes, SURVEY 0.2) and no t_thresh");
-    if (m->head_mode == 1) launch_final<true>(seg, pf, N, s, fa, m->sum_after_mlp != 0);
-    else launch_final<false>(seg, pf, N, s, fa, m->sum_after_mlp != 0);
+    if (m->head_mode == 1) launch_final<true>(seg, pf, N, s, fa, m->sum_after_mlp != 0, ad);
+    else launch_final<false>(seg, pf, N, s, fa, m->sum_after_mlp != 0, ad);
 
     if (sam_rows) {
         SgridArgs sa{};
@@ -1981,13 +2145,19 @@ int samnerf_mask_forward(const samnerf_model* m, uint32_t N, float* logits, cons
     if (!logits || !workspace) return fail(SAMNERF_EINVAL, "mask_forward: null pointer");
     if (m->mask_out < 1 || m->mask_out > 32)
         return fail(SAMNERF_EINVAL, "mask_forward: mask_out %u outside 1..32", m->mask_out);
-    for (int i = 0; i < 3; ++i)
-        if (!m->mask_w[i]) return fail(SAMNERF_EINVAL, "mask_forward: null mask_mlp weight");
     if (m->num_steps[2] != 32) return fail(SAMNERF_EINVAL, "mask_forward: fused path is built for 32 final samples");
     Workspace w = carve(m, N, const_cast<void*>(workspace));
     if (workspace_bytes < w.bytes)
         return fail(SAMNERF_EWORKSPACE, "mask_forward: workspace needs %zu bytes, got %zu", w.bytes,
                     workspace_bytes);
+    if (m->mask_kind != 0) {                            // adaptive: k_final wrote them
+        if (hipMemcpyAsync(logits, w.mlog, sizeof(float) * m->mask_out * (size_t)N, hipMemcpyDeviceToDevice,
+                           reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
+            return fail(SAMNERF_ELAUNCH, "mask_forward: copy failed");
+        return SAMNERF_OK;
+    }
+    for (int i = 0; i < 3; ++i)
+        if (!m->mask_w[i]) return fail(SAMNERF_EINVAL, "mask_forward: null mask_mlp weight");
     GridDesc<16> gm;
     int rc = make_grid_desc(m->m_grid, 8, 16, gm, "m_grid");
     if (rc) return rc;

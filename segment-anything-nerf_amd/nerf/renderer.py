@@ -171,10 +171,10 @@ class NeRFRenderer(nn.Module):
         return results
 
     def _fused_ok(self, rays_o, perturb, return_mask, kwargs):
-        if return_mask and not (getattr(self.opt, "with_mask", False)
-                                and self.opt.mask_mlp_type == "default"
-                                and self.mask_mlp[0].net[2].weight.shape[0] <= 32):
-            return False                     # the other mask heads: unfused path
+        if return_mask:
+            from samnerf_amd.fused import mask_kind
+            if mask_kind(self) is None:
+                return False                 # the other mask heads: unfused path
         return (self.fused and rays_o.is_cuda and not perturb
                 and not self.training and self.opt.background == "last_sample"
                 # sum_after_mlp: RGB (+ mask) models on the fused path; with SAM

@@ -36,7 +36,8 @@ class SamnerfModel(ctypes.Structure):
                 ("with_sam", _int), ("aabb", _f32 * 6), ("grid_bound", _f32),
                 ("min_near", _f32), ("num_steps", _u32 * 3), ("head_mode", _int),
                 ("t_thresh", _f32), ("view_width", _u32),
-                ("with_mask", _int), ("m_grid", SamnerfGrid), ("mask_w", _vp * 3), ("mask_out", _u32),
+                ("with_mask", _int), ("mask_kind", _int), ("m_grid", SamnerfGrid), ("mask_w", _vp * 8),
+                ("mask_out", _u32),
                 ("sum_after_mlp", _int)]
 
 

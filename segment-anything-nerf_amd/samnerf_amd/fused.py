@@ -24,6 +24,25 @@ def _param(t, name):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def mask_kind(net):
+    """The fused kernels' mask_kind for the network's --with_mask head, or None
+    when it runs on the unfused path: 0 'default' (K <= 32), 1 'adaptive' /
+    'density', 2 'adaptive' / 'rgb' with sum_after_mlp (without it the
+    reference's view_mlp intermediates are per ray and its cat fails); the
+    'lightweight_mask' and adaptive 'sam' heads raise in the reference."""
+    o = net.opt
+    if not getattr(o, "with_mask", False):
+        return None
+    if o.mask_mlp_type == "default":
+        return 0 if net.mask_mlp[0].net[2].weight.shape[0] <= 32 else None
+    if o.mask_mlp_type == "adaptive" and net.mask_mlp[-1].weight.shape[0] <= 32:
+        if o.adaptive_mlp_type == "density":
+            return 1
+        if o.adaptive_mlp_type == "rgb" and getattr(o, "sum_after_mlp", False):
+            return 2
+    return None
+
+
 class FusedRenderer:
     """head_mode: 0 = bf16x3 split precision for grid_mlp and the SAM head
     (default), 1 = exact fp32.  t_thresh: 0 (default) = the reference's
@@ -109,12 +128,18 @@ class FusedRenderer:
             m.num_steps[i] = int(v)
         m.head_mode = int(self.head_mode)
         m.t_thresh = float(self.t_thresh)
-        if self.fused_mask_ok():                        # --with_mask, mask_mlp_type 'default'
+        kind = mask_kind(n)
+        if kind == 0:                                   # --with_mask, mask_mlp_type 'default'
             m.m_grid = self._grid(n.m_grid, "m_grid")
             skip = n.mask_mlp[0]
             for i in range(3):
                 m.mask_w[i] = _param(skip.net[i].weight, f"mask_mlp.0.net.{i}.weight")
             m.mask_out = int(skip.net[2].weight.shape[0])
+        elif kind is not None:                          # 'adaptive': density / rgb
+            for i, lin in enumerate(n.mask_mlp):
+                m.mask_w[i] = _param(lin.weight, f"mask_mlp.{i}.weight")
+            m.mask_out = int(n.mask_mlp[-1].weight.shape[0])
+        m.mask_kind = kind or 0
         m.with_mask = 0                                 # set per call (render(mask=True))
         m.sum_after_mlp = int(bool(getattr(opt, "sum_after_mlp", False)))
         return m
@@ -133,11 +158,8 @@ class FusedRenderer:
         return ws, need
 
     def fused_mask_ok(self):
-        """The mask heads the fused kernels run: mask_mlp_type 'default' (m_grid
-        L16C8 + SkipConnMLP 143->256->256->K), K <= 32."""
-        o = self.net.opt
-        return (getattr(o, "with_mask", False) and o.mask_mlp_type == "default"
-                and self.net.mask_mlp[0].net[2].weight.shape[0] <= 32)
+        """The network's mask head runs on the fused kernels (mask_kind)."""
+        return mask_kind(self.net) is not None
 
     # -------------------------------------------------------------- render --
     @torch.no_grad()
@@ -169,7 +191,7 @@ class FusedRenderer:
         m = self.model()
         m.view_width = 0 if taps else int(view_width or 0)
         if mask and not self.fused_mask_ok():
-            raise NotImplementedError("fused render: only the 'default' mask head")
+            raise NotImplementedError("fused render: this mask head runs on the unfused path")
         m.with_mask = 1 if mask else 0
         if own_workspace:
             need = lib().samnerf_render_workspace_size(ctypes.byref(m), N)

@@ -121,3 +121,44 @@ def test_fused_sum_after_mlp_rgb_matches_unfused(hip_lib, cuda, monkeypatch):
             for k in ("image", "weights_sum"):
                 err = (out[k] - ref[k][:n]).abs().max().item()
                 assert err < 1e-3, (seg, n, k, err)
+
+
+@pytest.mark.parametrize("name", ["render_mask_adaptive_density", "render_mask_adaptive_rgb"])
+def test_fused_adaptive_mask_heads_match_reference_golden(hip_lib, cuda, name):
+    """The 'adaptive' heads (bias-free Linear chains on the grid_mlp / view_mlp
+    intermediates) on the fused path: k_final<..., AD> accumulates the
+    weighted per-sample inputs, k_mask_eff multiplies the chain out; the
+    reference's goldens within 1e-3 (both fixtures use sum_after_mlp)."""
+    fx = np.load(os.path.join(GOLDEN, name + ".npz"))
+    spec = spec_from_fixture(fx)
+    net = make_net(spec, fixture_params(fx, spec), cuda)
+    ro = torch.from_numpy(fx["rays_o"]).to(cuda)
+    rd = torch.from_numpy(fx["rays_d"]).to(cuda)
+    with torch.no_grad():
+        out = net.render(ro, rd, staged=False, return_mask=1)
+    assert net._fused is not None and net._fused.fused_mask_ok()
+    for k in ("image", "weights_sum", "instance_mask_logits"):
+        err = (out[k].cpu() - torch.from_numpy(fx[k])).abs().max().item()
+        print(name, k, err)
+        assert err < 1e-3, (k, err)
+
+
+@pytest.mark.parametrize("sum_after", [False, True])
+def test_fused_adaptive_density_matches_unfused_path(hip_lib, cuda, sum_after):
+    """Adaptive 'density' head at full table size, with and without
+    sum_after_mlp, against the unfused op sequence on a 64 x 64 view."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer
+    spec = synth.ModelSpec(with_sam=False, with_mask=True, mask_type="adaptive", adaptive_type="density",
+                           n_inst=4, sum_after_mlp=sum_after)
+    net = make_net(spec, synth.make_params(spec, seed=13, emb_scale=0.5), cuda)
+    pose, intr = synth.gui_camera(64, 64, rot=synth.random_rotation(9))
+    ro, rd = ops.get_rays(pose, intr, 64, 64, device=cuda)
+    with torch.no_grad():
+        ref = net.run_torch(ro, rd, return_mask=1)
+        got = FusedRenderer(net).render(ro, rd, mask=True, view_width=64)
+    for k in ("image", "instance_mask_logits"):
+        err = (got[k] - ref[k]).abs().max().item()
+        scale = ref[k].abs().max().item()
+        print("adaptive density", sum_after, k, err, scale)
+        assert err < 1e-3 * max(1.0, scale), (k, err, scale)
