@@ -192,8 +192,13 @@ struct MaskStepper {
             f0[t] = cur[t * 64];
             f1[t] = cur[512 + t * 64];
         }
+#ifdef SAMNERF_DIAG_MASK_NOMFMA
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t][0] += __uint_as_float(f0[t].x ^ f1[t].y ^ b0.x ^ b1.w);
+#else
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] = kblock<EXACT>(f0[t], f1[t], b0, b1, acc[t]);
+#endif
         finish();
     }
 
@@ -270,7 +275,12 @@ k_mask_head(MaskArgs a) {
         for (int kb = 0; kb < 8; ++kb) {
             float f[8];
             const LevelDesc d = sLv[2 * kb + h];
+#ifdef SAMNERF_DIAG_MASK_NOGATHER
+#pragma unroll
+            for (int m = 0; m < 8; ++m) f[m] = ux * (float)(m + 1) + d.fres * uy;
+#else
             lookup_level3<8>(a.grid.emb, d, ux, uy, uz, f);
+#endif
             uint4 xa, xb;
             to_operand<EXACT>(f, xa, xb);
             Xw[(2 * kb) * 64 + lane] = xa;
