@@ -319,6 +319,9 @@ __global__ void __launch_bounds__(256) k_snf(PropArgs a) {
 // values and the same interpolation as one walk over the whole ray, so the
 // indices and bins are identical, with a quarter of the dependent steps.
 template <int T, int TN, bool FIRST>
+__device__ __forceinline__ void prop_pdf_phases(const PropArgs& a, float* sw, uint32_t r0, uint32_t nr);
+
+template <int T, int TN, bool FIRST>
 __global__ void __launch_bounds__(256) k_prop_pdf(PropArgs a) {
     constexpr int SW = T + 1;                 // T + 1 cdf entries per row (odd stride)
     __shared__ float sw[64 * SW];
@@ -343,6 +346,16 @@ __global__ void __launch_bounds__(256) k_prop_pdf(PropArgs a) {
         for (int k = 0; k < TQ; ++k) row[part * TQ + k] = v[k];
     }
     __syncthreads();
+    prop_pdf_phases<T, TN, FIRST>(a, sw, r0, nr);
+}
+
+// Phases A and B of the proposal pdf over 64 rays whose ds rows sit in LDS
+// (row stride T + 1); every thread of the block calls it after a barrier.
+template <int T, int TN, bool FIRST>
+__device__ __forceinline__ void prop_pdf_phases(const PropArgs& a, float* sw, uint32_t r0, uint32_t nr) {
+    constexpr int SW = T + 1;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, part = tid >> 6, N = a.N;
+    float* row = sw + lane * SW;
     if (part == 0 && lane < nr) {
         // unrolled by 8: the LDS reads run ahead of the double-precision
         // chains (a full unroll takes 248 VGPRs and halves occupancy)
@@ -393,6 +406,61 @@ __global__ void __launch_bounds__(256) k_prop_pdf(PropArgs a) {
         a.bins_out[(size_t)j * N + r] = b0 + t * (b1 - b0);
         if (a.inds_out) a.inds_out[(size_t)j * N + r] = i;    // torch.searchsorted(cdf, u, right=True)
     }
+}
+
+// The proposal stage in one kernel (round 2, DESIGN.md 5 "intermediates"): a
+// block owns 64 ray slots and all T samples -- wave w evaluates samples w,
+// w + 4, .. of its 64 rays (each ray's origin, direction and near/far loaded
+// once, not once per sample) and writes ds into the LDS rows k_prop_pdf
+// staged from HBM -- then the same pdf phases.  ds ([T][N], 134 MB per 512^2
+// view at T = 128) never leaves the CU.  Bit-identical to the two-kernel form
+// but 1.9x slower (prop0 1.10 vs 0.59 ms): 33 KB of LDS and 125 VGPRs per
+// block leave 4 waves per SIMD instead of k_prop_sigma's 8 to hide the gather
+// latency, and the serial pdf phase holds the block's slots while 3 of its 4
+// waves wait at the barrier.  A selectable variant (SAMNERF_PROP_FUSED=1).
+template <int T, int TN, bool FIRST>
+__global__ void __launch_bounds__(256) k_prop_fused(PropArgs a) {
+    constexpr int SW = T + 1;
+    __shared__ float sw[64 * SW];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, part = tid >> 6;
+    const uint32_t r0 = xcd_chunk(blockIdx.x, (a.N + 63u) / 64u) * 64u, N = a.N;
+    if (r0 >= N) return;
+    const uint32_t nr = min(64u, N - r0);
+    if (lane < nr) {
+        const uint32_t r = r0 + lane, ray = a.tiles(r);
+        float o[3], d[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            o[c] = a.rays_o[(size_t)ray * 3 + c];
+            d[c] = a.rays_d[(size_t)ray * 3 + c];
+        }
+        const float sn = a.snf[r], sf = a.snf[N + r];
+        float* row = sw + lane * SW;
+#pragma unroll 2
+        for (int kk = 0; kk < T / 4; ++kk) {
+            const int k = (int)part + 4 * kk;
+            float b0, b1;
+            if constexpr (FIRST) {
+                b0 = a.bins0(k);
+                b1 = a.bins0(k + 1);
+            } else {
+                b0 = a.bins_in[(size_t)k * N + r];
+                b1 = a.bins_in[(size_t)(k + 1) * N + r];
+            }
+            const float rb_prev = real_bin(sn, sf, b0), rb_next = real_bin(sn, sf, b1);
+            const float t = (rb_next + rb_prev) / 2.0f;
+            float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
+            contract3(x, y, z);
+            float feat[10];
+            grid_features<5, 2, false>(a.grid, a.gs(x), a.gs(y), a.gs(z), feat);
+            float h[16], sv;
+            dense_pk<16, 10, true>(a.W0, feat, h);
+            dense<1, 16, false>(a.W1, h, &sv);
+            row[k] = (rb_next - rb_prev) * expf(sv);      // trunc_exp forward
+        }
+    }
+    __syncthreads();
+    prop_pdf_phases<T, TN, FIRST>(a, sw, r0, nr);
 }
 
 struct FinalArgs {
@@ -2000,8 +2068,17 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     const int look = lookup_mode();
     mark_stage(0, s);
     k_snf<<<div_up(N, 256), 256, 0, s>>>(pa);
-    launch_prop_sigma<128, true>(look, N, s, pa);
-    k_prop_pdf<128, 65, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
+    // SAMNERF_PROP_FUSED=1: one kernel per proposal stage, ds kept in LDS
+    // (k_prop_fused; bit-identical, but measured 1.9x slower -- prop0 1.10 vs
+    // 0.59 ms per view -- so the two-kernel form stays the default)
+    const char* pfv = getenv("SAMNERF_PROP_FUSED");
+    const bool pfused = !g_taps_on && look == kLookAuto && pfv && pfv[0] == '1';
+    if (pfused) {
+        k_prop_fused<128, 65, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
+    } else {
+        launch_prop_sigma<128, true>(look, N, s, pa);
+        k_prop_pdf<128, 65, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
+    }
 
     // stage 1: 64 samples -> 33 bins
     pa.grid = gp1;
@@ -2014,8 +2091,12 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.inds_out = tp.inds2;
     pa.w_out = tp.w1;
     mark_stage(1, s);
-    launch_prop_sigma<64, false>(look, N, s, pa);
-    k_prop_pdf<64, 33, false><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
+    if (pfused) {
+        k_prop_fused<64, 33, false><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
+    } else {
+        launch_prop_sigma<64, false>(look, N, s, pa);
+        k_prop_pdf<64, 33, false><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
+    }
 
     // stage 2: 32 samples through the full network
     FinalArgs fa{};

@@ -457,3 +457,27 @@ def test_ray_tiling_bit_identical(hip_lib, cuda, surface):
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
         assert torch.equal(outs[0][k][:H * W - 2 * W], outs[2][k]), k
+
+
+def test_fused_proposal_kernel_bit_identical(hip_lib, cuda, monkeypatch):
+    """k_prop_fused (ds kept in LDS, one kernel per proposal stage; the
+    SAMNERF_PROP_FUSED=1 variant, measured slower) against the default
+    two-kernel form k_prop_sigma + k_prop_pdf: every output, head rows
+    included, bit for bit, at a full-view-like and a ragged ray count."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer
+    spec = synth.ModelSpec(with_sam=True)
+    net = make_net(spec, synth.make_params(spec, seed=31, emb_scale=0.5, ln_jitter=0.1), cuda)
+    pose, intr = synth.gui_camera(256, 256, rot=synth.random_rotation(3))
+    ro, rd = ops.get_rays(pose, intr, 256, 256, device=cuda)
+    fr = FusedRenderer(net)
+    for n in (256 * 256, 9001):
+        outs = []
+        for flag in ("1", "0"):
+            monkeypatch.setenv("SAMNERF_PROP_FUSED", flag)
+            rows = torch.empty(n, 164, device=cuda)
+            o = fr.render(ro[:n], rd[:n], rows=rows)
+            o["rows"] = rows
+            outs.append({k: v.cpu() for k, v in o.items()})
+        for k in outs[0]:
+            assert torch.equal(outs[0][k], outs[1][k]), (n, k)
