@@ -20,7 +20,7 @@
 // Orientation and weight stream are k_sam_head_bf3's (sam_head.hip):
 // out^T[256 units x 32 rays] = W . act^T, 8 accumulator tiles per wave whose
 // registers are the next layer's B operands, weights in 16 KiB steps through
-// a 3-deep LDS ring by direct DMA, shared by the 4 waves.  27 steps per sample:
+// a 4-deep LDS ring by direct DMA, shared by the 4 waves.  27 steps per sample:
 // layer 0 (9 k-blocks x 8 tiles), layer 1 (16 x 8), layer 2 (16 k-blocks x
 // the one output tile, 8 per step).  The weighted sum over samples stays in
 // the output tile's registers.
@@ -49,6 +49,22 @@ constexpr int kStepsPerSample = kL0kb + kHkb + 2;   // 27
 constexpr int kStepVec = 2 * 8 * 64;          // uint4 per step
 constexpr int kSlots = 128;                   // ray slots per workgroup
 constexpr int kT = 32;                        // final samples per ray
+// weight ring depth (LDS steps); the DMA runs kRing - 1 steps ahead.  4
+// (137 KB of LDS with the operand stage): 8.92 -> 8.35 ms per 512^2 view
+// against 3; the stream alone (no gathers, no MFMAs) is the same at both
+// depths, 9.2 ms -- a DMA throughput limit (~1.15 us per 16 KiB step per CU),
+// not its latency
+#ifndef SAMNERF_MASK_RING
+#define SAMNERF_MASK_RING 4
+#endif
+constexpr uint32_t kRing = SAMNERF_MASK_RING;
+#define MASK_STR2(x) #x
+#define MASK_STR(x) MASK_STR2(x)
+#define MASK_VMCNT_AHEAD "s_waitcnt vmcnt(" MASK_STR(SAMNERF_MASK_VMCNT) ")"
+#ifndef SAMNERF_MASK_VMCNT
+#define SAMNERF_MASK_VMCNT 8                          // 4 DMA instructions per step x (kRing - 2)
+#endif
+static_assert(SAMNERF_MASK_VMCNT == 4 * (SAMNERF_MASK_RING - 2), "vmcnt of the ring depth");
 
 __device__ __forceinline__ int rho(int q) { return (q & 3) + 8 * (q >> 2); }
 __device__ __forceinline__ int hidden_unit(int kb, int h, int m) {
@@ -147,7 +163,7 @@ struct MaskArgs {
 };
 
 // The weight stream of sam_head.hip's HeadStepper (DMA from inline asm into a
-// 3-step LDS ring, two steps ahead, counted vmcnt): the gathers issued at the
+// kRing-step LDS ring, kRing - 1 steps ahead, counted vmcnt): the gathers issued at the
 // start of each sample are ordinary loads younger or older than the DMAs, and
 // either way only make those counted waits wait longer.
 struct MaskStepper {
@@ -158,8 +174,11 @@ struct MaskStepper {
     uint32_t total;
 
     __device__ __forceinline__ void issue(uint32_t s) {
+#ifdef SAMNERF_DIAG_MASK_NODMA
+        return;
+#endif
         const uint4* src = packed + (size_t)(s % kStepsPerSample) * kStepVec + wave * 256 + lane;
-        const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(Wb + (s % 3u) * kStepVec + wave * 256);
+        const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(Wb + (s % kRing) * kStepVec + wave * 256);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const uint32_t d = __builtin_amdgcn_readfirstlane(dst + c * 1024u);
@@ -174,18 +193,20 @@ struct MaskStepper {
     }
 
     __device__ __forceinline__ void finish() {
-        if (step + 2 < total) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // step + 1 landed
+        if (step + kRing - 1 < total) asm volatile(MASK_VMCNT_AHEAD ::: "memory");   // step + 1 landed
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef SAMNERF_DIAG_MASK_NOBARRIER
         __builtin_amdgcn_s_barrier();
+#endif
         ++step;
     }
 
     // one k-block for all 8 output tiles
     template <bool EXACT>
     __device__ __forceinline__ void run8(floatx16 (&acc)[8], const uint4& b0, const uint4& b1) {
-        if (step + 2 < total) issue(step + 2);
-        const uint4* cur = Wb + (step % 3u) * kStepVec + lane;
+        if (step + kRing - 1 < total) issue(step + kRing - 1);
+        const uint4* cur = Wb + (step % kRing) * kStepVec + lane;
         uint4 f0[8], f1[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -205,8 +226,8 @@ struct MaskStepper {
     // eight k-blocks of the one output tile
     template <bool EXACT>
     __device__ __forceinline__ void run1(floatx16& acc, const uint4* b0, const uint4* b1) {
-        if (step + 2 < total) issue(step + 2);
-        const uint4* cur = Wb + (step % 3u) * kStepVec + lane;
+        if (step + kRing - 1 < total) issue(step + kRing - 1);
+        const uint4* cur = Wb + (step % kRing) * kStepVec + lane;
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc = kblock<EXACT>(cur[k * 64], cur[512 + k * 64], b0[k], b1[k], acc);
         finish();
@@ -235,26 +256,26 @@ constexpr int kDescVec = (16 * (int)sizeof(LevelDesc) + 15) / 16;
 template <bool EXACT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_mask_head(MaskArgs a) {
-    // one LDS object: the 3-step weight ring | each wave's layer-0 B operands
+    // one LDS object: the kRing-step weight ring | each wave's layer-0 B operands
     // of the current sample (the gathers land there, not in 72 VGPRs that
     // would live through layer 0 next to the accumulators, fragments and
     // activations: with them the kernel spilled ~350 registers) | the m_grid
     // level descriptors (read per lane: a select between two kernel-argument
     // descriptors became per-lane loads from the kernarg segment)
-    __shared__ uint4 smem[3 * kStepVec + 4 * kXVec + kDescVec];
+    __shared__ uint4 smem[kRing * kStepVec + 4 * kXVec + kDescVec];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int j = lane & 31, h = lane >> 5;
     const uint32_t slot = blockIdx.x * kSlots + wave * 32u + j;
     const bool live = slot < a.N;
     const uint32_t ss = live ? slot : a.N - 1u, N = a.N;
-    uint4* const Xw = smem + 3 * kStepVec + wave * kXVec;
-    LevelDesc* const sLv = reinterpret_cast<LevelDesc*>(smem + 3 * kStepVec + 4 * kXVec);
+    uint4* const Xw = smem + kRing * kStepVec + wave * kXVec;
+    LevelDesc* const sLv = reinterpret_cast<LevelDesc*>(smem + kRing * kStepVec + 4 * kXVec);
     if (tid < 16) sLv[tid] = a.grid.lv[tid];
 
     MaskStepper st{a.packed, smem, wave, lane, 0u, (uint32_t)kT * kStepsPerSample};
-    st.issue(0);
-    st.issue(1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");          // step 0 landed
+#pragma unroll
+    for (uint32_t i = 0; i + 1 < kRing; ++i) st.issue(i);
+    asm volatile(MASK_VMCNT_AHEAD ::: "memory");              // step 0 landed
     __syncthreads();
 
     floatx16 sum = {};                                       // sum_k w_k * logits_k

@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp
-for v in product mask_nogather mask_nomfma mask_neither; do
+for v in ${VARIANTS:-product mask_nogather mask_nomfma mask_neither}; do
   if [ $v = product ]; then L=""; else L="$GRAFT_REPO_ROOT/tools/diag/lib/$v.so"; fi
   SAMNERF_LIB=$L timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_r2y_$v" -o m -- python3 -c "
 import sys, torch
