@@ -481,3 +481,61 @@ def test_fused_proposal_kernel_bit_identical(hip_lib, cuda, monkeypatch):
             outs.append({k: v.cpu() for k, v in o.items()})
         for k in outs[0]:
             assert torch.equal(outs[0][k], outs[1][k]), (n, k)
+
+
+def _twice_equal(render):
+    a = {k: v.cpu() for k, v in render().items()}
+    b = {k: v.cpu() for k, v in render().items()}
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("seg", ["1", "2", "4"])
+@pytest.mark.parametrize("pf", ["0", "1"])
+@pytest.mark.parametrize("head_mode", [0, 1])
+def test_final_forms_deterministic(hip_lib, cuda, monkeypatch, seg, pf, head_mode):
+    """Every k_final form renders the same bits twice (a forward
+    whose output varies run to run has a hazard): S = 1 / 2 / 4, with and
+    without the cross-sample prefetch, both precisions, feature rows on."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer, ROW
+    monkeypatch.setenv("SAMNERF_FINAL_S", seg)
+    monkeypatch.setenv("SAMNERF_FINAL_PF", pf)
+    spec = synth.ModelSpec(with_sam=True)
+    net = make_net(spec, synth.make_params(spec, seed=23, emb_scale=0.5, ln_jitter=0.1), cuda)
+    pose, intr = synth.gui_camera(512, 80, rot=synth.random_rotation(11))
+    ro, rd = ops.get_rays(pose, intr, 80, 512, device=cuda)
+    fr = FusedRenderer(net, head_mode=head_mode)
+    rows = torch.empty(ro.shape[0], ROW, device=cuda)
+
+    def render():
+        o = fr.render(ro, rd, rows=rows, view_width=512)
+        o["rows"] = rows.clone()
+        return o
+    _twice_equal(render)
+
+
+@pytest.mark.parametrize("form", ["exit", "mask_default", "sum_after", "adaptive_density", "adaptive_rgb"])
+def test_final_mode_forms_deterministic(hip_lib, cuda, form):
+    """The EXIT (N1), GEO (+ k_mask_head), SA and AD instantiations of k_final
+    (and the mask kernels after them) render the same bits twice."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer
+    kw, mask, t = {}, False, 0.0
+    if form == "exit":
+        spec = synth.ModelSpec(with_sam=True)
+        params = synth.make_surface_params(spec, seed=3)
+        t = 1e-3
+    else:
+        kw = {"mask_default": dict(mask_type="default"),
+              "sum_after": dict(mask_type="default", sum_after_mlp=True),
+              "adaptive_density": dict(mask_type="adaptive", adaptive_type="density"),
+              "adaptive_rgb": dict(mask_type="adaptive", adaptive_type="rgb", sum_after_mlp=True)}[form]
+        spec = synth.ModelSpec(with_sam=False, with_mask=True, **kw)
+        params = synth.make_params(spec, seed=17, emb_scale=0.5)
+        mask = True
+    net = make_net(spec, params, cuda)
+    pose, intr = synth.gui_camera(256, 128, rot=synth.random_rotation(2))
+    ro, rd = ops.get_rays(pose, intr, 128, 256, device=cuda)
+    fr = FusedRenderer(net, t_thresh=t)
+    _twice_equal(lambda: fr.render(ro, rd, mask=mask, view_width=256))
