@@ -25,6 +25,11 @@
 // the one output tile, 8 per step).  The weighted sum over samples stays in
 // the output tile's registers.
 //
+// Weight stream (round 2): first through LDS-DMA like the SAM head (3-, then
+// 4-deep ring), measured DMA-throughput-bound; now staged through VGPRs by
+// ordinary loads (MaskStager, 392 VGPRs, no spills): 512^2 mask view 10.1 ->
+// 8.75 ms.
+//
 // Precision (head_mode): 0 = bf16x3 split precision (3 bf16 MFMAs per 16-deep
 // k-block, ~1e-5 relative); 1 = exact fp32 (8 v_mfma_f32_32x32x2_f32 per
 // k-block, the step holds the fp32 weights in the same 32 B per lane and
@@ -234,6 +239,78 @@ struct MaskStepper {
     }
 };
 
+// SAMNERF_MASK_STAGE=1: the weight stream through VGPRs instead of LDS-DMA.
+// Steps go in groups of kGroup: the block's 256 threads load the next group
+// (kGroup x 16 KiB, four 16-B loads per thread and step) at the start of a
+// group, write it to the other half of a 2-group LDS ring after the group's
+// MFMAs, then one barrier per group.  Ordinary loads and stores whose waits
+// the compiler places itself.
+#ifndef SAMNERF_MASK_STAGE
+#define SAMNERF_MASK_STAGE 1
+#endif
+#ifndef SAMNERF_MASK_GROUP
+#define SAMNERF_MASK_GROUP 1          // 2: 512 VGPRs and 52-93 spilled (vs 392, none)
+#endif
+constexpr uint32_t kGroup = SAMNERF_MASK_GROUP;
+struct MaskStager {
+    const uint4* __restrict__ packed;
+    uint4* Wb;            // [2][kGroup][kStepVec]
+    int tid, lane;
+    uint32_t step;
+    uint32_t total;
+    uint4 stg[4 * kGroup];
+
+    __device__ __forceinline__ void load(uint32_t g) {          // group g = steps g kGroup ..
+#pragma unroll
+        for (uint32_t i = 0; i < kGroup; ++i) {
+            const uint32_t s = g * kGroup + i;
+            const uint4* src = packed + (size_t)(s % kStepsPerSample) * kStepVec + tid;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) stg[4 * i + c] = s < total ? src[c * 256] : make_uint4(0, 0, 0, 0);
+        }
+    }
+    __device__ __forceinline__ void store(uint32_t g) {
+        uint4* dst = Wb + (size_t)(g & 1u) * kGroup * kStepVec + tid;
+#pragma unroll
+        for (uint32_t i = 0; i < kGroup; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) dst[i * kStepVec + c * 256] = stg[4 * i + c];
+    }
+    __device__ __forceinline__ void begin() {
+        load(0);
+        store(0);
+        __syncthreads();
+    }
+    __device__ __forceinline__ const uint4* start() {
+        const uint32_t g = step / kGroup, i = step % kGroup;
+        if (i == 0 && (g + 1) * kGroup < total) load(g + 1);
+        return Wb + ((size_t)(g & 1u) * kGroup + i) * kStepVec + lane;
+    }
+    __device__ __forceinline__ void finish() {
+        const uint32_t g = step / kGroup, i = step % kGroup;
+        if (i == kGroup - 1 || step + 1 == total) {
+            if ((g + 1) * kGroup < total) store(g + 1);
+            __syncthreads();
+        }
+        ++step;
+    }
+
+    template <bool EXACT>
+    __device__ __forceinline__ void run8(floatx16 (&acc)[8], const uint4& b0, const uint4& b1) {
+        const uint4* cur = start();
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = kblock<EXACT>(cur[t * 64], cur[512 + t * 64], b0, b1, acc[t]);
+        finish();
+    }
+    template <bool EXACT>
+    __device__ __forceinline__ void run1(floatx16& acc, const uint4* b0, const uint4* b1) {
+        const uint4* cur = start();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = kblock<EXACT>(cur[k * 64], cur[512 + k * 64], b0[k], b1[k], acc);
+        finish();
+    }
+};
+
 __device__ __forceinline__ float leaky(float x) { return x < 0.0f ? x * 0.01f : x; }
 
 // leaky_relu on the accumulators, then the next layer's B operands (k-block
@@ -262,21 +339,27 @@ k_mask_head(MaskArgs a) {
     // activations: with them the kernel spilled ~350 registers) | the m_grid
     // level descriptors (read per lane: a select between two kernel-argument
     // descriptors became per-lane loads from the kernarg segment)
-    __shared__ uint4 smem[kRing * kStepVec + 4 * kXVec + kDescVec];
+    constexpr uint32_t kRingUsed = SAMNERF_MASK_STAGE ? 2u * kGroup : kRing;
+    __shared__ uint4 smem[kRingUsed * kStepVec + 4 * kXVec + kDescVec];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int j = lane & 31, h = lane >> 5;
     const uint32_t slot = blockIdx.x * kSlots + wave * 32u + j;
     const bool live = slot < a.N;
     const uint32_t ss = live ? slot : a.N - 1u, N = a.N;
-    uint4* const Xw = smem + kRing * kStepVec + wave * kXVec;
-    LevelDesc* const sLv = reinterpret_cast<LevelDesc*>(smem + kRing * kStepVec + 4 * kXVec);
+    uint4* const Xw = smem + kRingUsed * kStepVec + wave * kXVec;
+    LevelDesc* const sLv = reinterpret_cast<LevelDesc*>(smem + kRingUsed * kStepVec + 4 * kXVec);
     if (tid < 16) sLv[tid] = a.grid.lv[tid];
 
+#if SAMNERF_MASK_STAGE
+    MaskStager st{a.packed, smem, tid, lane, 0u, (uint32_t)kT * kStepsPerSample, {}};
+    st.begin();
+#else
     MaskStepper st{a.packed, smem, wave, lane, 0u, (uint32_t)kT * kStepsPerSample};
 #pragma unroll
     for (uint32_t i = 0; i + 1 < kRing; ++i) st.issue(i);
     asm volatile(MASK_VMCNT_AHEAD ::: "memory");              // step 0 landed
     __syncthreads();
+#endif
 
     floatx16 sum = {};                                       // sum_k w_k * logits_k
     floatx16 acc[8];
