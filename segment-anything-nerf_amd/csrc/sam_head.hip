@@ -371,6 +371,50 @@ struct HeadStepper {
     }
 };
 
+// SAMNERF_HEAD_STAGE=1: the same stream staged through VGPRs by ordinary
+// loads (mask_head.hip's MaskStager): each thread loads its four 16-B pieces
+// of step s + 1 at the start of step s and writes them to the other half of a
+// 2-step LDS ring after step s's MFMAs, then the barrier.  500 VGPRs, no
+// spills, but slower here: 0.58 -> 0.82 ms per view (one step of lookahead
+// exposes the load latency before the store; the DMA runs two steps ahead
+// without registers).  The mask head, whose DMA form spilled, gains from it.
+#ifndef SAMNERF_HEAD_STAGE
+#define SAMNERF_HEAD_STAGE 0
+#endif
+struct HeadStager {
+    const uint4* __restrict__ packed;
+    uint4* Wb;            // LDS [2][kStepVec]
+    int tid, lane;
+    int step;
+    uint4 stg[4];
+
+    __device__ __forceinline__ void load(int s) {
+        const uint4* src = packed + (size_t)s * kStepVec + tid;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) stg[c] = src[c * 256];
+    }
+    __device__ __forceinline__ void store(int s) {
+        uint4* dst = Wb + (s & 1) * kStepVec + tid;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dst[c * 256] = stg[c];
+    }
+    __device__ __forceinline__ void begin() {
+        load(0);
+        store(0);
+        __syncthreads();
+    }
+    __device__ __forceinline__ void run(floatx16 (&acc)[8], const uint4& bh, const uint4& bl) {
+        const bool ahead = step + 1 < kSteps;
+        if (ahead) load(step + 1);
+        const uint4* cur = Wb + (step & 1) * kStepVec + lane;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = mfma3(cur[t * 64], cur[512 + t * 64], bh, bl, acc[t]);
+        if (ahead) store(step + 1);
+        __syncthreads();
+        ++step;
+    }
+};
+
 __device__ __forceinline__ float leaky(float x, bool act) { return act && x < 0.0f ? x * 0.01f : x; }
 
 // bias (+ leaky_relu) on the accumulators, then the hi/lo split into the next
@@ -397,9 +441,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 k_sam_head_bf3(HeadArgsB a) {
     // one LDS object (a second __shared__ object can de-pipeline the DMA
     // waits): 3 x 16 KiB weight steps, then biases and LN weight/bias
-    __shared__ uint4 smem[3 * kStepVec + (7 * 256) / 4];
+    constexpr int kRingSteps = SAMNERF_HEAD_STAGE ? 2 : 3;
+    __shared__ uint4 smem[kRingSteps * kStepVec + (7 * 256) / 4];
     uint4* Wb = smem;
-    float* Bs = reinterpret_cast<float*>(smem + 3 * kStepVec);
+    float* Bs = reinterpret_cast<float*>(smem + kRingSteps * kStepVec);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int j = lane & 31, h = lane >> 5;
     const uint32_t ray = blockIdx.x * kRaysV5 + wave * 32u + j;
@@ -433,11 +478,16 @@ k_sam_head_bf3(HeadArgsB a) {
     uint4 xh[kXkb], xl[kXkb];
 #pragma unroll
     for (int kb = 0; kb < kXkb; ++kb) load_x(kb, xh[kb], xl[kb]);
+#if SAMNERF_HEAD_STAGE
+    HeadStager st{a.packed, Wb, tid, lane, 0, {}};
+    st.begin();
+#else
     HeadStepper st{a.packed, Wb, wave, lane, 0};
     st.issue(0);
     st.issue(1);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");          // step 0 landed
     __syncthreads();
+#endif
     floatx16 acc[8];
     uint4 ah[kHkb], al[kHkb];
     auto zero = [&]() {
