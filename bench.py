@@ -686,6 +686,28 @@ def main():
                     "(synth.make_surface_params), same view"}
 
     if not args.no_alt and world == 1 and args.rank_share <= 1:
+        # perturb=True (renderer.py:266-271, :100-101: the distillation step's
+        # teacher render, the GUI's spp > 1) on the fused kernels, the torch
+        # draws of the perturbed positions inside the timed region
+        fr = FusedRenderer(net, head_mode=args.head_mode)
+        ro, rd = ops.get_rays(pose, intr, H, W, device=dev)
+        k = max(3, args.steps // 2)
+        for _ in range(2):
+            outp = fr.render(ro, rd, feats=with_sam, view_width=W, perturb=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            outp = fr.render(ro, rd, feats=with_sam, view_width=W, perturb=True)
+        torch.cuda.synchronize()
+        dtp = (time.perf_counter() - t0) / k
+        side["perturbed_render"] = {
+            "value": H * W / dtp, "unit": "rays/s", "ms_per_step": dtp * 1e3, "steps": k,
+            "max_abs_image_vs_unperturbed": float((outp["image"] - last["image"]).abs().max()),
+            "what": "the headline view with perturb=True: torch.rand_like draws of the perturbed "
+                    "stage-0 bins and sample_pdf positions (fused.perturbed_positions) + the fused "
+                    "render fed them (samnerf_model.perturb), one stream"}
+
+    if not args.no_alt and world == 1 and args.rank_share <= 1:
         # the --with_mask instance head on the fused kernels
         side["mask_default_head"] = mask_view(dev, max(3, args.steps // 2), 2, args.head_mode)
 

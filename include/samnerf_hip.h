@@ -203,13 +203,20 @@ typedef struct {
     int sum_after_mlp;            /* --sum_after_mlp (renderer.py:339-342): image =
                                      sigmoid(sum_k w_k view_mlp(colour_k)); RGB / mask models only
                                      (with SAM features the reference crashes) */
+    /* perturb=True (renderer.py:266-271 and sample_pdf's :100-101): the perturbed
+     * sample positions as the reference computes them from torch.rand_like, ray order:
+     * perturb[0] = the stage-0 bins clamp(linspace(0, 1, T0+1) + (rand - 0.5) / T0, 0, 1)
+     * [N][num_steps[0]+1]; perturb[1], perturb[2] = sample_pdf's u = linspace(0.5/T,
+     * 1-0.5/T, T) + (rand - 0.5) / T of stages 1 and 2, [N][T] with T = num_steps[s]+1.
+     * Set per call; all NULL = perturb=False (the default), all three or none. */
+    const float* perturb[3];
 } samnerf_model;
 
 /* Bytes of device workspace samnerf_render_forward needs for N rays. */
 size_t samnerf_render_workspace_size(const samnerf_model* model, uint32_t N);
 
 /* The whole ray-march inner loop for N rays (NeRFRenderer.run in eval mode:
- * perturb = False, background 'last_sample', sum_after_mlp = False,
+ * perturb = False unless model->perturb is set, background 'last_sample', sum_after_mlp = False,
  * sam_use_view_direction = True): near/far, 3 proposal rounds with
  * inverse-CDF resampling, hash-grid + SH encoding, sigma / colour MLPs,
  * compositing, view MLP, and (with_sam) the s_grid feature composite plus the

@@ -70,18 +70,21 @@ def contract(x):
     return z.view(*shape, C)
 
 
-def sample_pdf(bins, weights, T, perturb=False, return_inds=False):
-    """nerf/renderer.py:84-119 (inverse-CDF resampling, deterministic u)."""
+def sample_pdf(bins, weights, T, perturb=False, return_inds=False, u=None):
+    """nerf/renderer.py:84-119 (inverse-CDF resampling).  `u` [N, T]: given
+    sample positions (a perturbed draw made beforehand) instead of lines
+    97-103's."""
     N, T0 = weights.shape
     weights = weights + 0.01
     weights_sum = torch.sum(weights, -1, keepdim=True)
     pdf = weights / weights_sum
     cdf = torch.cumsum(pdf, -1).clamp(max=1)
     cdf = torch.cat([torch.zeros_like(cdf[..., :1]), cdf], -1)
-    u = torch.linspace(0.5 / T, 1 - 0.5 / T, steps=T).to(weights.device)
-    u = u.expand(N, T)
-    if perturb:
-        u = u + (torch.rand_like(u) - 0.5) / T
+    if u is None:
+        u = torch.linspace(0.5 / T, 1 - 0.5 / T, steps=T).to(weights.device)
+        u = u.expand(N, T)
+        if perturb:
+            u = u + (torch.rand_like(u) - 0.5) / T
     u = u.contiguous()
     inds = torch.searchsorted(cdf, u, right=True)
     below = torch.clamp(inds - 1, 0, T0)
@@ -279,11 +282,14 @@ class OracleNeRF:
 
     @torch.no_grad()
     def run(self, rays_o, rays_d, bg_color=None, return_feats=0, return_mask=0, H=None, W=None,
-            keep=None):
-        """nerf/renderer.py:221-464 in eval mode (perturb=False, contract=True,
+            keep=None, perturb=False, perturbed=None):
+        """nerf/renderer.py:221-464 in eval mode (contract=True,
         background='last_sample', sam_use_view_direction; sum_after_mlp for
         the RGB + mask configurations).  `keep` (a dict) receives per-stage
-        intermediates for finer checks."""
+        intermediates for finer checks.  perturb=True draws torch.rand_like
+        where the reference does (renderer.py:268-271, :100-101); `perturbed`
+        = (bins0 [N, T0+1], u1 [N, T1+1], u2 [N, T2+1]) supplies those
+        positions instead (the same draw made beforehand)."""
         rays_o = rays_o.contiguous()
         rays_d = rays_d.contiguous()
         N = rays_o.shape[0]
@@ -299,8 +305,14 @@ class OracleNeRF:
             if prop_iter == 0:
                 bins = torch.linspace(0, 1, steps[prop_iter] + 1).unsqueeze(0)
                 bins = bins.expand(N, -1)
+                if perturbed is not None:
+                    bins = perturbed[0]
+                elif perturb:
+                    bins = bins + (torch.rand_like(bins) - 0.5) / (steps[prop_iter])
+                    bins = bins.clamp(0, 1)
             else:
-                bins = sample_pdf(bins, weights, steps[prop_iter] + 1, False).detach()
+                u = perturbed[prop_iter] if perturbed is not None else None
+                bins = sample_pdf(bins, weights, steps[prop_iter] + 1, perturb, u=u).detach()
             real_bins = spacing_fn_inv(s_nears * (1 - bins) + s_fars * bins)
             rays_t = (real_bins[..., 1:] + real_bins[..., :-1]) / 2
             xyzs = rays_o.unsqueeze(1) + rays_d.unsqueeze(1) * rays_t.unsqueeze(2)
@@ -320,6 +332,8 @@ class OracleNeRF:
                     masks = self.m_grid(xyzs, bound=self.bound)
             weights = composite_weights(real_bins, sigmas)
             if keep is not None:
+                if prop_iter < len(steps) - 1 and perturbed is not None:
+                    keep[f"u{prop_iter}"] = perturbed[prop_iter + 1]
                 keep[f"bins{prop_iter}"] = bins.clone()
                 keep[f"weights{prop_iter}"] = weights.clone()
                 keep[f"sigmas{prop_iter}"] = sigmas.clone()

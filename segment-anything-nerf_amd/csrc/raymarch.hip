@@ -170,6 +170,11 @@ struct PropArgs {
     const float* W1;       // [1, 16]
     Lin bins0;             // stage 0: linspace(0, 1, T+1)
     Lin u;                 // sample_pdf positions for the next stage
+    // perturb=True (samnerf_model.perturb, ray order): the stage-0 bins [N][T+1]
+    // and sample_pdf's u [N][TN] as the reference computes them from
+    // torch.rand_like; null: linspace (bins0 / u above)
+    const float* pbins0;
+    const float* pu;
     const float* bins_in;  // [T+1][N] (stages > 0)
     float* snf;            // [2][N] spacing(near), spacing(far)
     float* wtmp;           // [T][N]: ds per sample
@@ -177,6 +182,15 @@ struct PropArgs {
     int32_t* inds_out;     // [TN][N] searchsorted indices, or null (parity taps only)
     float* w_out;          // [T][N] composited weights, or null (parity taps only)
 };
+
+// Bin i of a stage's input for slot r (ray `ray`): stage 0 linspace(0, 1, T+1)
+// or its perturbed copy (renderer.py:264-271), later stages the previous
+// stage's resampled bins (slot-major workspace).
+template <int T, bool FIRST>
+__device__ __forceinline__ float stage_bin(const PropArgs& a, int i, uint32_t r, uint32_t ray) {
+    if constexpr (FIRST) return a.pbins0 ? a.pbins0[(size_t)ray * (T + 1) + i] : a.bins0(i);
+    else return a.bins_in[(size_t)i * a.N + r];
+}
 
 // Proposal stage, part 1: one thread per (ray, sample).  A wave is 64
 // neighbouring rays at one sample index (their corner gathers share cache
@@ -223,14 +237,7 @@ __global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
         d[c] = a.rays_d[(size_t)ray * 3 + c];
     }
     const float sn = a.snf[r], sf = a.snf[N + r];           // k_snf (stage 0) / stage 0 (stage 1)
-    float b0, b1;
-    if constexpr (FIRST) {
-        b0 = a.bins0(k);
-        b1 = a.bins0(k + 1);
-    } else {
-        b0 = a.bins_in[(size_t)k * N + r];
-        b1 = a.bins_in[(size_t)(k + 1) * N + r];
-    }
+    const float b0 = stage_bin<T, FIRST>(a, (int)k, r, ray), b1 = stage_bin<T, FIRST>(a, (int)k + 1, r, ray);
     const float rb_prev = real_bin(sn, sf, b0), rb_next = real_bin(sn, sf, b1);
     const float t = (rb_next + rb_prev) / 2.0f;
     float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
@@ -379,15 +386,16 @@ __device__ __forceinline__ void prop_pdf_phases(const PropArgs& a, float* sw, ui
     }
     __syncthreads();
     if (lane >= nr) return;
-    const uint32_t r = r0 + lane;
-    auto bin = [&](int i) -> float {
-        if constexpr (FIRST) return a.bins0(i);
-        else return a.bins_in[(size_t)i * N + r];
-    };
+    const uint32_t r = r0 + lane, ray = a.tiles(r);
+    auto bin = [&](int i) -> float { return stage_bin<T, FIRST>(a, i, r, ray); };
+    // u_j: linspace, or the perturbed positions (nondecreasing up to rounding:
+    // u_j < (j+1)/TN <= u_{j+1} before it, hence the backward step below)
+    const float* pu = a.pu ? a.pu + (size_t)ray * TN : nullptr;
+    auto uj = [&](int j) -> float { return pu ? pu[j] : a.u(j); };
     constexpr int QN = TN / 4;
     const int j0 = (int)part * QN, j1 = part == 3 ? TN : j0 + QN;
     // first index with cdf > u_j0 (cdf is nondecreasing, cdf[0] = 0 <= u)
-    const float u0 = a.u(j0);
+    const float u0 = uj(j0);
     int lo = 1, hi = T + 1;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -396,7 +404,9 @@ __device__ __forceinline__ void prop_pdf_phases(const PropArgs& a, float* sw, ui
     }
     int i = lo;
     for (int j = j0; j < j1; ++j) {
-        const float u = a.u(j);
+        const float u = uj(j);
+        if (pu)
+            while (i > 1 && row[i - 1] > u) --i;
         while (i <= T && row[i] <= u) ++i;
         const int below = i - 1, above = i <= T ? i : T;
         const float g0 = row[below], g1 = row[above];
@@ -439,14 +449,7 @@ __global__ void __launch_bounds__(256) k_prop_fused(PropArgs a) {
 #pragma unroll 2
         for (int kk = 0; kk < T / 4; ++kk) {
             const int k = (int)part + 4 * kk;
-            float b0, b1;
-            if constexpr (FIRST) {
-                b0 = a.bins0(k);
-                b1 = a.bins0(k + 1);
-            } else {
-                b0 = a.bins_in[(size_t)k * N + r];
-                b1 = a.bins_in[(size_t)(k + 1) * N + r];
-            }
+            const float b0 = stage_bin<T, FIRST>(a, k, r, ray), b1 = stage_bin<T, FIRST>(a, k + 1, r, ray);
             const float rb_prev = real_bin(sn, sf, b0), rb_next = real_bin(sn, sf, b1);
             const float t = (rb_next + rb_prev) / 2.0f;
             float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
@@ -2013,7 +2016,8 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     // at all
     if (cam_near_far && n_cnf != 1 && n_cnf != N)
         return fail(SAMNERF_EINVAL, "render: cam_near_far must have 1 or N rows");
-    if (N == 0) return SAMNERF_OK;
+    if (!m->perturb[0] != !m->perturb[1] || !m->perturb[0] != !m->perturb[2])
+        return fail(SAMNERF_EINVAL, "render: perturb needs all three position arrays or none");
     Workspace w = carve(m, N, workspace);
     if (!workspace || workspace_bytes < w.bytes)
         return fail(SAMNERF_EWORKSPACE, "render: workspace needs %zu bytes, got %zu", w.bytes,
@@ -2061,6 +2065,8 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.bins0 = make_lin(0.0f, 1.0f, 129);
     pa.u = make_lin((float)(0.5 / 65), (float)(1.0 - 0.5 / 65), 65);
     pa.bins_in = nullptr;
+    pa.pbins0 = m->perturb[0];
+    pa.pu = m->perturb[1];
     pa.bins_out = bins1;
     pa.wtmp = tp.ds0 ? tp.ds0 : w.wtmp;
     pa.inds_out = tp.inds1;
@@ -2085,6 +2091,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     pa.W0 = m->prop_mlp[1][0];
     pa.W1 = m->prop_mlp[1][1];
     pa.u = make_lin((float)(0.5 / 33), (float)(1.0 - 0.5 / 33), 33);
+    pa.pu = m->perturb[2];
     pa.bins_in = bins1;
     pa.bins_out = bins2;
     pa.wtmp = tp.ds1 ? tp.ds1 : w.wtmp;

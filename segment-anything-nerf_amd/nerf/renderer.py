@@ -6,8 +6,10 @@ executes the whole ray-march loop as the fused HIP pipeline
 (samnerf_amd.fused, raymarch.hip).  `run_torch()` is the reference's own
 unfused op sequence on the GPU with the drop-in encoders -- the
 "reference-equivalent" single-GPU baseline of BASELINE.md and the path for
-options the fused kernels do not cover (perturbed sampling, training-mode
-bookkeeping).  Staged rendering chunks rays like renderer.py:185-219 but,
+options the fused kernels do not cover (training-mode bookkeeping and
+autograd).  Perturbed sampling runs fused: the perturbed positions are drawn
+with torch's generator in the reference's order (fused.perturbed_positions).
+Staged rendering chunks rays like renderer.py:185-219 but,
 unlike the reference, also works with return_feats (flat [N,256] rows are
 reshaped once at the end, fixing the SURVEY.md 0.3 crash).
 """
@@ -175,8 +177,13 @@ class NeRFRenderer(nn.Module):
             from samnerf_amd.fused import mask_kind
             if mask_kind(self) is None:
                 return False                 # the other mask heads: unfused path
-        return (self.fused and rays_o.is_cuda and not perturb
-                and not self.training and self.opt.background == "last_sample"
+        # training mode only for no-grad renders without the train-mode extras
+        # (renderer.py:348-356 adds them only without SAM and masks): the SAM
+        # distillation's teacher render, utils.py:1078-1079
+        train_ok = not self.training or (not torch.is_grad_enabled() and (
+            self.opt.with_sam or getattr(self.opt, "with_mask", False)))
+        return (self.fused and rays_o.is_cuda and train_ok
+                and self.opt.background == "last_sample"
                 # sum_after_mlp: RGB (+ mask) models on the fused path; with SAM
                 # the reference's branch crashes and run_torch raises
                 and not (getattr(self.opt, "sum_after_mlp", False) and self.opt.with_sam)
@@ -192,7 +199,8 @@ class NeRFRenderer(nn.Module):
             n = rays_o.shape[0]
             vw = W if (W is not None and n % W == 0) else 0      # a whole number of image rows
             out = self._fused.render(rays_o, rays_d, cam_near_far, bg_color,
-                                     feats=return_feats > 0, view_width=vw, mask=return_mask > 0)
+                                     feats=return_feats > 0, view_width=vw, mask=return_mask > 0,
+                                     perturb=perturb)
             samvit = out.pop("samvit", None)
             if return_feats > 0 and samvit is not None:
                 out["samvit"] = samvit.view(H, W, -1) if H is not None else samvit
@@ -205,8 +213,8 @@ class NeRFRenderer(nn.Module):
                   update_proposal=True, return_feats=0, return_mask=0, H=None, W=None, **kwargs):
         """The reference's unfused op sequence (renderer.py:221-464) with the
         HIP drop-in encoders: ~350 small kernels per call.  Covers what the
-        fused kernels do not: perturbed sampling, training-mode extras,
-        sum_after_mlp and the --with_mask instance heads."""
+        fused kernels do not: training-mode extras and autograd, the
+        'lightweight_mask' / adaptive 'sam' heads, sum_after_mlp with SAM."""
         opt = self.opt
         with_mask = getattr(opt, "with_mask", False)
         mask_type = getattr(opt, "mask_mlp_type", "default")

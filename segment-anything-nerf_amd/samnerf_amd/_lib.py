@@ -38,7 +38,7 @@ class SamnerfModel(ctypes.Structure):
                 ("t_thresh", _f32), ("view_width", _u32),
                 ("with_mask", _int), ("mask_kind", _int), ("m_grid", SamnerfGrid), ("mask_w", _vp * 8),
                 ("mask_out", _u32),
-                ("sum_after_mlp", _int)]
+                ("sum_after_mlp", _int), ("perturb", _vp * 3)]
 
 
 _SIGS = {

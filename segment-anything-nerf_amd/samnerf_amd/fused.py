@@ -43,6 +43,24 @@ def mask_kind(net):
     return None
 
 
+def perturbed_positions(N, num_steps, device):
+    """The sample positions of perturb=True, drawn and computed exactly as the
+    reference does (torch.rand_like in its order, the same expressions): the
+    stage-0 bins (renderer.py:264-271) and sample_pdf's u for stages 1 and 2
+    (renderer.py:97-103, called at :274-275).  The proposal stages draw nothing
+    else, so drawing all three first consumes the generator identically.
+    Returns (bins0 [N, T0+1], u1 [N, T1+1], u2 [N, T2+1])."""
+    T0 = int(num_steps[0])
+    bins = torch.linspace(0, 1, T0 + 1, device=device).unsqueeze(0).expand(N, -1)
+    bins = (bins + (torch.rand_like(bins) - 0.5) / T0).clamp(0, 1)
+    out = [bins.contiguous()]
+    for T in (int(num_steps[1]) + 1, int(num_steps[2]) + 1):
+        u = torch.linspace(0.5 / T, 1 - 0.5 / T, steps=T, device=device).expand(N, T)
+        u = u + (torch.rand_like(u) - 0.5) / T
+        out.append(u.contiguous())
+    return tuple(out)
+
+
 class FusedRenderer:
     """head_mode: 0 = bf16x3 split precision for grid_mlp and the SAM head
     (default), 1 = exact fp32.  t_thresh: 0 (default) = the reference's
@@ -165,7 +183,7 @@ class FusedRenderer:
     @torch.no_grad()
     def render(self, rays_o, rays_d, cam_near_far=None, bg_color=None, rows=None,
                keep_workspace=False, feats=True, taps=False, own_workspace=False, view_width=0,
-               mask=False):
+               mask=False, perturb=False):
         """rays_o, rays_d [N,3] (CUDA fp32) -> dict(image [N,3], depth [N],
         weights_sum [N], samvit [N,256] if with_sam and feats).  `rows`
         (optional [N,164] tensor) receives the head input cat(f_sam, f_image,
@@ -183,7 +201,11 @@ class FusedRenderer:
         tiles per wave, same outputs bit for bit, faster gathers.
         mask=True (a 'default' mask head, fused_mask_ok): also
         instance_mask_logits [N, n_inst + redundant_instance]
-        (samnerf_mask_forward on the render's workspace)."""
+        (samnerf_mask_forward on the render's workspace).
+        perturb: False (default), True (draw the perturbed sample positions
+        with torch's generator, perturbed_positions -- the reference's
+        perturb=True), or a (bins0, u1, u2) tuple of them [N, 129], [N, 65],
+        [N, 33] (samnerf_model.perturb)."""
         rays_o = rays_o.contiguous().float()
         rays_d = rays_d.contiguous().float()
         N = rays_o.shape[0]
@@ -193,6 +215,19 @@ class FusedRenderer:
         if mask and not self.fused_mask_ok():
             raise NotImplementedError("fused render: this mask head runs on the unfused path")
         m.with_mask = 1 if mask else 0
+        pert = None
+        if isinstance(perturb, (tuple, list)) or perturb:      # the GUI passes spp (an int) as perturb
+            pert = tuple(perturb) if isinstance(perturb, (tuple, list)) else \
+                perturbed_positions(N, list(m.num_steps), dev)
+            shapes = [(N, int(m.num_steps[0]) + 1), (N, int(m.num_steps[1]) + 1), (N, int(m.num_steps[2]) + 1)]
+            if len(pert) != 3 or any(tuple(t.shape) != sh for t, sh in zip(pert, shapes)):
+                raise ValueError(f"fused render: perturb arrays must have shapes {shapes}")
+            pert = tuple(t.contiguous().float() for t in pert)
+            for i in range(3):
+                m.perturb[i] = _param(pert[i], f"perturb[{i}]")
+        else:
+            for i in range(3):
+                m.perturb[i] = None
         if own_workspace:
             need = lib().samnerf_render_workspace_size(ctypes.byref(m), N)
             ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
@@ -240,6 +275,8 @@ class FusedRenderer:
         finally:
             if taps:
                 lib().samnerf_set_taps(None, 0)
+            for i in range(3):
+                m.perturb[i] = None
         out = {"image": image, "depth": depth, "weights_sum": wsum}
         if mask:
             out["instance_mask_logits"] = logits

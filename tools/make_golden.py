@@ -124,11 +124,17 @@ def install_reference():
     s.SHEncoder = StandInSHEncoder
     sys.modules["gridencoder"] = g
     sys.modules["shencoder"] = s
+    # the product package's directory (put on sys.path by oracle/synth.py)
+    # holds a regular `nerf` package, which would win over the reference's
+    # namespace package wherever it sits on the path
+    sys.path[:] = [p for p in sys.path if not p.rstrip("/").endswith("segment-anything-nerf_amd")]
     sys.path.insert(0, REF)
     import importlib
     network = importlib.import_module("nerf.network")
     renderer = importlib.import_module("nerf.renderer")
     utils = importlib.import_module("nerf.utils")
+    for mod in (network, renderer, utils):
+        assert os.path.realpath(mod.__file__).startswith(REF + "/"), mod.__file__
     return network, renderer, utils
 
 
@@ -232,6 +238,65 @@ def mask_fixtures(network):
                         **{k + "_msg": np.array(v[1]) for k, v in errs.items()})
 
 
+def perturbed_draws(N, steps, seed):
+    """The random positions of run(perturb=True) drawn in the reference's order
+    from torch.manual_seed(seed): renderer.py:268-271 (stage-0 bins), then
+    sample_pdf's u (renderer.py:97-103) for stages 1 and 2 -- nothing else
+    draws in between."""
+    torch.manual_seed(seed)
+    T0 = steps[0]
+    bins = torch.linspace(0, 1, T0 + 1).unsqueeze(0).expand(N, -1)
+    bins = (bins + (torch.rand_like(bins) - 0.5) / T0).clamp(0, 1)
+    out = [bins.contiguous()]
+    for T in (steps[1] + 1, steps[2] + 1):
+        u = torch.linspace(0.5 / T, 1 - 0.5 / T, steps=T).expand(N, T)
+        out.append((u + (torch.rand_like(u) - 0.5) / T).contiguous())
+    return out
+
+
+def perturbed_fixture(network):
+    """run(perturb=True) of the reference (renderer.py:221-390 with the random
+    sample positions of :268-271 and :100-101) on a 16x16 SAM view, from
+    torch.manual_seed(11).  Stores the positions the draw produced, so the
+    GPU path can be fed the same ones (the device generator draws others)."""
+    spec = synth.ModelSpec(with_sam=True, grid_log2=12, s_grid_log2=11, prop_log2=10)
+    TABLE_LOG2.clear()
+    TABLE_LOG2[(16, 2, int(2048 * spec.grid_bound))] = spec.grid_log2
+    TABLE_LOG2[(16, 8, 512)] = spec.s_grid_log2
+    TABLE_LOG2[(5, 2, 128)] = spec.prop_log2
+    TABLE_LOG2[(5, 2, 256)] = spec.prop_log2
+    params = synth.make_params(spec, seed=12, emb_scale=0.5, ln_jitter=0.1)
+    model = network.NeRFNetwork(make_opt(spec))
+    model.load_state_dict({k: torch.from_numpy(np.asarray(params[k])) for k in model.state_dict()},
+                          strict=True)
+    model.eval()
+    H = W = 16
+    pose, intr = synth.gui_camera(W, H, rot=synth.random_rotation(9))
+    rays_o, rays_d = orc.get_rays(pose, intr, H, W)
+    torch.manual_seed(11)
+    with torch.no_grad():
+        ref = model.run(rays_o, rays_d, perturb=True, return_feats=1, H=H, W=W)
+    draws = perturbed_draws(H * W, list(spec.num_steps), 11)
+    oracle = orc.OracleNeRF(spec, params)
+    torch.manual_seed(11)
+    mine = oracle.run(rays_o, rays_d, return_feats=1, H=H, W=W, perturb=True)
+    given = oracle.run(rays_o, rays_d, return_feats=1, H=H, W=W, perturbed=draws)
+    for k, v in ref.items():
+        for other, what in ((mine, "perturb=True"), (given, "perturbed draws")):
+            d = (v - other[k]).abs().max().item()
+            print(f"  render_perturbed_sam: {k:12s} max|ref-oracle({what})| = {d:.3e}")
+            assert d == 0.0, f"oracle restatement diverges from reference on {k} ({what})"
+    np.savez_compressed(
+        os.path.join(GOLDEN, "render_perturbed_sam.npz"),
+        spec=np.array([spec.with_sam, spec.grid_log2, spec.s_grid_log2, spec.prop_log2], np.int64),
+        seed=np.int64(12), emb_scale=np.float64(0.5), ln_jitter=np.float64(0.1), torch_seed=np.int64(11),
+        pose=pose, intrinsics=intr, H=np.int64(H), W=np.int64(W),
+        rays_o=rays_o.numpy(), rays_d=rays_d.numpy(),
+        bins0=draws[0].numpy(), u1=draws[1].numpy(), u2=draws[2].numpy(),
+        image=ref["image"].numpy(), depth=ref["depth"].numpy(),
+        weights_sum=ref["weights_sum"].numpy(), samvit=ref["samvit"].reshape(H * W, -1).numpy())
+
+
 def units_fixture(renderer, utils):
     g = torch.Generator().manual_seed(1234)
     out = {}
@@ -276,10 +341,14 @@ def units_fixture(renderer, utils):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
+    ap.add_argument("--only", choices=["perturbed"], help="write just this fixture")
     args = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
     enc.build()
     network, renderer, utils = install_reference()
+    if args.only == "perturbed":
+        perturbed_fixture(network)
+        return
     units_fixture(renderer, utils)
     small = dict(grid_log2=12, s_grid_log2=11, prop_log2=10)
     render_fixture(network, "render_small_rgb", synth.ModelSpec(with_sam=False, **small),
@@ -290,6 +359,7 @@ def main():
                    synth.ModelSpec(with_sam=True, **small),
                    seed=5, emb_scale=1e-4, H=8, W=8, rot_seed=None, ln_jitter=0.0)
     mask_fixtures(network)
+    perturbed_fixture(network)
     if not args.skip_full:
         render_fixture(network, "render_full_sam", synth.ModelSpec(with_sam=True),
                        seed=3, emb_scale=0.5, H=8, W=8, rot_seed=5)
