@@ -1396,16 +1396,22 @@ k_sgrid_box4(SgridArgs a) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) acc[l][c] = 0.0f;
     const int k0 = (int)q * TQ;
-    float ux = a.u_in[((size_t)k0 * 3 + 0) * N + rr];
-    float uy = a.u_in[((size_t)k0 * 3 + 1) * N + rr];
-    float uz = a.u_in[((size_t)k0 * 3 + 2) * N + rr];
-    float w = a.w_in[(size_t)k0 * N + rr];
+    // 32-bit byte offsets (the host launches this form only for 384 N < 2^32):
+    // uniform base + lane offset loads, no 64-bit address arithmetic per sample
+    const char* ub = reinterpret_cast<const char*>(a.u_in);
+    const char* wb = reinterpret_cast<const char*>(a.w_in);
+    const uint32_t N4 = N * 4u;
+    auto ld = [](const char* b, uint32_t off) { return *reinterpret_cast<const float*>(b + off); };
+    float ux = ld(ub, ((uint32_t)k0 * 3u + 0u) * N4 + rr * 4u);
+    float uy = ld(ub, ((uint32_t)k0 * 3u + 1u) * N4 + rr * 4u);
+    float uz = ld(ub, ((uint32_t)k0 * 3u + 2u) * N4 + rr * 4u);
+    float w = ld(wb, (uint32_t)k0 * N4 + rr * 4u);
     for (int k = k0; k < k0 + TQ; ++k) {
-        const int kn = k + 1 < k0 + TQ ? k + 1 : k;          // prefetch (clamped)
-        const float nx = a.u_in[((size_t)kn * 3 + 0) * N + rr];
-        const float ny = a.u_in[((size_t)kn * 3 + 1) * N + rr];
-        const float nz = a.u_in[((size_t)kn * 3 + 2) * N + rr];
-        const float nw = a.w_in[(size_t)kn * N + rr];
+        const uint32_t kn = (uint32_t)(k + 1 < k0 + TQ ? k + 1 : k);          // prefetch (clamped)
+        const float nx = ld(ub, (kn * 3u + 0u) * N4 + rr * 4u);
+        const float ny = ld(ub, (kn * 3u + 1u) * N4 + rr * 4u);
+        const float nz = ld(ub, (kn * 3u + 2u) * N4 + rr * 4u);
+        const float nw = ld(wb, kn * N4 + rr * 4u);
         // samples with weight 0 on all 64 rays (N1's dropped samples) add nothing
         if (__builtin_amdgcn_ballot_w64(w != 0.0f) != 0) {
             const URange ur = wave_urange(ux, uy, uz);
@@ -2195,7 +2201,8 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
         mark_stage(3, s);
         const dim3 sg(xcd_blocks(div_up(N, 64)), 16);
         if (look == kLookRef) k_sgrid<32, kLookRef><<<sg, 256, 0, s>>>(sa);
-        else if ((look == kLookBox4 || (look == kLookAuto && N >= kBox4MinRays)) && box4_ok(gs))
+        else if ((look == kLookBox4 || (look == kLookAuto && N >= kBox4MinRays)) && box4_ok(gs) &&
+                 (uint64_t)N * 384u < (1ull << 32))
             k_sgrid_box4<32><<<dim3(xcd_blocks(div_up(N, 64)), 4), 256, 0, s>>>(sa);
         else k_sgrid<32, kLookPacked><<<sg, 256, 0, s>>>(sa);
         if ((rc = check_launch("render"))) return rc;

@@ -102,15 +102,41 @@ __device__ __forceinline__ int wave_imax(int v) {
 // to cell 0.  NaN lanes are neutral (INT_MAX in the min, INT_MIN in the max),
 // as fminf / fmaxf skip NaN; an all-NaN wave yields NaN bits / -0.0, cell 0
 // like the float reduction's NaN.
+// The six reductions run in lockstep (independent DPP chains, so no hazard
+// wait states between steps); across the rows of 16, row_bcast:15 and
+// row_bcast:31 fold the row results into row 3 and one readlane of lane 63
+// takes the total (round 1: four readlanes, two copies and a min3 per value).
 __device__ __forceinline__ URange wave_urange(float ux, float uy, float uz) {
     const float u[3] = {ux, uy, uz};
-    URange r;
+    int lo[3], hi[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const int b = __float_as_int(u[c]);
         const bool nan = u[c] != u[c];
-        r.lo[c] = __int_as_float(wave_imin(nan ? INT_MAX : b));
-        r.hi[c] = __int_as_float(wave_imax(nan ? INT_MIN : b));
+        lo[c] = nan ? INT_MAX : b;
+        hi[c] = nan ? INT_MIN : b;
+    }
+#define SAMNERF_URANGE_STEP(EXPR_LO, EXPR_HI)                                   \
+    _Pragma("unroll") for (int c = 0; c < 3; ++c) {                             \
+        lo[c] = min(lo[c], EXPR_LO);                                            \
+        hi[c] = max(hi[c], EXPR_HI);                                            \
+    }
+    SAMNERF_URANGE_STEP(dpp_i<0xB1>(lo[c]), dpp_i<0xB1>(hi[c]))        // quad_perm [1,0,3,2]
+    SAMNERF_URANGE_STEP(dpp_i<0x4E>(lo[c]), dpp_i<0x4E>(hi[c]))        // quad_perm [2,3,0,1]
+    SAMNERF_URANGE_STEP(dpp_i<0x141>(lo[c]), dpp_i<0x141>(hi[c]))      // row_half_mirror
+    SAMNERF_URANGE_STEP(dpp_i<0x140>(lo[c]), dpp_i<0x140>(hi[c]))      // row_mirror: row totals
+    // rows 1, 3 take lane 15 of the row below, rows 2, 3 lane 31 (the other
+    // rows see the identity, so min / max fold into one DPP instruction each)
+    SAMNERF_URANGE_STEP(__builtin_amdgcn_update_dpp(INT_MAX, lo[c], 0x142, 0xa, 0xf, false),
+                        __builtin_amdgcn_update_dpp(INT_MIN, hi[c], 0x142, 0xa, 0xf, false))
+    SAMNERF_URANGE_STEP(__builtin_amdgcn_update_dpp(INT_MAX, lo[c], 0x143, 0xc, 0xf, false),
+                        __builtin_amdgcn_update_dpp(INT_MIN, hi[c], 0x143, 0xc, 0xf, false))
+#undef SAMNERF_URANGE_STEP
+    URange r;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        r.lo[c] = __int_as_float(__builtin_amdgcn_readlane(lo[c], 63));
+        r.hi[c] = __int_as_float(__builtin_amdgcn_readlane(hi[c], 63));
     }
     return r;
 }
