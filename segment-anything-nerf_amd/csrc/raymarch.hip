@@ -1414,11 +1414,19 @@ k_sgrid_box4(SgridArgs a) {
         const float nw = ld(wb, kn * N4 + rr * 4u);
         // samples with weight 0 on all 64 rays (N1's dropped samples) add nothing
         if (__builtin_amdgcn_ballot_w64(w != 0.0f) != 0) {
+            const f2v wv = {w, w};
+            auto add = [&](int l, const float* f) {
+#pragma unroll
+                for (int c = 0; c < 8; c += 2) {
+                    const f2v s2 = f2v{acc[l][c], acc[l][c + 1]} + wv * f2v{f[c], f[c + 1]};
+                    acc[l][c] = s2.x;
+                    acc[l][c + 1] = s2.y;
+                }
+            };
             const URange ur = wave_urange(ux, uy, uz);
             const bool ordered = wave_positions_ordered(ux, uy, uz);
             uint32_t p0, p1, p2;
             pbox_lane(mine, ur, p0, p1, p2);
-            const f2v wv = {w, w};
 #pragma unroll
             for (int l = 0; l < 4; ++l) {
                 const PBox b = pbox_read(p0, p1, p2, l);
@@ -1434,12 +1442,7 @@ k_sgrid_box4(SgridArgs a) {
                 } else {
                     lookup_level3<8>(a.grid.emb, L[l], ux, uy, uz, f);
                 }
-#pragma unroll
-                for (int c = 0; c < 8; c += 2) {
-                    const f2v s2 = f2v{acc[l][c], acc[l][c + 1]} + wv * f2v{f[c], f[c + 1]};
-                    acc[l][c] = s2.x;
-                    acc[l][c + 1] = s2.y;
-                }
+                add(l, f);
             }
         }
         ux = nx;

@@ -257,28 +257,44 @@ __device__ __forceinline__ void lookup_level3_pbox(const float* __restrict__ emb
             return;
         }
     }
-    const uint32_t X[2] = {lx0, lx1};
-    const uint32_t Y[2] = {ly0 << b.lx, ly1 << b.lx};
-    const uint32_t Z[2] = {lz0 << (b.lx + b.ly), lz1 << (b.lx + b.ly)};
+    // corner c's slot byte offset: the (x, y, z) = (0, 0, 0) corner plus
+    // per-axis steps of 0 (clamped top cell) or one slot row, one add each
+    constexpr uint32_t RB = C * 4u;                     // bytes per slot
+    const uint32_t lxy = b.lx + b.ly;
+    const uint32_t o0 = (lx0 + (ly0 << b.lx) + (lz0 << lxy)) * RB;
+    const uint32_t DX = (lx1 - lx0) * RB, DY = ((ly1 - ly0) << b.lx) * RB, DZ = ((lz1 - lz0) << lxy) * RB;
+    uint32_t off[8];
+    off[0] = o0;
+    off[1] = o0 + DX;
+    off[2] = o0 + DY;
+    off[3] = off[2] + DX;
+    off[4] = o0 + DZ;
+    off[5] = off[4] + DX;
+    off[6] = off[4] + DY;
+    off[7] = off[6] + DX;
+    // the corner weights of lookup_level3 (wxy[c & 3] * (c & 4 ? fz : 1 - fz)),
+    // two per packed multiply
     const float wx0 = 1.0f - fx, wy0 = 1.0f - fy, wz0 = 1.0f - fz;
-    const float wxy[4] = {wx0 * wy0, fx * wy0, wx0 * fy, fx * fy};
+    const f2v xw = {wx0, fx};
+    const f2v wxy01 = xw * f2v{wy0, wy0}, wxy23 = xw * f2v{fy, fy};
+    const f2v wc[4] = {wxy01 * f2v{wz0, wz0}, wxy23 * f2v{wz0, wz0}, wxy01 * f2v{fz, fz}, wxy23 * f2v{fz, fz}};
+    const char* sb = reinterpret_cast<const char*>(slice);
     f2v a[C / 2];
 #pragma unroll
     for (int i = 0; i < C / 2; ++i) a[i] = f2v{0.0f, 0.0f};
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        const float w = wxy[c & 3] * ((c & 4) ? fz : wz0);
-        const uint32_t j = X[c & 1] + Y[(c >> 1) & 1] + Z[c >> 2];
-        const f2v wc = {w, w};
+        const float w = (c & 1) ? wc[c >> 1].y : wc[c >> 1].x;
+        const f2v wv = {w, w};
         if constexpr (C == 2) {
-            const float2 v = *reinterpret_cast<const float2*>(slice + j * 2);
-            a[0] = __builtin_elementwise_fma(wc, f2v{v.x, v.y}, a[0]);
+            const float2 v = *reinterpret_cast<const float2*>(sb + off[c]);
+            a[0] = __builtin_elementwise_fma(wv, f2v{v.x, v.y}, a[0]);
         } else {
 #pragma unroll
             for (int i = 0; i < C; i += 4) {
-                const float4 v = *reinterpret_cast<const float4*>(slice + j * C + i);
-                a[i / 2] = __builtin_elementwise_fma(wc, f2v{v.x, v.y}, a[i / 2]);
-                a[i / 2 + 1] = __builtin_elementwise_fma(wc, f2v{v.z, v.w}, a[i / 2 + 1]);
+                const float4 v = *reinterpret_cast<const float4*>(sb + off[c] + i * 4);
+                a[i / 2] = __builtin_elementwise_fma(wv, f2v{v.x, v.y}, a[i / 2]);
+                a[i / 2 + 1] = __builtin_elementwise_fma(wv, f2v{v.z, v.w}, a[i / 2 + 1]);
             }
         }
     }
