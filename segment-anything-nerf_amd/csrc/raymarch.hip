@@ -736,12 +736,12 @@ __device__ __forceinline__ void gather_finish_c2(const GatherC2<NL>& g, float* f
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
         if constexpr (PK) {
-            const float wx0 = 1.0f - g.fx[l], wy0 = 1.0f - g.fy[l], wz0 = 1.0f - g.fz[l];
-            const float wxy[4] = {wx0 * wy0, g.fx[l] * wy0, wx0 * g.fy[l], g.fx[l] * g.fy[l]};
+            f2v wc[4];
+            corner_weights_pk(g.fx[l], g.fy[l], g.fz[l], wc);
             f2v acc = {0.0f, 0.0f};
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
-                const float w = wxy[c & 3] * ((c & 4) ? g.fz[l] : wz0);
+                const float w = corner_w(wc, c);
                 acc = __builtin_elementwise_fma(f2v{w, w}, f2v{g.e[l][c].x, g.e[l][c].y}, acc);
             }
             f[2 * l] = acc.x;

@@ -139,6 +139,22 @@ __device__ __forceinline__ void load_row_b(const char* __restrict__ base, uint32
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+// The 8 trilinear corner weights (wx * wy) * wz of corner c (bit d <-> axis d,
+// gridencoder.cu:168-201), two per packed multiply: wc[c >> 1] holds corners
+// c & ~1 (.x) and c | 1 (.y).  Each lane of v_pk_mul_f32 is the scalar IEEE
+// multiply, so the weights are the bits of the scalar form.
+__device__ __forceinline__ void corner_weights_pk(float fx, float fy, float fz, f2v* wc) {
+    const float wx0 = 1.0f - fx, wy0 = 1.0f - fy, wz0 = 1.0f - fz;
+    const f2v xw = {wx0, fx};
+    const f2v wxy01 = xw * f2v{wy0, wy0}, wxy23 = xw * f2v{fy, fy};
+    wc[0] = wxy01 * f2v{wz0, wz0};
+    wc[1] = wxy23 * f2v{wz0, wz0};
+    wc[2] = wxy01 * f2v{fz, fz};
+    wc[3] = wxy23 * f2v{fz, fz};
+}
+
+__device__ __forceinline__ float corner_w(const f2v* wc, int c) { return (c & 1) ? wc[c >> 1].y : wc[c >> 1].x; }
+
 // Byte offsets (from the table base) of the 8 corner rows of the cell holding
 // (ux, uy, uz) and their trilinear weights, corner c = bit d <-> axis d
 // (gridencoder.cu:168-201).  Built from per-axis terms: 4 multiplies per
@@ -172,10 +188,19 @@ __device__ __forceinline__ void corner_rows(const LevelDesc& d, float ux, float 
 #pragma unroll
         for (int c = 0; c < 8; ++c) off[c] = (xy[c & 3] + ((c & 4) ? z1 : z0)) * RB;
     }
-    const float wx0 = 1.0f - fx, wy0 = 1.0f - fy, wz0 = 1.0f - fz;
-    const float wxy[4] = {wx0 * wy0, fx * wy0, wx0 * fy, fx * fy};
+    if constexpr (C == 2) {
+        f2v wc[4];
+        corner_weights_pk(fx, fy, fz, wc);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) w[c] = wxy[c & 3] * ((c & 4) ? fz : wz0);
+        for (int c = 0; c < 8; ++c) w[c] = corner_w(wc, c);
+    } else {
+        // scalar products for the C = 8 fallback of k_sgrid_box4: the packed
+        // form shifts its register allocation into spills in the sample loop
+        const float wx0 = 1.0f - fx, wy0 = 1.0f - fy, wz0 = 1.0f - fz;
+        const float wxy[4] = {wx0 * wy0, fx * wy0, wx0 * fy, fx * fy};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) w[c] = wxy[c & 3] * ((c & 4) ? fz : wz0);
+    }
 }
 
 // Trilinear lookup of one level (D = 3, linear interpolation, no
@@ -215,14 +240,14 @@ __device__ __forceinline__ void lookup_dense_c2_paired(const float* __restrict__
     f4a8 v[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) v[p] = *reinterpret_cast<const f4a8*>(base + pr[p] * 8u);
-    const float wx0 = 1.0f - fx, wy0 = 1.0f - fy, wz0 = 1.0f - fz;
-    const float wxy[4] = {wx0 * wy0, fx * wy0, wx0 * fy, fx * fy};
+    f2v wc[4];
+    corner_weights_pk(fx, fy, fz, wc);
     f2v a = {0.0f, 0.0f};
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         const f4a8& q = v[c >> 1];              // pair (y, z) = (c >> 1 & 1, c >> 2)
         const f2v e = (c & 1) ? f2v{q.z, q.w} : f2v{q.x, q.y};
-        const float w = wxy[c & 3] * ((c & 4) ? fz : wz0);
+        const float w = corner_w(wc, c);
         a = __builtin_elementwise_fma(f2v{w, w}, e, a);
     }
     acc[0] = a.x;

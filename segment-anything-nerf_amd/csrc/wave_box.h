@@ -272,19 +272,15 @@ __device__ __forceinline__ void lookup_level3_pbox(const float* __restrict__ emb
     off[5] = off[4] + DX;
     off[6] = off[4] + DY;
     off[7] = off[6] + DX;
-    // the corner weights of lookup_level3 (wxy[c & 3] * (c & 4 ? fz : 1 - fz)),
-    // two per packed multiply
-    const float wx0 = 1.0f - fx, wy0 = 1.0f - fy, wz0 = 1.0f - fz;
-    const f2v xw = {wx0, fx};
-    const f2v wxy01 = xw * f2v{wy0, wy0}, wxy23 = xw * f2v{fy, fy};
-    const f2v wc[4] = {wxy01 * f2v{wz0, wz0}, wxy23 * f2v{wz0, wz0}, wxy01 * f2v{fz, fz}, wxy23 * f2v{fz, fz}};
+    f2v wc[4];
+    corner_weights_pk(fx, fy, fz, wc);
     const char* sb = reinterpret_cast<const char*>(slice);
     f2v a[C / 2];
 #pragma unroll
     for (int i = 0; i < C / 2; ++i) a[i] = f2v{0.0f, 0.0f};
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        const float w = (c & 1) ? wc[c >> 1].y : wc[c >> 1].x;
+        const float w = corner_w(wc, c);
         const f2v wv = {w, w};
         if constexpr (C == 2) {
             const float2 v = *reinterpret_cast<const float2*>(sb + off[c]);
