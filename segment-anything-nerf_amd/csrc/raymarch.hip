@@ -1021,8 +1021,8 @@ k_final(FinalArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            h1a[i] = fmaxf(h1a[i], 0.0f);
-            h1b[i] = fmaxf(h1b[i], 0.0f);
+            h1a[i] = relu_bits(h1a[i]);
+            h1b[i] = relu_bits(h1b[i]);
         }
         floatx16 h2a = {}, h2b = {};
         if constexpr (EXACT) {
@@ -1051,8 +1051,8 @@ k_final(FinalArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            h2a[i] = fmaxf(h2a[i], 0.0f);
-            h2b[i] = fmaxf(h2b[i], 0.0f);
+            h2a[i] = relu_bits(h2a[i]);
+            h2b[i] = relu_bits(h2b[i]);
         }
         floatx16 o3 = {};
         if constexpr (EXACT) {
@@ -1117,12 +1117,12 @@ k_final(FinalArgs a) {
 #pragma unroll
             for (int s2 = 0; s2 < 8; ++s2) p1 = MFMA32(Vl[kV1 + (8 + s2) * 64 + lane], sh[2 * s2 + hh], p1);
 #pragma unroll
-            for (int q = 0; q < 16; ++q) p1[q] = fmaxf(p1[q], 0.0f);
+            for (int q = 0; q < 16; ++q) p1[q] = relu_bits(p1[q]);
             floatx16 p2 = {};
 #pragma unroll
             for (int q = 0; q < 16; ++q) p2 = MFMA32(Vl[kV2 + q * 64 + lane], p1[q], p2);
 #pragma unroll
-            for (int q = 0; q < 16; ++q) p2[q] = fmaxf(p2[q], 0.0f);
+            for (int q = 0; q < 16; ++q) p2[q] = relu_bits(p2[q]);
             floatx16 p3 = {};
 #pragma unroll
             for (int q = 0; q < 16; ++q) p3 = MFMA32(Vl[kV3 + q * 64 + lane], p2[q], p3);
@@ -1206,12 +1206,12 @@ k_final(FinalArgs a) {
 #pragma unroll
         for (int s = 0; s < 8; ++s) v1 = MFMA32(Vl[kV1 + (8 + s) * 64 + lane], sh[2 * s + hh] * ws, v1);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v1[i] = fmaxf(v1[i], 0.0f);
+        for (int i = 0; i < 16; ++i) v1[i] = relu_bits(v1[i]);
         floatx16 v2 = {};
 #pragma unroll
         for (int q = 0; q < 16; ++q) v2 = MFMA32(Vl[kV2 + q * 64 + lane], v1[q], v2);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v2[i] = fmaxf(v2[i], 0.0f);
+        for (int i = 0; i < 16; ++i) v2[i] = relu_bits(v2[i]);
 #pragma unroll
         for (int q = 0; q < 16; ++q) v3 = MFMA32(Vl[kV3 + q * 64 + lane], v2[q], v3);
     }

@@ -74,6 +74,15 @@ __device__ __forceinline__ float clamp_med3(float p, float top) {
     return __builtin_amdgcn_fmed3f(p, 0.0f, top);
 }
 
+// ReLU as one v_max_i32 on the float's bits: fmaxf(x, 0) on an MFMA
+// accumulator (not known to be canonical) costs a canonicalising v_max first
+// (and LLVM turns med3(x, 0, inf) back into that).  Same value as fmaxf for
+// every non-NaN x (negative and -0.0 -> +0.0); a positive NaN passes through,
+// as in torch.relu.
+__device__ __forceinline__ float relu_bits(float x) {
+    return __int_as_float(max(__float_as_int(x), 0));
+}
+
 // The same with the level's float resolution precomputed: frac = p -
 // floorf(p) is p - (float)cell exactly (p in [0, res - 1], res < 2^24).
 __device__ __forceinline__ void locate_axis(float u, const LevelDesc& d, uint32_t& cell, float& frac) {

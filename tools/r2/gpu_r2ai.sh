@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B on one box: previous commit's library (tools/diag/lib/prev.so) vs the tree's
+# A/B on one box: previous commit (tools/diag/lib/prev.so) vs the tree (ReLU on float bits)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_render.py tests/test_gpu_fullview.py tests/test_gpu_train.py tests/test_gpu_mask.py tests/test_gpu_n1.py tests/test_perturb.py tests/test_gpu_encoders.py > gpurun_out/r2ai_tests.log 2>&1; rc=$?
