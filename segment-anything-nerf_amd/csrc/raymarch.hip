@@ -747,13 +747,12 @@ __device__ __forceinline__ void gather_finish_c2(const GatherC2<NL>& g, float* f
             f[2 * l] = acc.x;
             f[2 * l + 1] = acc.y;
         } else {
+            f2v wc[4];
+            corner_weights_pk(g.fx[l], g.fy[l], g.fz[l], wc);
             float f0 = 0.0f, f1 = 0.0f;
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
-                const float wx = (c & 1) ? g.fx[l] : 1.0f - g.fx[l];
-                const float wy = (c & 2) ? g.fy[l] : 1.0f - g.fy[l];
-                const float wz = (c & 4) ? g.fz[l] : 1.0f - g.fz[l];
-                const float w = (wx * wy) * wz;
+                const float w = corner_w(wc, c);
                 f0 = __builtin_fmaf(w, g.e[l][c].x, f0);
                 f1 = __builtin_fmaf(w, g.e[l][c].y, f1);
             }
