@@ -297,6 +297,42 @@ int samnerf_head_train_backward(const samnerf_model* model, const float* rows,
                                 float* grad_ln_b, void* workspace, size_t workspace_bytes,
                                 samnerf_stream_t stream);
 
+/* One RGB training step (Trainer.train_step's RGB branch, nerf/utils.py:897-937,
+ * over NeRFRenderer.run in train mode, nerf/renderer.py:221-362): the render of
+ * N rays (perturbed when model->perturb is set, as the reference trains), the loss
+ * MSE(image, gt) + lambda_proposal * proposal_loss (renderer.py:30-57, when
+ * update_proposal) + lambda_distort * distort_loss (renderer.py:17-27, the
+ * eff_distloss form) + lambda_entropy * entropy(weights_sum) (utils.py:926-929),
+ * and its gradient w.r.t. every trained tensor -- what loss.backward() leaves in
+ * .grad.  RGB models only (no SAM / mask head, sum_after_mlp off).  fp32.
+ *   gt_rgb [N,3] (already composited on the background); image [N,3], depth [N],
+ *   weights_sum [N] the render's outputs; loss [5] (device): mse, proposal,
+ *   distortion, entropy (the unweighted means) and the total.
+ *   Gradients are OVERWRITTEN (zero-filled first); with update_proposal == 0 (or
+ *   lambda_proposal == 0) the proposal gradients are not touched and may be NULL
+ *   (the reference computes no gradient for them then).
+ * Replaces the ~350-op forward and the autograd backward of the torch path. */
+typedef struct {
+    float lambda_proposal;        /* main.py:106, default 1 */
+    float lambda_distort;         /* main.py:108, default 0.02 */
+    float lambda_entropy;         /* main.py:100, default 0 */
+    int update_proposal;          /* utils.py:912-913 */
+    float bg_color;               /* scalar background (1 for 'last_sample') */
+} samnerf_rgb_train_opts;
+typedef struct {
+    float* grid;                  /* grid.embeddings [rows,2] */
+    float* grid_mlp[3];           /* [64,32] [64,64] [16,64] */
+    float* view_mlp[3];           /* [32,31] [32,32] [3,32] */
+    float* prop[2];               /* prop_encoders.{0,1}.embeddings */
+    float* prop_mlp[2][2];        /* [16,10] [1,16] each */
+} samnerf_rgb_grads;
+size_t samnerf_rgb_train_workspace_size(const samnerf_model* model, uint32_t N);
+int samnerf_rgb_train_step(const samnerf_model* model, const float* rays_o, const float* rays_d,
+                           uint32_t N, const float* cam_near_far, uint32_t n_cnf, const float* gt_rgb,
+                           const samnerf_rgb_train_opts* opts, float* image, float* depth,
+                           float* weights_sum, float* loss, const samnerf_rgb_grads* grads,
+                           void* workspace, size_t workspace_bytes, samnerf_stream_t stream);
+
 /* Transport record of the per-ray outputs for the all-gather of a
  * ray-sharded view (samnerf_amd/dist.py; no reference counterpart: the
  * reference renders on one GPU, nerf/renderer.py:185-219).  One record of

@@ -1945,6 +1945,71 @@ int make_grid_desc(const samnerf_grid& g, uint32_t C, uint32_t L, GridDesc<16>& 
 
 }  // namespace
 
+// The proposal stages of a training render (rgb_train.hip): the same kernels
+// as samnerf_render_forward's stages 0 and 1, ray order (no tiling), writing
+// every intermediate the RGB backward reads to the caller's buffers.
+namespace samnerf {
+
+int train_geometry(const samnerf_model* m, TrainGeometry& g) {
+    int rc;
+    GridDesc<16> d;
+    if ((rc = make_grid_desc(m->grid, 2, 16, d, "grid"))) return rc;
+    g.grid = d;
+    for (int p = 0; p < 2; ++p) {
+        if ((rc = make_grid_desc(m->prop[p], 2, 5, d, p ? "prop_encoders.1" : "prop_encoders.0")))
+            return rc;
+        g.prop[p] = d;
+    }
+    const GridScale gs = make_grid_scale(m->grid_bound);
+    g.bound = gs.bound;
+    g.b2 = gs.b2;
+    g.inv_b2 = gs.inv_b2;
+    return SAMNERF_OK;
+}
+
+int proposal_forward(const samnerf_model* m, const TrainGeometry& g, const float* rays_o,
+                     const float* rays_d, uint32_t N, const float* cnf, uint32_t n_cnf,
+                     const ProposalOut& o, hipStream_t s) {
+    PropArgs pa{};
+    pa.rays_o = rays_o;
+    pa.rays_d = rays_d;
+    pa.cnf = cnf;
+    pa.N = N;
+    pa.tiles = RayTiles{0u, 0u};
+    pa.n_cnf = n_cnf;
+    for (int i = 0; i < 6; ++i) pa.aabb[i] = m->aabb[i];
+    pa.min_near = m->min_near;
+    pa.gs = make_grid_scale(m->grid_bound);
+    pa.snf = o.snf;
+    pa.grid = g.prop[0];
+    pa.W0 = m->prop_mlp[0][0];
+    pa.W1 = m->prop_mlp[0][1];
+    pa.bins0 = make_lin(0.0f, 1.0f, 129);
+    pa.u = make_lin((float)(0.5 / 65), (float)(1.0 - 0.5 / 65), 65);
+    pa.pbins0 = m->perturb[0];
+    pa.pu = m->perturb[1];
+    pa.bins_out = o.bins1;
+    pa.wtmp = o.ds0;
+    pa.w_out = o.w0;
+    k_snf<<<div_up(N, 256), 256, 0, s>>>(pa);
+    launch_prop_sigma<128, true>(kLookPacked, N, s, pa);
+    k_prop_pdf<128, 65, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
+    pa.grid = g.prop[1];
+    pa.W0 = m->prop_mlp[1][0];
+    pa.W1 = m->prop_mlp[1][1];
+    pa.u = make_lin((float)(0.5 / 33), (float)(1.0 - 0.5 / 33), 33);
+    pa.pu = m->perturb[2];
+    pa.bins_in = o.bins1;
+    pa.bins_out = o.bins2;
+    pa.wtmp = o.ds1;
+    pa.w_out = o.w1;
+    launch_prop_sigma<64, false>(kLookPacked, N, s, pa);
+    k_prop_pdf<64, 33, false><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
+    return check_launch("proposal_forward");
+}
+
+}  // namespace samnerf
+
 extern "C" {
 
 int samnerf_get_rays(const float* pose, float fx, float fy, float cx, float cy, uint32_t H,

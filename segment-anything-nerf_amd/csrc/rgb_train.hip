@@ -1,0 +1,1023 @@
+// rgb_train.hip -- one RGB training step of the reference's Trainer
+// (nerf/utils.py:897-937: render with perturb=True and update_proposal, MSE +
+// lambda_proposal * proposal_loss + lambda_distort * distort_loss (+
+// lambda_entropy * entropy), backward) as gfx950 kernels: the forward keeps
+// what the backward needs, the backward is written out by hand -- no autograd
+// graph, no [N, T, C] temporaries, ~17 launches instead of the ~700 ATen
+// kernels of the torch path (nerf/renderer.py run_torch + autograd).
+//
+// Forward
+//   proposal stages     the fused render's own kernels (raymarch.hip
+//                       proposal_forward): ds, weights and bins of both stages
+//   k_rt_final_fwd      one thread per final sample: bins -> position ->
+//                       contract -> grid L16C2 gather -> grid_mlp (exact fp32,
+//                       weights in LDS); saves u, grid features, both hidden
+//                       layers and the 16 outputs
+//   k_rt_composite      one thread per ray: compositing (renderer.py:309-335),
+//                       SH(4), f_image, view_mlp, sigmoid, background; the
+//                       per-ray loss terms (MSE, distortion, entropy)
+// Backward
+//   k_rt_final_bwd_ray  per ray: loss -> image -> view_mlp -> f_image ->
+//                       weights (+ distortion, entropy, background terms) ->
+//                       delta*sigma (reverse scan) -> trunc_exp -> d(grid_mlp out)
+//   k_rt_final_bwd      per sample: grid_mlp backward, d(grid features) scattered
+//                       into grid.embeddings' gradient (float atomics, as
+//                       kernel_grid_backward, gridencoder.cu:252-349)
+//   k_rt_prop_ray<T>    per ray and stage: proposal_loss (renderer.py:30-57)
+//                       w.r.t. the stage's weights (the final stage's are
+//                       detached), then the stage's compositing backward
+//   k_rt_prop_bwd<T>    per proposal sample: prop_mlp backward + prop grid scatter
+//   k_rt_outer          weight gradients dW = sum_s dY[:, s] X[:, s]^T (split-K,
+//                       LDS tiles, one atomic per output and chunk)
+//   k_rt_loss           the loss terms, fixed-order reductions
+// Arithmetic is fp32 throughout (the reference's precision); the forward
+// repeats the fused render's op order (bins, positions, gathers, compositing),
+// so its proposal stages are bit-identical to samnerf_render_forward's.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "raymarch_device.h"
+#include "samnerf_common.h"
+#include "sh_device.h"
+#include "wave_box.h"
+
+using namespace samnerf;
+
+namespace {
+
+constexpr int kT = 32;                                    // final samples per ray
+constexpr int kG0 = 64 * 32, kG1 = 64 * 64, kG2 = 16 * 64; // grid_mlp [64,32] [64,64] [16,64]
+constexpr int kGW = kG0 + kG1 + kG2;
+constexpr int kV1 = 32 * 31, kV2 = kV1 + 32 * 32, kVW = kV2 + 3 * 32;   // view_mlp in LDS
+
+// torch.linspace(start, end, steps) on the CPU (samnerf_linspace_host; the
+// same formula as raymarch.hip's stage-0 bins)
+struct LinSpace {
+    float start, end, step;
+    uint32_t steps;
+    __device__ __forceinline__ float operator()(int j) const {
+        return (uint32_t)j < steps / 2u ? __builtin_fmaf(step, (float)j, start)
+                                        : __builtin_fmaf(-step, (float)(steps - 1u - j), end);
+    }
+};
+
+LinSpace make_linspace(float start, float end, uint32_t steps) {
+    LinSpace l;
+    l.start = start;
+    l.end = end;
+    l.steps = steps;
+    l.step = steps > 1 ? (end - start) / (float)(steps - 1u) : 0.0f;
+    return l;
+}
+
+struct RtArgs {
+    const float* rays_o;
+    const float* rays_d;
+    uint32_t N;
+    float bound, b2, inv_b2;
+    float bg;
+    GridDesc<16> grid;
+    const float* G[3];        // grid_mlp
+    const float* V[3];        // view_mlp
+    const float* snf;         // [2][N]
+    const float* bins2;       // [33][N]
+    const float* gt;          // [N][3]
+    float c_mse, c_dist, c_ent;   // 2 / (3N), lambda_distort / N, lambda_entropy / N
+    // per final sample s = 32 r + k (ray-major): [channel][S], S = 32 N
+    float* pos;               // [3] grid-space u
+    float* feat;              // [32] grid features
+    float* h1;                // [64] relu(G0 feat)
+    float* h2;                // [64] relu(G1 h1)
+    float* out;               // [16] G2 h2: sigma pre-activation, geo_feat
+    float* delta;             // [1] real_bins[k+1] - real_bins[k]
+    float* tmid;              // [1] rays_t
+    float* dout;              // [16]
+    float* dh1;               // [64]
+    float* dh2;               // [64]
+    // per ray: [channel][N]
+    float* w;                 // [32] final weights
+    float* fimg;              // [31] f_image
+    float* v1;                // [32] view_mlp hidden
+    float* v2;                // [32]
+    float* sig;               // [3] sigmoid(view_mlp)
+    float* dz;                // [3]
+    float* dv1;               // [32]
+    float* dv2;               // [32]
+    float* terms;             // [4]: mse (sum of 3), proposal, distortion, entropy
+    float* image;             // [N][3]
+    float* depth;             // [N]
+    float* wsum;              // [N]
+    float* grad_grid;         // [rows][2]
+};
+
+__device__ __forceinline__ float grid_u(const RtArgs& a, float x) {
+    return a.inv_b2 != 0.0f ? (x + a.bound) * a.inv_b2 : (x + a.bound) / a.b2;
+}
+
+__device__ __forceinline__ void load_grid_mlp(const RtArgs& a, float* sw) {
+    for (int i = threadIdx.x; i < kG0; i += blockDim.x) sw[i] = a.G[0][i];
+    for (int i = threadIdx.x; i < kG1; i += blockDim.x) sw[kG0 + i] = a.G[1][i];
+    for (int i = threadIdx.x; i < kG2; i += blockDim.x) sw[kG0 + kG1 + i] = a.G[2][i];
+    __syncthreads();
+}
+
+// Scatter one sample's d(features) of a C = 2 level into the gradient table
+// (kernel_grid_backward's atomics, gridencoder.cu:252-349).  Float atomics
+// execute at the memory side, priced per 64-B request (MI355X_MICROARCH.md
+// "Global float atomics": 64 lanes in 64 rows is ~17x slower than 256
+// contiguous bytes), so the per-sample kernels run ray-major -- a wave is 64
+// consecutive samples of two rays, neighbours in space -- and the adds are
+// shaped before they leave:
+//  (1) runs of equal rows in consecutive lanes (consecutive samples of a ray
+//      often share cells) are summed by a segmented scan and the run's last
+//      lane adds the sum;
+//  (2) the corners c and c + 1 (x and x + 1) sit in one 64-B segment 7 times in
+//      8 on dense AND hashed levels (x ^ (x + 1) only flips low bits), so a quad
+//      of lanes emits one sample's corner pair -- both channels of both rows,
+//      16 bytes, one request -- through a per-wave LDS transpose, instead of one
+//      channel of 64 rows per instruction.
+// Every lane of the wave must call it (live = false past the end); `stage` is
+// the wave's 384-float LDS slice.
+__device__ __forceinline__ void scatter_level_c2(float* __restrict__ gtab, const LevelDesc& d, float ux,
+                                                 float uy, float uz, float g0, float g1, bool live,
+                                                 float* stage) {
+    uint32_t off[8];
+    float cw[8];
+    corner_rows<2>(d, ux, uy, uz, off, cw);
+    const uint32_t lane = threadIdx.x & 63u, j = lane & 3u, quad = lane & ~3u;
+    float4* sv = reinterpret_cast<float4*>(stage);             // [lane] 4 values
+    uint2* so = reinterpret_cast<uint2*>(stage + 256);         // [lane] 2 row offsets
+    constexpr uint32_t kDead = 0xFFFFFFFFu;
+#pragma unroll
+    for (int c = 0; c < 8; c += 2) {
+        float v[4];
+        uint32_t o[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            o[h] = off[c + h];
+            float v0 = cw[c + h] * g0, v1 = cw[c + h] * g1;
+            // runs of equal rows in consecutive lanes (samples along a ray)
+            // summed by a segmented scan; the run's last lane keeps the sum
+            const uint32_t po = __shfl_up(o[h], 1);
+            const bool pl = __shfl_up((int)live, 1) != 0;
+            bool seg = lane == 0u || !live || !pl || po != o[h];   // run head
+            const bool head = seg;
+#pragma unroll
+            for (uint32_t sd = 1; sd < 64u; sd <<= 1) {
+                const float a0 = __shfl_up(v0, sd), a1 = __shfl_up(v1, sd);
+                const bool af = __shfl_up((int)seg, sd) != 0;
+                if (lane >= sd && !seg) {
+                    v0 += a0;
+                    v1 += a1;
+                    seg = af;
+                }
+            }
+            const bool next_head = __shfl_down((int)head, 1) != 0;
+            const bool alive = live && (lane == 63u || next_head);
+            v[2 * h] = v0;
+            v[2 * h + 1] = v1;
+            if (!alive) o[h] = kDead;
+        }
+        sv[lane] = make_float4(v[0], v[1], v[2], v[3]);
+        so[lane] = make_uint2(o[0], o[1]);
+        wave_lds_sync();
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t src = quad | q;
+            const float val = stage[src * 4u + j];
+            const uint32_t oo = reinterpret_cast<const uint32_t*>(so)[src * 2u + (j >> 1)];
+            if (oo != kDead) atomicAdd(gtab + (oo >> 2) + (j & 1u), val);
+        }
+        wave_lds_sync();
+    }
+}
+
+// ------------------------------------------------------------- forward --
+
+// One thread per final sample, ray-major (s = 32 r + k).
+// renderer.py:278-286 (bins -> position -> contract), network.py:221-229
+// (grid -> grid_mlp; trunc_exp is applied by the compositing kernel).
+__global__ void __launch_bounds__(256) k_rt_final_fwd(RtArgs a) {
+    __shared__ float sw[kGW];
+    load_grid_mlp(a, sw);
+    const uint32_t N = a.N;
+    const size_t S = (size_t)kT * N, s = (size_t)blockIdx.x * 256u + threadIdx.x;
+    if (s >= S) return;
+    const uint32_t r = (uint32_t)(s / kT), k = (uint32_t)(s % kT);
+    const size_t ks = (size_t)k * N + r;
+    float o[3], d[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        o[c] = a.rays_o[(size_t)r * 3 + c];
+        d[c] = a.rays_d[(size_t)r * 3 + c];
+    }
+    const float sn = a.snf[r], sf = a.snf[N + r];
+    const float rbp = real_bin(sn, sf, a.bins2[ks]), rbn = real_bin(sn, sf, a.bins2[ks + N]);
+    const float t = (rbn + rbp) / 2.0f;
+    float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
+    contract3(x, y, z);
+    const float ux = grid_u(a, x), uy = grid_u(a, y), uz = grid_u(a, z);
+    a.pos[s] = ux;
+    a.pos[S + s] = uy;
+    a.pos[2 * S + s] = uz;
+    a.delta[s] = rbn - rbp;
+    a.tmid[s] = t;
+    float f[32];
+#pragma unroll
+    for (int l = 0; l < 16; ++l) lookup_level3_ref<2>(a.grid.emb, a.grid.lv[l], ux, uy, uz, f + 2 * l);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) a.feat[i * S + s] = f[i];
+    float h[64];
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) acc = __builtin_fmaf(sw[q * 32 + i], f[i], acc);
+        h[q] = fmaxf(acc, 0.0f);
+        a.h1[q * S + s] = h[q];
+    }
+#pragma unroll 4
+    for (int q = 0; q < 64; ++q) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 64; ++i) acc = __builtin_fmaf(sw[kG0 + q * 64 + i], h[i], acc);
+        a.h2[q * S + s] = fmaxf(acc, 0.0f);
+    }
+    float h2v[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) h2v[i] = a.h2[i * S + s];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 64; ++i) acc = __builtin_fmaf(sw[kG0 + kG1 + q * 64 + i], h2v[i], acc);
+        a.out[q * S + s] = acc;
+    }
+}
+
+// SH(4) of the ray's direction, normalised twice (renderer.py:295 and
+// sphere_harmonics.py:79-82), as k_final
+__device__ __forceinline__ void ray_sh(const RtArgs& a, uint32_t r, float* sh) {
+    float dx = a.rays_d[(size_t)r * 3], dy = a.rays_d[(size_t)r * 3 + 1], dz = a.rays_d[(size_t)r * 3 + 2];
+    normalize3(dx, dy, dz);
+    normalize3(dx, dy, dz);
+    sh_values<4>(dx, dy, dz, sh);
+}
+
+// One thread per ray: renderer.py:309-358 (last_sample background) plus the
+// per-ray loss terms of utils.py:917-931.
+__global__ void __launch_bounds__(256) k_rt_composite(RtArgs a) {
+    const uint32_t N = a.N, r = blockIdx.x * 256u + threadIdx.x;
+    if (r >= N) return;
+    const size_t S = (size_t)kT * N;
+    double cum = 0.0, wsd = 0.0, dep = 0.0;
+    float fg[15];
+#pragma unroll
+    for (int j = 0; j < 15; ++j) fg[j] = 0.0f;
+    float W = 0.0f, WM = 0.0f, bi = 0.0f, uni = 0.0f;     // distortion (renderer.py:17-27)
+    float b0 = a.bins2[r];
+#pragma unroll 2
+    for (int k = 0; k < kT; ++k) {
+        const size_t s = (size_t)r * kT + k, ks = (size_t)k * N + r;
+        const float sigma = expf(a.out[s]);                 // trunc_exp forward
+        const float w = composite_step(a.delta[s] * sigma, cum, k == kT - 1);
+        a.w[ks] = w;
+        wsd += (double)w;
+        dep += (double)(w * a.tmid[s]);
+#pragma unroll
+        for (int j = 0; j < 15; ++j) fg[j] = fg[j] + w * a.out[(size_t)(1 + j) * S + s];
+        const float b1 = a.bins2[ks + N];
+        const float iv = b1 - b0, mid = b0 + iv / 2.0f;
+        b0 = b1;
+        uni = uni + iv * (w * w);
+        const float wm = w * mid;
+        if (k > 0) bi = bi + (wm * W - w * WM);
+        W = W + w;
+        WM = WM + wm;
+    }
+    const float ws = (float)wsd;
+    float sh[16];
+    ray_sh(a, r, sh);
+    float fi[31];
+#pragma unroll
+    for (int j = 0; j < 15; ++j) fi[j] = fg[j];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) fi[15 + j] = sh[j] * ws;
+#pragma unroll
+    for (int j = 0; j < 31; ++j) a.fimg[(size_t)j * N + r] = fi[j];
+    float v1[32], v2[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 31; ++i) acc = __builtin_fmaf(a.V[0][q * 31 + i], fi[i], acc);
+        v1[q] = fmaxf(acc, 0.0f);
+        a.v1[(size_t)q * N + r] = v1[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) acc = __builtin_fmaf(a.V[1][q * 32 + i], v1[i], acc);
+        v2[q] = fmaxf(acc, 0.0f);
+        a.v2[(size_t)q * N + r] = v2[q];
+    }
+    float mse = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) acc = __builtin_fmaf(a.V[2][c * 32 + i], v2[i], acc);
+        const float sg = sigmoidf(acc);
+        a.sig[(size_t)c * N + r] = sg;
+        const float img = sg + (1.0f - ws) * a.bg;
+        a.image[(size_t)r * 3 + c] = img;
+        const float e = img - a.gt[(size_t)r * 3 + c];
+        mse = mse + e * e;
+    }
+    a.depth[r] = (float)dep;
+    a.wsum[r] = ws;
+    const float we = fminf(fmaxf(ws, 1e-5f), 1.0f - 1e-5f);
+    a.terms[r] = mse;
+    a.terms[N + r] = 0.0f;
+    a.terms[2 * N + r] = 2.0f * bi + uni / 3.0f;
+    a.terms[3 * N + r] = -we * log2f(we) - (1.0f - we) * log2f(1.0f - we);
+}
+
+// ------------------------------------------------------------ backward --
+
+// One thread per ray (64 per block): d(loss) -> d(image) -> view_mlp ->
+// f_image -> weights -> delta*sigma -> d(grid_mlp output) of every final
+// sample.  The per-sample terms of the reverse scan live in LDS ([k][lane]:
+// no bank conflicts), not in 96 registers.
+__global__ void __launch_bounds__(64) k_rt_final_bwd_ray(RtArgs a) {
+    __shared__ float sdw[kT][64], sraw[kT][64], sev[kT][64];
+    __shared__ float sv[kVW];
+    for (int i = threadIdx.x; i < 32 * 31; i += 64) sv[i] = a.V[0][i];
+    for (int i = threadIdx.x; i < 32 * 32; i += 64) sv[kV1 + i] = a.V[1][i];
+    for (int i = threadIdx.x; i < 3 * 32; i += 64) sv[kV2 + i] = a.V[2][i];
+    __syncthreads();
+    const uint32_t N = a.N, lane = threadIdx.x, r = blockIdx.x * 64u + lane;
+    if (r >= N) return;
+    const size_t S = (size_t)kT * N;
+    const float ws = a.wsum[r];
+    float dimg[3], dz[3], dws = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        dimg[c] = a.c_mse * (a.image[(size_t)r * 3 + c] - a.gt[(size_t)r * 3 + c]);
+        dws = dws - dimg[c] * a.bg;                         // image += (1 - weights_sum) * bg
+        const float sg = a.sig[(size_t)c * N + r];
+        dz[c] = dimg[c] * (1.0f - sg) * sg;                 // sigmoid backward
+        a.dz[(size_t)c * N + r] = dz[c];
+    }
+    if (a.c_ent != 0.0f && ws >= 1e-5f && ws <= 1.0f - 1e-5f)   // clamp passes the gradient inside
+        dws = dws + a.c_ent * (log2f(1.0f - ws) - log2f(ws));
+    // transposed products as row sweeps (W^T g = sum_q g_q W[q, :]), the same
+    // ascending-q accumulation order per output
+    float dv2[32], dv1[32], dfi[31];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) dv2[i] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int i = 0; i < 32; ++i) dv2[i] = __builtin_fmaf(sv[kV2 + c * 32 + i], dz[c], dv2[i]);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        dv2[i] = a.v2[(size_t)i * N + r] > 0.0f ? dv2[i] : 0.0f;
+        a.dv2[(size_t)i * N + r] = dv2[i];
+        dv1[i] = 0.0f;
+    }
+#pragma unroll 2
+    for (int q = 0; q < 32; ++q)
+#pragma unroll
+        for (int i = 0; i < 32; ++i) dv1[i] = __builtin_fmaf(sv[kV1 + q * 32 + i], dv2[q], dv1[i]);
+#pragma unroll
+    for (int i = 0; i < 31; ++i) dfi[i] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        dv1[i] = a.v1[(size_t)i * N + r] > 0.0f ? dv1[i] : 0.0f;
+        a.dv1[(size_t)i * N + r] = dv1[i];
+    }
+#pragma unroll 2
+    for (int q = 0; q < 32; ++q)
+#pragma unroll
+        for (int j = 0; j < 31; ++j) dfi[j] = __builtin_fmaf(sv[q * 31 + j], dv1[q], dfi[j]);
+    float sh[16];
+    ray_sh(a, r, sh);
+    float shdot = 0.0f;                                     // d f_image[15:] / d w_k = sh
+#pragma unroll
+    for (int j = 0; j < 16; ++j) shdot = __builtin_fmaf(dfi[15 + j], sh[j], shdot);
+    // distortion totals (suffix sums below)
+    float Wt = 0.0f, WMt = 0.0f;
+    if (a.c_dist != 0.0f)
+        for (int k = 0; k < kT; ++k) {
+            const size_t ks = (size_t)k * N + r;
+            const float b0 = a.bins2[ks], b1 = a.bins2[ks + N], iv = b1 - b0, w = a.w[ks];
+            Wt = Wt + w;
+            WMt = WMt + w * (b0 + iv / 2.0f);
+        }
+    // forward pass: transmittance, raw weights, d(loss)/d(w_k)
+    double cum = 0.0;
+    float W = 0.0f, WM = 0.0f;
+#pragma unroll 1
+    for (int k = 0; k < kT; ++k) {
+        const size_t s = (size_t)r * kT + k, ks = (size_t)k * N + r;
+        const float ds = k == kT - 1 ? INFINITY : a.delta[s] * expf(a.out[s]);
+        const float e = expf(-ds), T = expf(-(float)cum);
+        cum += (double)ds;
+        const float raw = (1.0f - e) * T;
+        const float w = nan_to_num(raw);
+        float g = shdot + dws;
+#pragma unroll
+        for (int j = 0; j < 15; ++j) {
+            const size_t q = (size_t)(1 + j) * S + s;
+            g = __builtin_fmaf(dfi[j], a.out[q], g);
+            a.dout[q] = w * dfi[j];
+        }
+        if (a.c_dist != 0.0f) {
+            const float b0 = a.bins2[ks], b1 = a.bins2[ks + N], iv = b1 - b0, m = b0 + iv / 2.0f;
+            W = W + w;
+            WM = WM + w * m;
+            // d/dw_k [2 sum_i sum_{j<i} w_i w_j (m_i - m_j) + 1/3 sum_i s_i w_i^2]
+            const float before = m * (W - w) - (WM - w * m);
+            const float after = (WMt - WM) - m * (Wt - W);
+            g = __builtin_fmaf(a.c_dist, 2.0f * (before + after) + (2.0f / 3.0f) * iv * w, g);
+        }
+        const bool fin = isfinite(raw);                     // nan_to_num_ backward
+        sdw[k][lane] = fin ? g : 0.0f;
+        sraw[k][lane] = fin ? raw : 0.0f;
+        sev[k][lane] = e * T;
+    }
+    // reverse pass: d(ds_j) = dw_j e^-ds_j T_j - sum_{k>j} dw_k raw_k; the last
+    // sample's ds is the constant +inf
+    float acc = 0.0f;
+#pragma unroll 1
+    for (int k = kT - 1; k >= 0; --k) {
+        const size_t s = (size_t)r * kT + k;
+        float dx = 0.0f;
+        if (k < kT - 1) {
+            const float dds = sdw[k][lane] * sev[k][lane] - acc;
+            const float x = a.out[s];
+            dx = (dds * a.delta[s]) * expf(fminf(fmaxf(x, -15.0f), 15.0f));   // trunc_exp backward
+        }
+        acc = __builtin_fmaf(sdw[k][lane], sraw[k][lane], acc);
+        a.dout[s] = dx;
+    }
+}
+
+// One thread per final sample: grid_mlp backward (ReLU masks from the saved
+// activations) and the grid scatter.
+__global__ void __launch_bounds__(256) k_rt_final_bwd(RtArgs a) {
+    __shared__ float sw[kGW];
+    __shared__ float sstage[4][384];
+    float* stage = sstage[threadIdx.x >> 6];
+    load_grid_mlp(a, sw);
+    const uint32_t N = a.N;
+    const size_t S = (size_t)kT * N, s0 = (size_t)blockIdx.x * 256u + threadIdx.x;
+    if ((s0 & ~(size_t)63) >= S) return;                    // whole wave past the end
+    const bool live = s0 < S;                               // other lanes stay for the merges
+    const size_t s = live ? s0 : S - 1u;
+    float dy[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dy[q] = a.dout[q * S + s];
+    float g2[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc = __builtin_fmaf(sw[kG0 + kG1 + q * 64 + i], dy[q], acc);
+        g2[i] = a.h2[i * S + s] > 0.0f ? acc : 0.0f;
+        if (live) a.dh2[i * S + s] = g2[i];
+    }
+    float g1[64];
+#pragma unroll 4
+    for (int i = 0; i < 64; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 64; ++q) acc = __builtin_fmaf(sw[kG0 + q * 64 + i], g2[q], acc);
+        g1[i] = a.h1[i * S + s] > 0.0f ? acc : 0.0f;
+        if (live) a.dh1[i * S + s] = g1[i];
+    }
+    const float ux = a.pos[s], uy = a.pos[S + s], uz = a.pos[2 * S + s];
+#pragma unroll 1
+    for (int l = 0; l < 16; ++l) {
+        float df0 = 0.0f, df1 = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 64; ++q) {
+            df0 = __builtin_fmaf(sw[q * 32 + 2 * l], g1[q], df0);
+            df1 = __builtin_fmaf(sw[q * 32 + 2 * l + 1], g1[q], df1);
+        }
+        scatter_level_c2(a.grad_grid, a.grid.lv[l], ux, uy, uz, df0, df1, live, stage);
+    }
+}
+
+// dW[m][n] += sum_{s in chunk} A[i * S + s] * B[j * S + s] for m, n <= 64: a
+// block owns the whole m x n output for its chunk of samples (each operand row
+// read once), 32-sample LDS tiles stored k-major, a 4 x 4 register tile per
+// thread (16 FMAs per 8 LDS reads).  Each block stores its partial m x n sum
+// in a slab row and k_rt_outer_sum adds the rows in block order: float
+// atomics from every block into the same few KB serialise at the memory side
+// (0.2 ms per call measured), and this way the weight gradients are bitwise
+// reproducible.
+__host__ __device__ constexpr uint32_t outer_chunk(size_t S) {
+    // about 1,024 blocks (4 per CU: latency hiding for the dependent loads),
+    // chunks of at least 256 samples, a multiple of the 32-sample tile
+    return (uint32_t)(((S + 1023) / 1024 + 255) / 256 * 256);
+}
+
+__global__ void __launch_bounds__(256) k_rt_outer(const float* __restrict__ A, const float* __restrict__ B,
+                                                  uint32_t m, uint32_t n, size_t S, uint32_t chunk,
+                                                  float* __restrict__ slab) {
+    __shared__ float4 As[32][17], Bs[32][17];              // [k][i / 4], one float4 of padding
+    const uint32_t tid = threadIdx.x, ti = tid >> 4, tj = tid & 15u;
+    const size_t s0 = (size_t)blockIdx.x * chunk;
+    const size_t s1 = s0 + chunk < S ? s0 + chunk : S;
+    float acc[4][4] = {};
+    float* as = reinterpret_cast<float*>(As);
+    float* bs = reinterpret_cast<float*>(Bs);
+    // 64 rows x 32 samples of each operand per tile: lane -> (row, sample),
+    // the sample fastest (128-B row segments); the next tile's loads are in
+    // flight while this one is multiplied
+    float pa[8], pb[8];
+    auto fetch = [&](size_t sb) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t idx = tid + 256u * q, row = idx >> 5, kk = idx & 31u;
+            const size_t sc = sb + kk;
+            pa[q] = (row < m && sc < s1) ? A[(size_t)row * S + sc] : 0.0f;
+            pb[q] = (row < n && sc < s1) ? B[(size_t)row * S + sc] : 0.0f;
+        }
+    };
+    fetch(s0);
+    for (size_t sb = s0; sb < s1; sb += 32) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t idx = tid + 256u * q, row = idx >> 5, kk = idx & 31u;
+            as[kk * 68 + row] = pa[q];
+            bs[kk * 68 + row] = pb[q];
+        }
+        __syncthreads();
+        if (sb + 32 < s1) fetch(sb + 32);
+#pragma unroll 8
+        for (int k = 0; k < 32; ++k) {
+            const float4 x = As[k][ti], y = Bs[k][tj];
+            const float xa[4] = {x.x, x.y, x.z, x.w}, ya[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_fmaf(xa[i], ya[j], acc[i][j]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t oi = ti * 4u + i, oj = tj * 4u + j;
+            if (oi < m && oj < n) slab[(size_t)blockIdx.x * m * n + (size_t)oi * n + oj] = acc[i][j];
+        }
+}
+
+// out[e] = sum over slab rows in a fixed order: 16 outputs x 16 row groups per
+// block, the groups combined in order through LDS
+__global__ void __launch_bounds__(256) k_rt_outer_sum(const float* __restrict__ slab, uint32_t mn,
+                                                      uint32_t blocks, float* __restrict__ out) {
+    __shared__ float part[16][17];
+    const uint32_t tid = threadIdx.x, eo = tid & 15u, g = tid >> 4, e = blockIdx.x * 16u + eo;
+    float acc = 0.0f;
+    if (e < mn) {
+#pragma unroll 8
+        for (uint32_t b = g; b < blocks; b += 16u) acc += slab[(size_t)b * mn + e];
+    }
+    part[g][eo] = acc;
+    __syncthreads();
+    if (g == 0 && e < mn) {
+        float t = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t += part[q][eo];
+        out[e] = t;
+    }
+}
+
+struct PropBwdArgs {
+    const float* rays_o;
+    const float* rays_d;
+    uint32_t N;
+    float bound, b2, inv_b2;
+    GridDesc<16> grid;        // prop_encoders[stage]
+    const float* P0;          // [16,10]
+    const float* P1;          // [1,16]
+    const float* snf;
+    LinSpace bins0;           // stage 0, perturb off
+    const float* pbins0;      // stage 0, perturb on: [N][129]
+    const float* bins_in;     // stage 1: [65][N]
+    const float* ws;          // [T][N] the stage's weights
+    const float* ds;          // [T][N] its delta * sigma
+    const float* bins2;       // [33][N] final bins (detached)
+    const float* wf;          // [32][N] final weights (detached)
+    float c_prop;             // lambda_proposal / (32 N)
+    float* dds;               // [T][N]
+    float* terms;             // [4][N] (row 1 accumulates the proposal loss)
+    // per sample s = T r + k: [channel][T N]
+    float* dh;                // [16]
+    float* feat;              // [10]
+    float* h;                 // [16]
+    float* dx;                // [1]
+    float* grad_grid;         // [rows][2]
+};
+
+template <int T, bool FIRST>
+__device__ __forceinline__ float stage_bin_t(const PropBwdArgs& a, int i, uint32_t r) {
+    if constexpr (FIRST) return a.pbins0 ? a.pbins0[(size_t)r * (T + 1) + i] : a.bins0(i);
+    else return a.bins_in[(size_t)i * a.N + r];
+}
+
+// torch.searchsorted(arr[0..n), v, right=True) by the binary search of ATen's
+// kernels (cus_upper_bound): the same index even where arr is not sorted
+template <class F>
+__device__ __forceinline__ int upper_bound_t(int n, float v, F arr) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = lo + ((hi - lo) >> 1);
+        if (!(v < arr(mid))) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// One thread per ray (32 rays per block): loss_interlevel(bins_ref, w_ref,
+// bins, w) of renderer.py:35-49 and its gradient w.r.t. the stage weights
+// (w = cw1[hi + 1] - cw1[lo] is a signed range sum: a difference array), then
+// the stage's compositing backward (the same reverse scan as the final stage).
+template <int T, bool FIRST>
+__global__ void __launch_bounds__(32) k_rt_prop_ray(PropBwdArgs a) {
+    __shared__ float Cw[32][T + 2];
+    __shared__ float D[32][T + 2];
+    const uint32_t N = a.N, r = blockIdx.x * 32u + threadIdx.x;
+    if (r >= N) return;
+    float* cw = Cw[threadIdx.x];
+    float* dd = D[threadIdx.x];
+    float c = 0.0f;
+    cw[0] = 0.0f;
+    for (int j = 0; j < T; ++j) {
+        c = c + a.ws[(size_t)j * N + r];
+        cw[j + 1] = c;
+        dd[j] = 0.0f;
+    }
+    dd[T] = 0.0f;
+    float loss = 0.0f;
+    for (int i = 0; i < kT; ++i) {
+        const float t0lo = a.bins2[(size_t)i * N + r], t0hi = a.bins2[(size_t)(i + 1) * N + r];
+        int lo = upper_bound_t(T, t0lo, [&](int q) { return stage_bin_t<T, FIRST>(a, q, r); }) - 1;
+        int hi = upper_bound_t(T, t0hi, [&](int q) { return stage_bin_t<T, FIRST>(a, q + 1, r); });
+        lo = min(max(lo, 0), T - 1);
+        hi = min(max(hi, 0), T - 1);
+        const float w = cw[hi + 1] - cw[lo];
+        const float w0 = a.wf[(size_t)i * N + r];
+        const float x = w0 - w;
+        if (x > 0.0f) {
+            const float den = w0 + 1e-8f;
+            loss = loss + (x * x) / den;
+            const float g = -2.0f * x / den * a.c_prop;
+            dd[lo] += g;
+            dd[hi + 1] -= g;
+        }
+    }
+    a.terms[N + r] += loss / (float)kT;
+    // compositing backward: cw <- dw_j * raw_j, dd <- dw_j * e^-ds_j T_j
+    double cum = 0.0;
+    float run = 0.0f;
+    for (int j = 0; j < T; ++j) {
+        run = run + dd[j];
+        const float ds = j == T - 1 ? INFINITY : a.ds[(size_t)j * N + r];
+        const float e = expf(-ds), Tj = expf(-(float)cum);
+        cum += (double)ds;
+        const float raw = (1.0f - e) * Tj;
+        const float dw = isfinite(raw) ? run : 0.0f;
+        cw[j] = isfinite(raw) ? dw * raw : 0.0f;
+        dd[j] = dw * (e * Tj);
+    }
+    float acc = 0.0f;
+    for (int j = T - 1; j >= 0; --j) {
+        a.dds[(size_t)j * N + r] = j < T - 1 ? dd[j] - acc : 0.0f;
+        acc = acc + cw[j];
+    }
+}
+
+// One thread per proposal sample, ray-major (s = T r + k): the density network of
+// the stage (network.py:248-259) re-evaluated, then its backward.
+template <int T, bool FIRST>
+__global__ void __launch_bounds__(256) k_rt_prop_bwd(PropBwdArgs a) {
+    __shared__ float sstage[4][384];
+    float* stage = sstage[threadIdx.x >> 6];
+    const uint32_t N = a.N;
+    const size_t S = (size_t)T * N, s0 = (size_t)blockIdx.x * 256u + threadIdx.x;
+    if ((s0 & ~(size_t)63) >= S) return;                    // whole wave past the end
+    const bool live = s0 < S;                               // other lanes stay for the merges
+    const size_t s = live ? s0 : S - 1u;                    // ray-major: s = T r + k
+    const uint32_t r = (uint32_t)(s / T), k = (uint32_t)(s % T);
+    float o[3], d[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        o[c] = a.rays_o[(size_t)r * 3 + c];
+        d[c] = a.rays_d[(size_t)r * 3 + c];
+    }
+    const float sn = a.snf[r], sf = a.snf[N + r];
+    const float rbp = real_bin(sn, sf, stage_bin_t<T, FIRST>(a, (int)k, r));
+    const float rbn = real_bin(sn, sf, stage_bin_t<T, FIRST>(a, (int)k + 1, r));
+    const float t = (rbn + rbp) / 2.0f;
+    float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
+    contract3(x, y, z);
+    auto gu = [&](float v) { return a.inv_b2 != 0.0f ? (v + a.bound) * a.inv_b2 : (v + a.bound) / a.b2; };
+    const float ux = gu(x), uy = gu(y), uz = gu(z);
+    float f[10];
+#pragma unroll
+    for (int l = 0; l < 5; ++l) lookup_level3_ref<2>(a.grid.emb, a.grid.lv[l], ux, uy, uz, f + 2 * l);
+    float h[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) acc = __builtin_fmaf(a.P0[q * 10 + i], f[i], acc);
+        h[q] = fmaxf(acc, 0.0f);
+    }
+    float sv = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sv = __builtin_fmaf(a.P1[i], h[i], sv);
+    const float dsig = a.dds[(size_t)k * N + r] * (rbn - rbp);
+    const float dx = dsig * expf(fminf(fmaxf(sv, -15.0f), 15.0f));
+    float dh[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dh[q] = h[q] > 0.0f ? a.P1[q] * dx : 0.0f;
+    float df[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc = __builtin_fmaf(a.P0[q * 10 + i], dh[q], acc);
+        df[i] = acc;
+    }
+    if (live) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            a.dh[q * S + s] = dh[q];
+            a.h[q * S + s] = h[q];
+        }
+#pragma unroll
+        for (int i = 0; i < 10; ++i) a.feat[i * S + s] = f[i];
+        a.dx[s] = dx;
+    }
+#pragma unroll
+    for (int l = 0; l < 5; ++l)
+        scatter_level_c2(a.grad_grid, a.grid.lv[l], ux, uy, uz, df[2 * l], df[2 * l + 1], live, stage);
+}
+
+// loss[0..3] = mse, proposal, distortion, entropy (means, fixed-order sums in
+// double); loss[4] = the total of utils.py:917-931.
+__global__ void __launch_bounds__(256) k_rt_loss(const float* terms, uint32_t N, float lp, float ld, float le,
+                                                 int with_prop, float* loss) {
+    __shared__ double red[256];
+    for (int t = 0; t < 4; ++t) {
+        double acc = 0.0;
+        for (uint32_t r = threadIdx.x; r < N; r += 256u) acc += (double)terms[(size_t)t * N + r];
+        red[threadIdx.x] = acc;
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) loss[t] = (float)(red[0] / (double)N / (t == 0 ? 3.0 : 1.0));
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        float total = loss[0];
+        if (with_prop && lp > 0.0f) total = total + lp * loss[1];
+        if (ld > 0.0f) total = total + ld * loss[2];
+        if (le > 0.0f) total = total + le * loss[3];
+        loss[4] = total;
+    }
+}
+
+struct RtWorkspace {
+    ProposalOut p;
+    float* dds0;
+    float* dds1;
+    float* fin[10];          // pos feat h1 h2 out delta tmid dout dh1 dh2
+    float* ray[10];          // w fimg v1 v2 sig dz dv1 dv2 terms (+ spare)
+    float* prop[4];          // dh feat h dx (stage 0 size, reused by stage 1)
+    float* slab;             // k_rt_outer partial sums
+    size_t bytes;
+};
+
+constexpr int kFinCh[10] = {3, 32, 64, 64, 16, 1, 1, 16, 64, 64};
+constexpr int kRayCh[10] = {32, 31, 32, 32, 3, 3, 32, 32, 4, 1};
+constexpr int kPropCh[4] = {16, 10, 16, 1};
+
+RtWorkspace carve_rt(uint32_t N, void* base) {
+    RtWorkspace w{};
+    char* p = static_cast<char*>(base);
+    size_t off = 0;
+    auto take = [&](size_t floats) {
+        float* q = base ? reinterpret_cast<float*>(p + off) : nullptr;
+        off += (floats * sizeof(float) + 255) & ~(size_t)255;
+        return q;
+    };
+    const size_t n = N;
+    w.p.snf = take(2 * n);
+    w.p.ds0 = take(128 * n);
+    w.p.w0 = take(128 * n);
+    w.p.bins1 = take(65 * n);
+    w.p.ds1 = take(64 * n);
+    w.p.w1 = take(64 * n);
+    w.p.bins2 = take(33 * n);
+    w.dds0 = take(128 * n);
+    w.dds1 = take(64 * n);
+    for (int i = 0; i < 10; ++i) w.fin[i] = take((size_t)kFinCh[i] * kT * n);
+    for (int i = 0; i < 10; ++i) w.ray[i] = take((size_t)kRayCh[i] * n);
+    for (int i = 0; i < 4; ++i) w.prop[i] = take((size_t)kPropCh[i] * 128 * n);
+    // the largest slab: grid_mlp.1 (64 x 64) over 32 N samples, or a proposal
+    // MLP (16 x 10) over 128 N
+    const size_t sf = (size_t)kT * n, sp = (size_t)128 * n;
+    const size_t sb = std::max((size_t)div_up(sf, outer_chunk(sf)) * 4096,
+                               (size_t)div_up(sp, outer_chunk(sp)) * 160);
+    w.slab = take(sb);
+    w.bytes = off;
+    return w;
+}
+
+// out[m][n] = sum_s A[:, s] B[:, s]^T (overwritten); slab >= blocks * m * n floats
+void outer(const float* A, const float* B, uint32_t m, uint32_t n, size_t S, float* out, float* slab,
+           hipStream_t s) {
+    const uint32_t chunk = outer_chunk(S), blocks = div_up(S, chunk);
+    k_rt_outer<<<blocks, 256, 0, s>>>(A, B, m, n, S, chunk, slab);
+    k_rt_outer_sum<<<div_up(m * n, 16), 256, 0, s>>>(slab, m * n, blocks, out);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t samnerf_rgb_train_workspace_size(const samnerf_model* model, uint32_t N) {
+    if (!model) return 0;
+    return carve_rt(N, nullptr).bytes;
+}
+
+int samnerf_rgb_train_step(const samnerf_model* m, const float* rays_o, const float* rays_d, uint32_t N,
+                           const float* cam_near_far, uint32_t n_cnf, const float* gt_rgb,
+                           const samnerf_rgb_train_opts* opts, float* image, float* depth,
+                           float* weights_sum, float* loss, const samnerf_rgb_grads* grads,
+                           void* workspace, size_t workspace_bytes, samnerf_stream_t stream) {
+    if (!m || !opts || !grads) return fail(SAMNERF_EINVAL, "rgb_train_step: null pointer");
+    if (N == 0) return SAMNERF_OK;
+    if (!rays_o || !rays_d || !gt_rgb || !image || !depth || !weights_sum || !loss)
+        return fail(SAMNERF_EINVAL, "rgb_train_step: null pointer");
+    if (m->num_steps[0] != 128 || m->num_steps[1] != 64 || m->num_steps[2] != 32)
+        return fail(SAMNERF_EINVAL, "rgb_train_step: built for num_steps = [128, 64, 32]");
+    if (m->with_sam || m->with_mask || m->sum_after_mlp)
+        return fail(SAMNERF_EINVAL, "rgb_train_step: RGB models only (no SAM / mask head, no sum_after_mlp; "
+                    "renderer.py:348 adds the training losses only then)");
+    if (cam_near_far && n_cnf != 1 && n_cnf != N)
+        return fail(SAMNERF_EINVAL, "rgb_train_step: cam_near_far must have 1 or N rows");
+    if (!m->perturb[0] != !m->perturb[1] || !m->perturb[0] != !m->perturb[2])
+        return fail(SAMNERF_EINVAL, "rgb_train_step: perturb needs all three position arrays or none");
+    if ((uint64_t)N * 128u >= (1ull << 31)) return fail(SAMNERF_EINVAL, "rgb_train_step: too many rays");
+    for (int i = 0; i < 3; ++i)
+        if (!m->grid_mlp[i] || !m->view_mlp[i] || !grads->grid_mlp[i] || !grads->view_mlp[i])
+            return fail(SAMNERF_EINVAL, "rgb_train_step: null MLP weight or gradient");
+    if (!grads->grid) return fail(SAMNERF_EINVAL, "rgb_train_step: null grid gradient");
+    const bool with_prop = opts->update_proposal && opts->lambda_proposal > 0.0f;
+    if (with_prop)
+        for (int p = 0; p < 2; ++p)
+            if (!grads->prop[p] || !grads->prop_mlp[p][0] || !grads->prop_mlp[p][1])
+                return fail(SAMNERF_EINVAL, "rgb_train_step: null proposal gradient");
+    RtWorkspace w = carve_rt(N, workspace);
+    if (!workspace || workspace_bytes < w.bytes)
+        return fail(SAMNERF_EWORKSPACE, "rgb_train_step: workspace needs %zu bytes, got %zu", w.bytes,
+                    workspace_bytes);
+    TrainGeometry geo;
+    int rc = train_geometry(m, geo);
+    if (rc) return rc;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+
+    // gradients are overwritten: the grid tables are zero-filled and scattered
+    // into (torch accumulates into zeroed .grad), the MLP weights' written whole
+    // by k_rt_outer_sum
+    auto zero = [&](float* p, size_t floats) { return hipMemsetAsync(p, 0, floats * sizeof(float), s); };
+    bool ok = zero(grads->grid, (size_t)m->grid.offsets_host[16] * 2) == hipSuccess;
+    if (with_prop)
+        for (int p = 0; p < 2; ++p)
+            ok = ok && zero(grads->prop[p], (size_t)m->prop[p].offsets_host[5] * 2) == hipSuccess;
+    if (!ok) return fail(SAMNERF_ELAUNCH, "rgb_train_step: gradient zero-fill failed");
+
+    // forward: proposal stages (the render's kernels), final samples, compositing
+    if ((rc = proposal_forward(m, geo, rays_o, rays_d, N, cam_near_far, n_cnf, w.p, s))) return rc;
+    RtArgs a{};
+    a.rays_o = rays_o;
+    a.rays_d = rays_d;
+    a.N = N;
+    a.bound = geo.bound;
+    a.b2 = geo.b2;
+    a.inv_b2 = geo.inv_b2;
+    a.bg = opts->bg_color;
+    a.grid = geo.grid;
+    for (int i = 0; i < 3; ++i) {
+        a.G[i] = m->grid_mlp[i];
+        a.V[i] = m->view_mlp[i];
+    }
+    a.snf = w.p.snf;
+    a.bins2 = w.p.bins2;
+    a.gt = gt_rgb;
+    a.c_mse = (float)(2.0 / (3.0 * N));
+    a.c_dist = opts->lambda_distort > 0.0f ? (float)(opts->lambda_distort / (double)N) : 0.0f;
+    a.c_ent = opts->lambda_entropy > 0.0f ? (float)(opts->lambda_entropy / (double)N) : 0.0f;
+    a.pos = w.fin[0];
+    a.feat = w.fin[1];
+    a.h1 = w.fin[2];
+    a.h2 = w.fin[3];
+    a.out = w.fin[4];
+    a.delta = w.fin[5];
+    a.tmid = w.fin[6];
+    a.dout = w.fin[7];
+    a.dh1 = w.fin[8];
+    a.dh2 = w.fin[9];
+    a.w = w.ray[0];
+    a.fimg = w.ray[1];
+    a.v1 = w.ray[2];
+    a.v2 = w.ray[3];
+    a.sig = w.ray[4];
+    a.dz = w.ray[5];
+    a.dv1 = w.ray[6];
+    a.dv2 = w.ray[7];
+    a.terms = w.ray[8];
+    a.image = image;
+    a.depth = depth;
+    a.wsum = weights_sum;
+    a.grad_grid = grads->grid;
+    const uint32_t gs = div_up((uint64_t)kT * N, 256);
+    k_rt_final_fwd<<<gs, 256, 0, s>>>(a);
+    k_rt_composite<<<div_up(N, 256), 256, 0, s>>>(a);
+
+    // backward: final stage
+    k_rt_final_bwd_ray<<<div_up(N, 64), 64, 0, s>>>(a);
+    k_rt_final_bwd<<<gs, 256, 0, s>>>(a);
+    const size_t S = (size_t)kT * N;
+    outer(a.dh1, a.feat, 64, 32, S, grads->grid_mlp[0], w.slab, s);
+    outer(a.dh2, a.h1, 64, 64, S, grads->grid_mlp[1], w.slab, s);
+    outer(a.dout, a.h2, 16, 64, S, grads->grid_mlp[2], w.slab, s);
+    outer(a.dv1, a.fimg, 32, 31, N, grads->view_mlp[0], w.slab, s);
+    outer(a.dv2, a.v1, 32, 32, N, grads->view_mlp[1], w.slab, s);
+    outer(a.dz, a.v2, 3, 32, N, grads->view_mlp[2], w.slab, s);
+
+    // backward: proposal stages (proposal_loss only; bins are detached)
+    if (with_prop) {
+        PropBwdArgs pb{};
+        pb.rays_o = rays_o;
+        pb.rays_d = rays_d;
+        pb.N = N;
+        pb.bound = geo.bound;
+        pb.b2 = geo.b2;
+        pb.inv_b2 = geo.inv_b2;
+        pb.snf = w.p.snf;
+        pb.bins0 = make_linspace(0.0f, 1.0f, 129);
+        pb.pbins0 = m->perturb[0];
+        pb.bins2 = w.p.bins2;
+        pb.wf = a.w;
+        pb.c_prop = (float)(opts->lambda_proposal / (32.0 * N));
+        pb.terms = a.terms;
+        pb.dh = w.prop[0];
+        pb.feat = w.prop[1];
+        pb.h = w.prop[2];
+        pb.dx = w.prop[3];
+        // stage 0: 128 samples on the linspace / perturbed bins
+        pb.grid = geo.prop[0];
+        pb.P0 = m->prop_mlp[0][0];
+        pb.P1 = m->prop_mlp[0][1];
+        pb.ws = w.p.w0;
+        pb.ds = w.p.ds0;
+        pb.dds = w.dds0;
+        pb.grad_grid = grads->prop[0];
+        k_rt_prop_ray<128, true><<<div_up(N, 32), 32, 0, s>>>(pb);
+        k_rt_prop_bwd<128, true><<<div_up((uint64_t)128 * N, 256), 256, 0, s>>>(pb);
+        outer(pb.dh, pb.feat, 16, 10, (size_t)128 * N, grads->prop_mlp[0][0], w.slab, s);
+        outer(pb.dx, pb.h, 1, 16, (size_t)128 * N, grads->prop_mlp[0][1], w.slab, s);
+        // stage 1: 64 samples on stage 0's resampled bins
+        pb.grid = geo.prop[1];
+        pb.P0 = m->prop_mlp[1][0];
+        pb.P1 = m->prop_mlp[1][1];
+        pb.bins_in = w.p.bins1;
+        pb.ws = w.p.w1;
+        pb.ds = w.p.ds1;
+        pb.dds = w.dds1;
+        pb.grad_grid = grads->prop[1];
+        k_rt_prop_ray<64, false><<<div_up(N, 32), 32, 0, s>>>(pb);
+        k_rt_prop_bwd<64, false><<<div_up((uint64_t)64 * N, 256), 256, 0, s>>>(pb);
+        outer(pb.dh, pb.feat, 16, 10, (size_t)64 * N, grads->prop_mlp[1][0], w.slab, s);
+        outer(pb.dx, pb.h, 1, 16, (size_t)64 * N, grads->prop_mlp[1][1], w.slab, s);
+    }
+    k_rt_loss<<<1, 256, 0, s>>>(a.terms, N, opts->lambda_proposal, opts->lambda_distort, opts->lambda_entropy,
+                                with_prop ? 1 : 0, loss);
+    return check_launch("rgb_train_step");
+}
+
+}  // extern "C"

@@ -54,6 +54,30 @@ struct GridDesc {
     LevelDesc lv[MAXL];
 };
 
+// What the RGB training step (rgb_train.hip) takes from the fused render
+// (raymarch.hip): the model's grids resolved as the render resolves them, the
+// grid-space scale, and the proposal stages run by the render's own kernels
+// with their intermediates written to the caller's buffers (sample-major
+// [k][N], ray order).
+struct TrainGeometry {
+    GridDesc<16> grid;         // L16 C2
+    GridDesc<16> prop[2];      // L5 C2
+    float bound, b2, inv_b2;   // u = (x + bound) * inv_b2, or / b2 when inv_b2 == 0
+};
+struct ProposalOut {
+    float* snf;                // [2][N] spacing(near), spacing(far)
+    float* ds0;                // [128][N] delta * sigma of stage 0
+    float* w0;                 // [128][N] its composited weights
+    float* bins1;              // [65][N] resampled bins
+    float* ds1;                // [64][N]
+    float* w1;                 // [64][N]
+    float* bins2;              // [33][N] the final stage's bins
+};
+int train_geometry(const samnerf_model* m, TrainGeometry& g);
+int proposal_forward(const samnerf_model* m, const TrainGeometry& g, const float* rays_o,
+                     const float* rays_d, uint32_t N, const float* cnf, uint32_t n_cnf,
+                     const ProposalOut& o, hipStream_t s);
+
 // ------------------------------------------------------------ device math --
 
 // pos = clamp(fma(u, res, -0.5), 0, res-1); cell = floor; frac = pos - cell.

@@ -74,6 +74,9 @@ _SIGS = {
     "samnerf_set_stage_events": ([ctypes.POINTER(_vp), _u32], _int),
     "samnerf_set_taps": ([ctypes.c_void_p, _u32], _int),
     "samnerf_adam_step": ([ctypes.c_void_p, _u32, _f64, _f64, _f64, _f64, _f64, _u32, _vp], _int),
+    "samnerf_rgb_train_workspace_size": ([ctypes.POINTER(SamnerfModel), _u32], _sz),
+    "samnerf_rgb_train_step": ([ctypes.POINTER(SamnerfModel), _vp, _vp, _u32, _vp, _u32, _vp,
+                                ctypes.c_void_p, _vp, _vp, _vp, _vp, ctypes.c_void_p, _vp, _sz, _vp], _int),
     "samnerf_head_train_workspace_size": ([_u32], _sz),
     "samnerf_head_train_forward": ([ctypes.POINTER(SamnerfModel), _vp, _u32, _vp, _vp, _sz, _vp], _int),
     "samnerf_head_train_backward": ([ctypes.POINTER(SamnerfModel), _vp, _vp, _u32, _vp,
@@ -92,6 +95,18 @@ class SamnerfTaps(ctypes.Structure):
     """samnerf_taps (include/samnerf_hip.h): parity-test taps of the render."""
     _fields_ = [("ds0", _vp), ("ds1", _vp), ("w0", _vp), ("w1", _vp), ("bins1", _vp),
                 ("bins2", _vp), ("inds1", _vp), ("inds2", _vp)]
+
+
+class SamnerfRgbTrainOpts(ctypes.Structure):
+    """samnerf_rgb_train_opts (include/samnerf_hip.h)."""
+    _fields_ = [("lambda_proposal", _f32), ("lambda_distort", _f32), ("lambda_entropy", _f32),
+                ("update_proposal", _int), ("bg_color", _f32)]
+
+
+class SamnerfRgbGrads(ctypes.Structure):
+    """samnerf_rgb_grads (include/samnerf_hip.h)."""
+    _fields_ = [("grid", _vp), ("grid_mlp", _vp * 3), ("view_mlp", _vp * 3), ("prop", _vp * 2),
+                ("prop_mlp", (_vp * 2) * 2)]
 
 
 EXPORTED = tuple(_SIGS)

@@ -48,6 +48,112 @@ def rgb_train_step(model, rays_o, rays_d, gt_rgb, global_step, bg_color=None,
     return pred_rgb, loss, outputs
 
 
+def _rgb_grad_params(model):
+    """The trained tensors in samnerf_rgb_grads order, and which of them are the
+    proposal networks' (network.py:201-206 get_params groups)."""
+    main = [model.grid.embeddings] + [model.grid_mlp.net[i].weight for i in range(3)] + \
+        [model.view_mlp.net[i].weight for i in range(3)]
+    prop = [model.prop_encoders[0].embeddings, model.prop_encoders[1].embeddings] + \
+        [model.prop_mlp[p].net[i].weight for p in range(2) for i in range(2)]
+    return main, prop
+
+
+def rgb_train_step_fused(model, rays_o, rays_d, gt_rgb, global_step, bg_color=None,
+                         cam_near_far=None, perturb=True):
+    """rgb_train_step on the HIP training kernels (samnerf_rgb_train_step,
+    csrc/rgb_train.hip): one C call renders the rays (the reference's perturbed
+    sampling, drawn with torch's generator in its order), forms the loss of
+    utils.py:917-931 and writes every trained tensor's gradient into .grad --
+    what loss.backward() leaves there (the proposal tensors' .grad is None on
+    the steps the reference does not update them, utils.py:912-913).  Returns
+    (pred_rgb, loss, outputs) like rgb_train_step; loss is a detached 0-d
+    tensor, outputs holds image / depth / weights_sum / num_points and the
+    unweighted loss terms."""
+    import ctypes
+
+    from ._lib import SamnerfRgbGrads, SamnerfRgbTrainOpts, check, lib
+    from .fused import FusedRenderer, perturbed_positions
+    from .ops import _ptr, _stream
+
+    opt = model.opt
+    if bg_color is None:
+        bg_color = 1
+    if gt_rgb.shape[-1] == 4:
+        gt_rgb = gt_rgb[..., :3] * gt_rgb[..., 3:] + bg_color * (1 - gt_rgb[..., 3:])
+    if torch.is_tensor(bg_color):
+        if bg_color.numel() != 1:
+            raise NotImplementedError("fused RGB step: per-ray background colours")
+        bg_color = float(bg_color)
+    update_proposal = update_proposal_now(global_step, opt.with_sam)
+    rays_o = rays_o.contiguous().float()
+    rays_d = rays_d.contiguous().float()
+    gt = gt_rgb.reshape(-1, 3).contiguous().float()
+    N = rays_o.shape[0]
+    dev = rays_o.device
+    fr = getattr(model, "_fused_train", None)
+    if fr is None or fr.net is not model:
+        fr = model._fused_train = FusedRenderer(model, head_mode=1)
+    m = fr.model()
+    m.view_width = 0
+    m.with_mask = 0
+    pert = None
+    if isinstance(perturb, (tuple, list)) or perturb:
+        pert = tuple(perturb) if isinstance(perturb, (tuple, list)) else \
+            perturbed_positions(N, list(m.num_steps), dev)
+        pert = tuple(t.contiguous().float() for t in pert)
+    for i in range(3):
+        m.perturb[i] = ctypes.c_void_p(pert[i].data_ptr()) if pert is not None else None
+    o = SamnerfRgbTrainOpts()
+    o.lambda_proposal = float(getattr(opt, "lambda_proposal", 0.0))
+    o.lambda_distort = float(getattr(opt, "lambda_distort", 0.0))
+    o.lambda_entropy = float(getattr(opt, "lambda_entropy", 0.0))
+    o.update_proposal = int(bool(update_proposal))
+    o.bg_color = float(bg_color)
+    with_prop = bool(update_proposal) and o.lambda_proposal > 0
+    main, prop = _rgb_grad_params(model)
+    for p in main + (prop if with_prop else []):
+        if p.grad is None or p.grad.shape != p.shape or not p.grad.is_contiguous():
+            p.grad = torch.empty_like(p)
+    if not with_prop:
+        for p in prop:
+            p.grad = None
+    g = SamnerfRgbGrads()
+    g.grid = main[0].grad.data_ptr()
+    for i in range(3):
+        g.grid_mlp[i] = main[1 + i].grad.data_ptr()
+        g.view_mlp[i] = main[4 + i].grad.data_ptr()
+    if with_prop:
+        g.prop[0], g.prop[1] = prop[0].grad.data_ptr(), prop[1].grad.data_ptr()
+        for q in range(2):
+            for i in range(2):
+                g.prop_mlp[q][i] = prop[2 + 2 * q + i].grad.data_ptr()
+    need = lib().samnerf_rgb_train_workspace_size(ctypes.byref(m), N)
+    ws = getattr(fr, "_rt_ws", None)
+    if ws is None or ws.device != dev or ws.numel() < need:
+        ws = fr._rt_ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+    cnf, n_cnf = None, 0
+    if cam_near_far is not None:
+        cnf = cam_near_far.contiguous().float()
+        n_cnf = cnf.shape[0]
+    image = torch.empty(N, 3, device=dev)
+    depth = torch.empty(N, device=dev)
+    wsum = torch.empty(N, device=dev)
+    loss = torch.empty(5, device=dev)
+    try:
+        check(lib().samnerf_rgb_train_step(
+            ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, _ptr(cnf), n_cnf, _ptr(gt),
+            ctypes.byref(o), _ptr(image), _ptr(depth), _ptr(wsum), _ptr(loss), ctypes.byref(g),
+            _ptr(ws), need, _stream(rays_o)), "rgb_train_step")
+    finally:
+        for i in range(3):
+            m.perturb[i] = None
+    outputs = {"image": image, "depth": depth, "weights_sum": wsum, "num_points": N * int(m.num_steps[2]),
+               "mse": loss[0], "proposal_loss": loss[1], "distort_loss": loss[2], "entropy": loss[3]}
+    if opt.adaptive_num_rays:
+        opt.num_rays = int(round((opt.num_points / outputs["num_points"]) * opt.num_rays))
+    return image, loss[4], outputs
+
+
 def sam_train_step(renderer, rays_o_lr, rays_d_lr, h, w, gt_samvit, cam_near_far=None):
     """utils.py:1091-1106 on the fused path: 64x64 feature rays, bilinear
     resize to the target, MSE.  Returns (pred [1,256,h',w'], loss)."""

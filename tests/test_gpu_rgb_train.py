@@ -1,0 +1,151 @@
+"""The RGB training step on the HIP training kernels (samnerf_rgb_train_step,
+csrc/rgb_train.hip; SURVEY.md 8f-2, nerf/utils.py:897-937).
+
+Checked against two references of the same step:
+  * the CPU twin -- the reference's op sequence (run_torch) with autograd on
+    the CPU and the C oracle's encoders (tests/oracle_backend.py), perturb off;
+  * the torch path on the GPU (run_torch + autograd with the drop-in encoder
+    kernels) with perturb on, both drawing the perturbed positions from the
+    same generator state.
+Tolerances: the loss terms to fp32 rounding; gradients per tensor as
+test_gpu_train.py's RGB test states them -- the density path's gradients are
+small sums of cancelling terms, so fp32 reassociation moves them ~1e-2
+relative (cosine > 0.9999 kept), every other tensor within 2e-3.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import make_net
+from oracle import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _rgb_nets(cuda, seed=12, log2=(12, 10), devices=("cuda", "cpu")):
+    spec = synth.ModelSpec(with_sam=False, grid_log2=log2[0], s_grid_log2=10, prop_log2=log2[1])
+    params = synth.make_params(spec, seed=seed, emb_scale=0.5)
+    return [make_net(spec, params, cuda if d == "cuda" else "cpu").train() for d in devices]
+
+
+def _rays(n_side, rot, cuda=None):
+    from oracle import renderer as orc
+    pose, intr = synth.gui_camera(n_side, n_side, rot=synth.random_rotation(rot))
+    ro, rd = orc.get_rays(pose, intr, n_side, n_side)
+    if cuda is not None:
+        ro, rd = ro.to(cuda), rd.to(cuda)
+    return ro, rd
+
+
+def _compare_grads(net_a, net_b, strict=2e-3, loose=2e-2):
+    worst = {}
+    for (k, pa), (_, pb) in zip(net_a.named_parameters(), net_b.named_parameters()):
+        if pb.grad is None:
+            assert pa.grad is None, k
+            continue
+        a, b = pa.grad.detach().cpu(), pb.grad.detach().cpu()
+        err = float((a - b).norm() / b.norm().clamp_min(1e-12))
+        worst[k] = err
+        if k.startswith("grid.") or k.startswith("grid_mlp."):
+            cos = float(F.cosine_similarity(a.flatten(), b.flatten(), dim=0))
+            assert err < loose and cos > 0.9999, (k, err, cos)
+        else:
+            assert err < strict, (k, err)
+    print("relative gradient errors:", {k: f"{v:.1e}" for k, v in worst.items()})
+    return worst
+
+
+def test_fused_rgb_step_matches_cpu_twin(hip_lib, cuda):
+    """perturb=False, update_proposal on (step 1): image, the four loss terms
+    and all 11 gradients against autograd of the reference's op sequence on
+    the CPU with the oracle encoders."""
+    from oracle_backend import oracle_encoders
+    from samnerf_amd.train import rgb_train_step, rgb_train_step_fused
+    gpu, cpu = _rgb_nets(cuda)
+    ro, rd = _rays(16, 6)
+    gt = torch.rand(256, 3, generator=torch.Generator().manual_seed(2))
+    img, loss, out = rgb_train_step_fused(gpu, ro.to(cuda), rd.to(cuda), gt.to(cuda), global_step=1,
+                                          perturb=False)
+    with oracle_encoders():
+        img_c, loss_c, out_c = rgb_train_step(cpu, ro, rd, gt, global_step=1, perturb=False)
+        loss_c.backward()
+    assert (img.cpu() - img_c.detach()).abs().max().item() < 1e-5
+    assert (out["weights_sum"].cpu() - out_c["weights_sum"].detach()).abs().max().item() < 1e-5
+    for k in ("proposal_loss", "distort_loss"):
+        a, b = float(out[k]), float(out_c[k])
+        assert abs(a - b) <= 1e-4 * abs(b) + 1e-8, (k, a, b)
+    assert abs(float(loss) - float(loss_c)) <= 1e-4 * abs(float(loss_c)) + 1e-7
+    _compare_grads(gpu, cpu)
+
+
+def test_fused_rgb_step_matches_torch_path_perturbed(hip_lib, cuda):
+    """perturb=True (the reference's training sampling): the fused step and the
+    torch path draw the same perturbed positions from the same seed and agree
+    on image, loss and gradients; 64 x 64 rays at the reference's table sizes
+    (grid 2^19, proposal 2^17)."""
+    from samnerf_amd.train import rgb_train_step, rgb_train_step_fused
+    a, b = _rgb_nets(cuda, seed=21, log2=(19, 17), devices=("cuda", "cuda"))
+    ro, rd = _rays(64, 3, cuda)
+    gt = torch.rand(4096, 3, generator=torch.Generator().manual_seed(5)).to(cuda)
+    torch.manual_seed(11)
+    img, loss, out = rgb_train_step_fused(a, ro, rd, gt, global_step=1)
+    torch.manual_seed(11)
+    img_t, loss_t, out_t = rgb_train_step(b, ro, rd, gt, global_step=1)
+    loss_t.backward()
+    assert (img - img_t.detach()).abs().max().item() < 1e-5
+    assert abs(float(loss) - float(loss_t)) <= 1e-4 * abs(float(loss_t)) + 1e-7
+    assert abs(float(out["proposal_loss"]) - float(out_t["proposal_loss"])) <= \
+        1e-4 * abs(float(out_t["proposal_loss"])) + 1e-8
+    _compare_grads(a, b)
+
+
+def test_fused_rgb_step_without_proposal_update(hip_lib, cuda):
+    """utils.py:912-913: after step 3000 the proposal networks train every 5th
+    step only; on the other steps their .grad stays None (no proposal loss)."""
+    from samnerf_amd.train import rgb_train_step, rgb_train_step_fused
+    a, b = _rgb_nets(cuda, seed=4, devices=("cuda", "cuda"))
+    ro, rd = _rays(16, 2, cuda)
+    gt = torch.rand(256, 3, generator=torch.Generator().manual_seed(8)).to(cuda)
+    torch.manual_seed(3)
+    _, loss, _ = rgb_train_step_fused(a, ro, rd, gt, global_step=3001)
+    torch.manual_seed(3)
+    _, loss_t, _ = rgb_train_step(b, ro, rd, gt, global_step=3001)
+    loss_t.backward()
+    assert abs(float(loss) - float(loss_t)) <= 1e-4 * abs(float(loss_t)) + 1e-7
+    assert all(p.grad is None for p in a.prop_encoders.parameters())
+    assert all(p.grad is None for p in a.prop_mlp.parameters())
+    _compare_grads(a, b)
+
+
+def test_fused_rgb_step_entropy_and_background(hip_lib, cuda):
+    """lambda_entropy > 0 (utils.py:926-929) and an RGBA target composited on the
+    background (utils.py:901-906), perturb off, against the torch path."""
+    from samnerf_amd.train import rgb_train_step, rgb_train_step_fused
+    a, b = _rgb_nets(cuda, seed=9, devices=("cuda", "cuda"))
+    for n in (a, b):
+        n.opt.lambda_entropy = 1e-3
+    ro, rd = _rays(16, 5, cuda)
+    gt = torch.rand(256, 4, generator=torch.Generator().manual_seed(1)).to(cuda)
+    _, loss, out = rgb_train_step_fused(a, ro, rd, gt, global_step=2, perturb=False)
+    _, loss_t, _ = rgb_train_step(b, ro, rd, gt, global_step=2, perturb=False)
+    loss_t.backward()
+    assert float(out["entropy"]) > 0
+    assert abs(float(loss) - float(loss_t)) <= 1e-4 * abs(float(loss_t)) + 1e-7
+    _compare_grads(a, b)
+
+
+def test_fused_rgb_training_reduces_loss(hip_lib, cuda):
+    """Eight fused steps with FusedAdam (main.py:296: Adam lr 1e-2, eps 1e-15):
+    the loss halves, as on the torch path (test_gpu_train.py)."""
+    from samnerf_amd.optim import FusedAdam
+    from samnerf_amd.train import rgb_train_step_fused
+    (net,) = _rgb_nets(cuda, seed=13, devices=("cuda",))
+    opt = FusedAdam(net.get_params(1e-2), eps=1e-15)
+    ro, rd = _rays(16, 7, cuda)
+    gt = torch.full((256, 3), 0.25, device=cuda)
+    losses = []
+    for step in range(1, 9):
+        _, loss, _ = rgb_train_step_fused(net, ro, rd, gt, global_step=step)
+        opt.step()
+        losses.append(float(loss))
+    assert losses[-1] < 0.5 * losses[0], losses
