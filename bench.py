@@ -115,7 +115,7 @@ def parse():
                     help="HIP streams the views are issued on round-robin, so view i+1's kernels "
                          "overlap view i's (each stream has its own workspace).  0 = 2 for 1-4 "
                          "ranks, 3 for 8 (one rank's 32K-ray share: +16%%)")
-    ap.add_argument("--mode", choices=["render", "train", "gui"], default="render",
+    ap.add_argument("--mode", choices=["render", "train", "gui", "rgbtrain"], default="render",
                     help="render: cfg 3 view throughput (the headline metric); train: cfg 5 "
                          "SAM-feature distillation step (4096 rays, forward + backward + Adam); "
                          "gui: the reference GUI's frame (readme.md:5) -- 512x512 RGB + 64x64 "
@@ -356,6 +356,69 @@ def train_steps(dev, steps, warmup, torch_adam=False):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return dt * 1e3 / steps, float(loss)
+
+
+def rgb_train_steps(dev, steps, warmup, fused=True, h=64, w=128):
+    """One RGB training step (utils.py:897-937, the reference's first training
+    stage): 8,192 rays -- the batch adaptive_num_rays settles on for
+    num_points = 2^18 (main.py:96, 226) -- of a parity-weight scene at the
+    reference's table sizes, perturbed sampling, MSE + proposal + distortion
+    losses, backward, Adam(lr 1e-2, eps 1e-15) over every group of get_params
+    (main.py:296).  fused: samnerf_rgb_train_step (rgb_train.hip); else the
+    torch path (run_torch + autograd with the drop-in encoder kernels).
+    Returns (ms per step, final loss)."""
+    from samnerf_amd import ops, synth
+    from samnerf_amd.optim import FusedAdam
+    from samnerf_amd.train import rgb_train_step, rgb_train_step_fused
+    net, _, _ = build_net(False, dev, seed=3, emb_scale=0.5)
+    net.train()
+    net.opt.adaptive_num_rays = False
+    opt = FusedAdam(net.get_params(1e-2), eps=1e-15)
+    pose, intr = synth.gui_camera(w, h)
+    ro, rd = ops.get_rays(pose, intr, h, w, device=dev)
+    gt = torch.rand(ro.shape[0], 3, generator=torch.Generator().manual_seed(4)).to(dev)
+
+    def step(i):
+        if fused:
+            _, loss, _ = rgb_train_step_fused(net, ro, rd, gt, global_step=1 + i)
+        else:
+            _, loss, _ = rgb_train_step(net, ro, rd, gt, global_step=1 + i)
+            for p in net.parameters():
+                p.grad = None
+            loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = step(warmup + i)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3 / steps, float(loss.detach())
+
+
+RGB_TRAIN_WHAT = {
+    "dtype": "fp32 throughout (forward in the fused render's op order, grid_mlp / view_mlp exact fp32; "
+             "hand-written backward; grid gradients by fp32 atomics)",
+    "data": "synthetic parity-weight scene (embeddings U(+-0.5)) at the reference's table sizes, "
+            "U(0,1) target colours",
+    "config": {"workload": "RGB training step (utils.py:897-937): 8192 rays (64x128), perturb, "
+                           "MSE + proposal + distortion losses, backward, Adam over all groups",
+               "optimizer": "FusedAdam lr 1e-2 eps 1e-15"},
+}
+
+
+def rgb_train_main(args, dev):
+    ms, loss = rgb_train_steps(dev, args.steps, args.warmup, fused=True)
+    ms_t, _ = rgb_train_steps(dev, max(3, args.steps // 2), 2, fused=False)
+    rec = {"metric": "RGB training steps/s (8192 rays, fwd+bwd+Adam)", "value": 1e3 / ms,
+           "unit": "steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": ms, "higher_is_better": True, "rays_per_s": 8192 * 1e3 / ms,
+           "final_loss": loss, "torch_path_ms_per_step": ms_t, "speedup_vs_torch_path": ms_t / ms,
+           **RGB_TRAIN_WHAT, "vs_baseline": None}
+    print(json.dumps(rec), flush=True)
 
 
 TRAIN_WHAT = {
@@ -599,11 +662,11 @@ def main():
     rc = maybe_launch(args)
     if rc is not None:
         sys.exit(rc)
-    if args.mode in ("train", "gui"):
+    if args.mode in ("train", "gui", "rgbtrain"):
         if args.gpus != 1:
             raise SystemExit(f"--mode {args.mode} runs on one GPU")
         torch.cuda.set_device(0)
-        fn = train_main if args.mode == "train" else gui_main
+        fn = {"train": train_main, "gui": gui_main, "rgbtrain": rgb_train_main}[args.mode]
         return fn(args, torch.device("cuda", 0))
     rank, world, dev = setup_dist(args)
     from samnerf_amd import ops
@@ -717,6 +780,16 @@ def main():
         side["cfg5_train"] = {"ms_per_step": ms5, "steps_per_s": 1e3 / ms5,
                               "rays_per_s": 4096 * 1e3 / ms5, "steps": 20, "warmup": 5,
                               "final_loss": loss5, **TRAIN_WHAT}
+
+    if not args.no_alt and world == 1 and args.rank_share <= 1:
+        # the reference's RGB training stage on the HIP training
+        # kernels, the torch path beside it
+        msr, lossr = rgb_train_steps(dev, 20, 5, fused=True)
+        msr_t, _ = rgb_train_steps(dev, 6, 2, fused=False)
+        side["rgb_train"] = {"ms_per_step": msr, "steps_per_s": 1e3 / msr, "rays_per_s": 8192 * 1e3 / msr,
+                             "steps": 20, "warmup": 5, "final_loss": lossr,
+                             "torch_path_ms_per_step": msr_t, "speedup_vs_torch_path": msr_t / msr,
+                             **RGB_TRAIN_WHAT}
 
     if rank == 0:
         rec = {
