@@ -372,6 +372,7 @@ def rgb_train_steps(dev, steps, warmup, fused=True, h=64, w=128):
     from samnerf_amd.train import rgb_train_step, rgb_train_step_fused
     net, _, _ = build_net(False, dev, seed=3, emb_scale=0.5)
     net.train()
+    net.fused = fused          # False: NeRFRenderer.run_torch under autograd
     net.opt.adaptive_num_rays = False
     opt = FusedAdam(net.get_params(1e-2), eps=1e-15)
     pose, intr = synth.gui_camera(w, h)

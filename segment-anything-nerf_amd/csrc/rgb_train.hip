@@ -82,8 +82,12 @@ struct RtArgs {
     const float* V[3];        // view_mlp
     const float* snf;         // [2][N]
     const float* bins2;       // [33][N]
-    const float* gt;          // [N][3]
-    float c_mse, c_dist, c_ent;   // 2 / (3N), lambda_distort / N, lambda_entropy / N
+    // upstream gradients of the render's outputs (the backward's inputs):
+    const float* g_img;       // [N][3] d loss / d image
+    const float* g_ws;        // [N] d loss / d weights_sum, or null
+    const float* g_depth;     // [N] d loss / d depth, or null
+    const float* g_loss;      // [2] d loss / d (proposal_loss, distort_loss) (device), or null
+    float inv_n;              // 1 / N
     // per final sample s = 32 r + k (ray-major): [channel][S], S = 32 N
     float* pos;               // [3] grid-space u
     float* feat;              // [32] grid features
@@ -323,7 +327,6 @@ __global__ void __launch_bounds__(256) k_rt_composite(RtArgs a) {
         v2[q] = fmaxf(acc, 0.0f);
         a.v2[(size_t)q * N + r] = v2[q];
     }
-    float mse = 0.0f;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         float acc = 0.0f;
@@ -331,18 +334,36 @@ __global__ void __launch_bounds__(256) k_rt_composite(RtArgs a) {
         for (int i = 0; i < 32; ++i) acc = __builtin_fmaf(a.V[2][c * 32 + i], v2[i], acc);
         const float sg = sigmoidf(acc);
         a.sig[(size_t)c * N + r] = sg;
-        const float img = sg + (1.0f - ws) * a.bg;
-        a.image[(size_t)r * 3 + c] = img;
-        const float e = img - a.gt[(size_t)r * 3 + c];
-        mse = mse + e * e;
+        a.image[(size_t)r * 3 + c] = sg + (1.0f - ws) * a.bg;
     }
     a.depth[r] = (float)dep;
     a.wsum[r] = ws;
-    const float we = fminf(fmaxf(ws, 1e-5f), 1.0f - 1e-5f);
-    a.terms[r] = mse;
     a.terms[N + r] = 0.0f;
     a.terms[2 * N + r] = 2.0f * bi + uni / 3.0f;
+}
+
+// The Trainer's own terms for the one-call step (utils.py:917, 926-929): per
+// ray MSE and entropy, and their gradients w.r.t. image and weights_sum -- the
+// upstream gradients a torch criterion would hand the render's backward.
+__global__ void __launch_bounds__(256) k_rt_rgb_loss_grad(RtArgs a, const float* __restrict__ gt, float c_ent,
+                                                          float* __restrict__ g_img, float* __restrict__ g_ws) {
+    const uint32_t N = a.N, r = blockIdx.x * 256u + threadIdx.x;
+    if (r >= N) return;
+    const float c_mse = (float)(2.0 / 3.0) * a.inv_n;
+    float mse = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float e = a.image[(size_t)r * 3 + c] - gt[(size_t)r * 3 + c];
+        mse = mse + e * e;
+        g_img[(size_t)r * 3 + c] = c_mse * e;
+    }
+    const float ws = a.wsum[r];
+    const float we = fminf(fmaxf(ws, 1e-5f), 1.0f - 1e-5f);
+    a.terms[r] = mse;
     a.terms[3 * N + r] = -we * log2f(we) - (1.0f - we) * log2f(1.0f - we);
+    // clamp(ws, 1e-5, 1 - 1e-5) passes the gradient inside its range
+    g_ws[r] = (c_ent != 0.0f && ws >= 1e-5f && ws <= 1.0f - 1e-5f) ? c_ent * (log2f(1.0f - ws) - log2f(ws))
+                                                                      : 0.0f;
 }
 
 // ------------------------------------------------------------ backward --
@@ -361,18 +382,17 @@ __global__ void __launch_bounds__(64) k_rt_final_bwd_ray(RtArgs a) {
     const uint32_t N = a.N, lane = threadIdx.x, r = blockIdx.x * 64u + lane;
     if (r >= N) return;
     const size_t S = (size_t)kT * N;
-    const float ws = a.wsum[r];
-    float dimg[3], dz[3], dws = 0.0f;
+    float dimg[3], dz[3], dws = a.g_ws ? a.g_ws[r] : 0.0f;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        dimg[c] = a.c_mse * (a.image[(size_t)r * 3 + c] - a.gt[(size_t)r * 3 + c]);
+        dimg[c] = a.g_img[(size_t)r * 3 + c];
         dws = dws - dimg[c] * a.bg;                         // image += (1 - weights_sum) * bg
         const float sg = a.sig[(size_t)c * N + r];
         dz[c] = dimg[c] * (1.0f - sg) * sg;                 // sigmoid backward
         a.dz[(size_t)c * N + r] = dz[c];
     }
-    if (a.c_ent != 0.0f && ws >= 1e-5f && ws <= 1.0f - 1e-5f)   // clamp passes the gradient inside
-        dws = dws + a.c_ent * (log2f(1.0f - ws) - log2f(ws));
+    const float gdep = a.g_depth ? a.g_depth[r] : 0.0f;     // depth = sum_k w_k t_k
+    const float c_dist = a.g_loss ? a.g_loss[1] * a.inv_n : 0.0f;
     // transposed products as row sweeps (W^T g = sum_q g_q W[q, :]), the same
     // ascending-q accumulation order per output
     float dv2[32], dv1[32], dfi[31];
@@ -410,7 +430,7 @@ __global__ void __launch_bounds__(64) k_rt_final_bwd_ray(RtArgs a) {
     for (int j = 0; j < 16; ++j) shdot = __builtin_fmaf(dfi[15 + j], sh[j], shdot);
     // distortion totals (suffix sums below)
     float Wt = 0.0f, WMt = 0.0f;
-    if (a.c_dist != 0.0f)
+    if (c_dist != 0.0f)
         for (int k = 0; k < kT; ++k) {
             const size_t ks = (size_t)k * N + r;
             const float b0 = a.bins2[ks], b1 = a.bins2[ks + N], iv = b1 - b0, w = a.w[ks];
@@ -428,21 +448,21 @@ __global__ void __launch_bounds__(64) k_rt_final_bwd_ray(RtArgs a) {
         cum += (double)ds;
         const float raw = (1.0f - e) * T;
         const float w = nan_to_num(raw);
-        float g = shdot + dws;
+        float g = __builtin_fmaf(gdep, a.tmid[s], shdot + dws);
 #pragma unroll
         for (int j = 0; j < 15; ++j) {
             const size_t q = (size_t)(1 + j) * S + s;
             g = __builtin_fmaf(dfi[j], a.out[q], g);
             a.dout[q] = w * dfi[j];
         }
-        if (a.c_dist != 0.0f) {
+        if (c_dist != 0.0f) {
             const float b0 = a.bins2[ks], b1 = a.bins2[ks + N], iv = b1 - b0, m = b0 + iv / 2.0f;
             W = W + w;
             WM = WM + w * m;
             // d/dw_k [2 sum_i sum_{j<i} w_i w_j (m_i - m_j) + 1/3 sum_i s_i w_i^2]
             const float before = m * (W - w) - (WM - w * m);
             const float after = (WMt - WM) - m * (Wt - W);
-            g = __builtin_fmaf(a.c_dist, 2.0f * (before + after) + (2.0f / 3.0f) * iv * w, g);
+            g = __builtin_fmaf(c_dist, 2.0f * (before + after) + (2.0f / 3.0f) * iv * w, g);
         }
         const bool fin = isfinite(raw);                     // nan_to_num_ backward
         sdw[k][lane] = fin ? g : 0.0f;
@@ -616,7 +636,8 @@ struct PropBwdArgs {
     const float* ds;          // [T][N] its delta * sigma
     const float* bins2;       // [33][N] final bins (detached)
     const float* wf;          // [32][N] final weights (detached)
-    float c_prop;             // lambda_proposal / (32 N)
+    float c_prop;             // 1 / (32 N): the forward stores the gradient of the unweighted loss
+    const float* g_loss;      // [2] upstream gradients (device); [0] scales the proposal backward
     float* dds;               // [T][N]
     float* terms;             // [4][N] (row 1 accumulates the proposal loss)
     // per sample s = T r + k: [channel][T N]
@@ -745,7 +766,7 @@ __global__ void __launch_bounds__(256) k_rt_prop_bwd(PropBwdArgs a) {
     float sv = 0.0f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) sv = __builtin_fmaf(a.P1[i], h[i], sv);
-    const float dsig = a.dds[(size_t)k * N + r] * (rbn - rbp);
+    const float dsig = (a.dds[(size_t)k * N + r] * a.g_loss[0]) * (rbn - rbp);
     const float dx = dsig * expf(fminf(fmaxf(sv, -15.0f), 15.0f));
     float dh[16];
 #pragma unroll
@@ -773,12 +794,15 @@ __global__ void __launch_bounds__(256) k_rt_prop_bwd(PropBwdArgs a) {
         scatter_level_c2(a.grad_grid, a.grid.lv[l], ux, uy, uz, df[2 * l], df[2 * l + 1], live, stage);
 }
 
-// loss[0..3] = mse, proposal, distortion, entropy (means, fixed-order sums in
-// double); loss[4] = the total of utils.py:917-931.
-__global__ void __launch_bounds__(256) k_rt_loss(const float* terms, uint32_t N, float lp, float ld, float le,
-                                                 int with_prop, float* loss) {
+// Means of the per-ray loss terms (fixed-order sums in double): terms rows
+// 0..3 = mse (sum of 3 channels), proposal, distortion, entropy.  loss5 (or
+// null) = the four means and the total of utils.py:917-931; loss2 (or null) =
+// (proposal, distortion), the render's own loss outputs.  nt = rows to reduce.
+__global__ void __launch_bounds__(256) k_rt_loss(const float* terms, uint32_t N, int t0, int nt, float lp,
+                                                 float ld, float le, int with_prop, float* loss5, float* loss2) {
     __shared__ double red[256];
-    for (int t = 0; t < 4; ++t) {
+    __shared__ float mean[4];
+    for (int t = t0; t < t0 + nt; ++t) {
         double acc = 0.0;
         for (uint32_t r = threadIdx.x; r < N; r += 256u) acc += (double)terms[(size_t)t * N + r];
         red[threadIdx.x] = acc;
@@ -787,16 +811,27 @@ __global__ void __launch_bounds__(256) k_rt_loss(const float* terms, uint32_t N,
             if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
             __syncthreads();
         }
-        if (threadIdx.x == 0) loss[t] = (float)(red[0] / (double)N / (t == 0 ? 3.0 : 1.0));
+        if (threadIdx.x == 0) mean[t] = (float)(red[0] / (double)N / (t == 0 ? 3.0 : 1.0));
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        float total = loss[0];
-        if (with_prop && lp > 0.0f) total = total + lp * loss[1];
-        if (ld > 0.0f) total = total + ld * loss[2];
-        if (le > 0.0f) total = total + le * loss[3];
-        loss[4] = total;
+    if (threadIdx.x != 0) return;
+    if (loss2) {
+        loss2[0] = mean[1];
+        loss2[1] = mean[2];
     }
+    if (loss5) {
+        for (int t = 0; t < 4; ++t) loss5[t] = mean[t];
+        float total = mean[0];
+        if (with_prop && lp > 0.0f) total = total + lp * mean[1];
+        if (ld > 0.0f) total = total + ld * mean[2];
+        if (le > 0.0f) total = total + le * mean[3];
+        loss5[4] = total;
+    }
+}
+
+__global__ void k_rt_set2(float* p, float x, float y) {
+    p[0] = x;
+    p[1] = y;
 }
 
 struct RtWorkspace {
@@ -804,14 +839,14 @@ struct RtWorkspace {
     float* dds0;
     float* dds1;
     float* fin[10];          // pos feat h1 h2 out delta tmid dout dh1 dh2
-    float* ray[10];          // w fimg v1 v2 sig dz dv1 dv2 terms (+ spare)
+    float* ray[10];          // w fimg v1 v2 sig dz dv1 dv2 terms, step scratch (g_img 3 | g_ws | g_loss 2)
     float* prop[4];          // dh feat h dx (stage 0 size, reused by stage 1)
     float* slab;             // k_rt_outer partial sums
     size_t bytes;
 };
 
 constexpr int kFinCh[10] = {3, 32, 64, 64, 16, 1, 1, 16, 64, 64};
-constexpr int kRayCh[10] = {32, 31, 32, 32, 3, 3, 32, 32, 4, 1};
+constexpr int kRayCh[10] = {32, 31, 32, 32, 3, 3, 32, 32, 4, 6};
 constexpr int kPropCh[4] = {16, 10, 16, 1};
 
 RtWorkspace carve_rt(uint32_t N, void* base) {
@@ -854,83 +889,43 @@ void outer(const float* A, const float* B, uint32_t m, uint32_t n, size_t S, flo
     k_rt_outer_sum<<<div_up(m * n, 16), 256, 0, s>>>(slab, m * n, blocks, out);
 }
 
-}  // namespace
 
-extern "C" {
-
-size_t samnerf_rgb_train_workspace_size(const samnerf_model* model, uint32_t N) {
-    if (!model) return 0;
-    return carve_rt(N, nullptr).bytes;
-}
-
-int samnerf_rgb_train_step(const samnerf_model* m, const float* rays_o, const float* rays_d, uint32_t N,
-                           const float* cam_near_far, uint32_t n_cnf, const float* gt_rgb,
-                           const samnerf_rgb_train_opts* opts, float* image, float* depth,
-                           float* weights_sum, float* loss, const samnerf_rgb_grads* grads,
-                           void* workspace, size_t workspace_bytes, samnerf_stream_t stream) {
-    if (!m || !opts || !grads) return fail(SAMNERF_EINVAL, "rgb_train_step: null pointer");
-    if (N == 0) return SAMNERF_OK;
-    if (!rays_o || !rays_d || !gt_rgb || !image || !depth || !weights_sum || !loss)
-        return fail(SAMNERF_EINVAL, "rgb_train_step: null pointer");
-    if (m->num_steps[0] != 128 || m->num_steps[1] != 64 || m->num_steps[2] != 32)
-        return fail(SAMNERF_EINVAL, "rgb_train_step: built for num_steps = [128, 64, 32]");
-    if (m->with_sam || m->with_mask || m->sum_after_mlp)
-        return fail(SAMNERF_EINVAL, "rgb_train_step: RGB models only (no SAM / mask head, no sum_after_mlp; "
-                    "renderer.py:348 adds the training losses only then)");
-    if (cam_near_far && n_cnf != 1 && n_cnf != N)
-        return fail(SAMNERF_EINVAL, "rgb_train_step: cam_near_far must have 1 or N rows");
-    if (!m->perturb[0] != !m->perturb[1] || !m->perturb[0] != !m->perturb[2])
-        return fail(SAMNERF_EINVAL, "rgb_train_step: perturb needs all three position arrays or none");
-    if ((uint64_t)N * 128u >= (1ull << 31)) return fail(SAMNERF_EINVAL, "rgb_train_step: too many rays");
-    for (int i = 0; i < 3; ++i)
-        if (!m->grid_mlp[i] || !m->view_mlp[i] || !grads->grid_mlp[i] || !grads->view_mlp[i])
-            return fail(SAMNERF_EINVAL, "rgb_train_step: null MLP weight or gradient");
-    if (!grads->grid) return fail(SAMNERF_EINVAL, "rgb_train_step: null grid gradient");
-    const bool with_prop = opts->update_proposal && opts->lambda_proposal > 0.0f;
-    if (with_prop)
-        for (int p = 0; p < 2; ++p)
-            if (!grads->prop[p] || !grads->prop_mlp[p][0] || !grads->prop_mlp[p][1])
-                return fail(SAMNERF_EINVAL, "rgb_train_step: null proposal gradient");
-    RtWorkspace w = carve_rt(N, workspace);
-    if (!workspace || workspace_bytes < w.bytes)
-        return fail(SAMNERF_EWORKSPACE, "rgb_train_step: workspace needs %zu bytes, got %zu", w.bytes,
-                    workspace_bytes);
+// What forward and backward share: the model's argument blocks over one workspace.
+struct RtCall {
     TrainGeometry geo;
-    int rc = train_geometry(m, geo);
+    RtArgs a;
+    PropBwdArgs pb;
+};
+
+int rt_setup(const samnerf_model* m, const float* rays_o, const float* rays_d, uint32_t N, float bg,
+             RtWorkspace& w, RtCall& c) {
+    if (m->num_steps[0] != 128 || m->num_steps[1] != 64 || m->num_steps[2] != 32)
+        return fail(SAMNERF_EINVAL, "rgb_train: built for num_steps = [128, 64, 32]");
+    if (m->with_sam || m->with_mask || m->sum_after_mlp)
+        return fail(SAMNERF_EINVAL, "rgb_train: RGB models only (no SAM / mask head, no sum_after_mlp; "
+                    "renderer.py:348 adds the training losses only then)");
+    if ((uint64_t)N * 128u >= (1ull << 31)) return fail(SAMNERF_EINVAL, "rgb_train: too many rays");
+    for (int i = 0; i < 3; ++i)
+        if (!m->grid_mlp[i] || !m->view_mlp[i]) return fail(SAMNERF_EINVAL, "rgb_train: null MLP weight");
+    int rc = train_geometry(m, c.geo);
     if (rc) return rc;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-
-    // gradients are overwritten: the grid tables are zero-filled and scattered
-    // into (torch accumulates into zeroed .grad), the MLP weights' written whole
-    // by k_rt_outer_sum
-    auto zero = [&](float* p, size_t floats) { return hipMemsetAsync(p, 0, floats * sizeof(float), s); };
-    bool ok = zero(grads->grid, (size_t)m->grid.offsets_host[16] * 2) == hipSuccess;
-    if (with_prop)
-        for (int p = 0; p < 2; ++p)
-            ok = ok && zero(grads->prop[p], (size_t)m->prop[p].offsets_host[5] * 2) == hipSuccess;
-    if (!ok) return fail(SAMNERF_ELAUNCH, "rgb_train_step: gradient zero-fill failed");
-
-    // forward: proposal stages (the render's kernels), final samples, compositing
-    if ((rc = proposal_forward(m, geo, rays_o, rays_d, N, cam_near_far, n_cnf, w.p, s))) return rc;
-    RtArgs a{};
+    RtArgs& a = c.a;
+    a = RtArgs{};
     a.rays_o = rays_o;
     a.rays_d = rays_d;
     a.N = N;
-    a.bound = geo.bound;
-    a.b2 = geo.b2;
-    a.inv_b2 = geo.inv_b2;
-    a.bg = opts->bg_color;
-    a.grid = geo.grid;
+    a.bound = c.geo.bound;
+    a.b2 = c.geo.b2;
+    a.inv_b2 = c.geo.inv_b2;
+    a.bg = bg;
+    a.grid = c.geo.grid;
     for (int i = 0; i < 3; ++i) {
         a.G[i] = m->grid_mlp[i];
         a.V[i] = m->view_mlp[i];
     }
     a.snf = w.p.snf;
     a.bins2 = w.p.bins2;
-    a.gt = gt_rgb;
-    a.c_mse = (float)(2.0 / (3.0 * N));
-    a.c_dist = opts->lambda_distort > 0.0f ? (float)(opts->lambda_distort / (double)N) : 0.0f;
-    a.c_ent = opts->lambda_entropy > 0.0f ? (float)(opts->lambda_entropy / (double)N) : 0.0f;
+    a.inv_n = (float)(1.0 / (double)N);
     a.pos = w.fin[0];
     a.feat = w.fin[1];
     a.h1 = w.fin[2];
@@ -950,73 +945,213 @@ int samnerf_rgb_train_step(const samnerf_model* m, const float* rays_o, const fl
     a.dv1 = w.ray[6];
     a.dv2 = w.ray[7];
     a.terms = w.ray[8];
-    a.image = image;
-    a.depth = depth;
-    a.wsum = weights_sum;
-    a.grad_grid = grads->grid;
-    const uint32_t gs = div_up((uint64_t)kT * N, 256);
-    k_rt_final_fwd<<<gs, 256, 0, s>>>(a);
-    k_rt_composite<<<div_up(N, 256), 256, 0, s>>>(a);
+    PropBwdArgs& pb = c.pb;
+    pb = PropBwdArgs{};
+    pb.rays_o = rays_o;
+    pb.rays_d = rays_d;
+    pb.N = N;
+    pb.bound = c.geo.bound;
+    pb.b2 = c.geo.b2;
+    pb.inv_b2 = c.geo.inv_b2;
+    pb.snf = w.p.snf;
+    pb.bins0 = make_linspace(0.0f, 1.0f, 129);
+    pb.pbins0 = m->perturb[0];
+    pb.bins_in = w.p.bins1;
+    pb.bins2 = w.p.bins2;
+    pb.wf = a.w;
+    pb.c_prop = (float)(1.0 / (32.0 * N));
+    pb.terms = a.terms;
+    pb.dh = w.prop[0];
+    pb.feat = w.prop[1];
+    pb.h = w.prop[2];
+    pb.dx = w.prop[3];
+    return SAMNERF_OK;
+}
 
-    // backward: final stage
-    k_rt_final_bwd_ray<<<div_up(N, 64), 64, 0, s>>>(a);
-    k_rt_final_bwd<<<gs, 256, 0, s>>>(a);
-    const size_t S = (size_t)kT * N;
-    outer(a.dh1, a.feat, 64, 32, S, grads->grid_mlp[0], w.slab, s);
-    outer(a.dh2, a.h1, 64, 64, S, grads->grid_mlp[1], w.slab, s);
-    outer(a.dout, a.h2, 16, 64, S, grads->grid_mlp[2], w.slab, s);
-    outer(a.dv1, a.fimg, 32, 31, N, grads->view_mlp[0], w.slab, s);
-    outer(a.dv2, a.v1, 32, 32, N, grads->view_mlp[1], w.slab, s);
-    outer(a.dz, a.v2, 3, 32, N, grads->view_mlp[2], w.slab, s);
+void rt_prop_stage(const samnerf_model* m, RtCall& c, const RtWorkspace& w, int stage) {
+    PropBwdArgs& pb = c.pb;
+    pb.grid = c.geo.prop[stage];
+    pb.P0 = m->prop_mlp[stage][0];
+    pb.P1 = m->prop_mlp[stage][1];
+    pb.ws = stage ? w.p.w1 : w.p.w0;
+    pb.ds = stage ? w.p.ds1 : w.p.ds0;
+    pb.dds = stage ? w.dds1 : w.dds0;
+}
 
-    // backward: proposal stages (proposal_loss only; bins are detached)
+// forward: proposal stages, final samples, compositing; with_prop: the
+// proposal loss and its (unit-weight) gradient through the stages' compositing
+int rt_forward(const samnerf_model* m, const float* rays_o, const float* rays_d, uint32_t N, const float* cnf,
+               uint32_t n_cnf, bool with_prop, float* image, float* depth, float* weights_sum, RtCall& c,
+               const RtWorkspace& w, hipStream_t s) {
+    int rc = proposal_forward(m, c.geo, rays_o, rays_d, N, cnf, n_cnf, w.p, s);
+    if (rc) return rc;
+    c.a.image = image;
+    c.a.depth = depth;
+    c.a.wsum = weights_sum;
+    k_rt_final_fwd<<<div_up((uint64_t)kT * N, 256), 256, 0, s>>>(c.a);
+    k_rt_composite<<<div_up(N, 256), 256, 0, s>>>(c.a);
     if (with_prop) {
-        PropBwdArgs pb{};
-        pb.rays_o = rays_o;
-        pb.rays_d = rays_d;
-        pb.N = N;
-        pb.bound = geo.bound;
-        pb.b2 = geo.b2;
-        pb.inv_b2 = geo.inv_b2;
-        pb.snf = w.p.snf;
-        pb.bins0 = make_linspace(0.0f, 1.0f, 129);
-        pb.pbins0 = m->perturb[0];
-        pb.bins2 = w.p.bins2;
-        pb.wf = a.w;
-        pb.c_prop = (float)(opts->lambda_proposal / (32.0 * N));
-        pb.terms = a.terms;
-        pb.dh = w.prop[0];
-        pb.feat = w.prop[1];
-        pb.h = w.prop[2];
-        pb.dx = w.prop[3];
-        // stage 0: 128 samples on the linspace / perturbed bins
-        pb.grid = geo.prop[0];
-        pb.P0 = m->prop_mlp[0][0];
-        pb.P1 = m->prop_mlp[0][1];
-        pb.ws = w.p.w0;
-        pb.ds = w.p.ds0;
-        pb.dds = w.dds0;
-        pb.grad_grid = grads->prop[0];
-        k_rt_prop_ray<128, true><<<div_up(N, 32), 32, 0, s>>>(pb);
-        k_rt_prop_bwd<128, true><<<div_up((uint64_t)128 * N, 256), 256, 0, s>>>(pb);
-        outer(pb.dh, pb.feat, 16, 10, (size_t)128 * N, grads->prop_mlp[0][0], w.slab, s);
-        outer(pb.dx, pb.h, 1, 16, (size_t)128 * N, grads->prop_mlp[0][1], w.slab, s);
-        // stage 1: 64 samples on stage 0's resampled bins
-        pb.grid = geo.prop[1];
-        pb.P0 = m->prop_mlp[1][0];
-        pb.P1 = m->prop_mlp[1][1];
-        pb.bins_in = w.p.bins1;
-        pb.ws = w.p.w1;
-        pb.ds = w.p.ds1;
-        pb.dds = w.dds1;
-        pb.grad_grid = grads->prop[1];
-        k_rt_prop_ray<64, false><<<div_up(N, 32), 32, 0, s>>>(pb);
-        k_rt_prop_bwd<64, false><<<div_up((uint64_t)64 * N, 256), 256, 0, s>>>(pb);
-        outer(pb.dh, pb.feat, 16, 10, (size_t)64 * N, grads->prop_mlp[1][0], w.slab, s);
-        outer(pb.dx, pb.h, 1, 16, (size_t)64 * N, grads->prop_mlp[1][1], w.slab, s);
+        rt_prop_stage(m, c, w, 0);
+        k_rt_prop_ray<128, true><<<div_up(N, 32), 32, 0, s>>>(c.pb);
+        rt_prop_stage(m, c, w, 1);
+        k_rt_prop_ray<64, false><<<div_up(N, 32), 32, 0, s>>>(c.pb);
     }
-    k_rt_loss<<<1, 256, 0, s>>>(a.terms, N, opts->lambda_proposal, opts->lambda_distort, opts->lambda_entropy,
-                                with_prop ? 1 : 0, loss);
+    return SAMNERF_OK;
+}
+
+// backward given the upstream gradients in c.a (g_img, g_ws, g_depth, g_loss)
+int rt_backward(const samnerf_model* m, uint32_t N, bool with_prop, const samnerf_rgb_grads* g, RtCall& c,
+                const RtWorkspace& w, hipStream_t s) {
+    if (!g || !g->grid) return fail(SAMNERF_EINVAL, "rgb_train: null grid gradient");
+    for (int i = 0; i < 3; ++i)
+        if (!g->grid_mlp[i] || !g->view_mlp[i]) return fail(SAMNERF_EINVAL, "rgb_train: null MLP gradient");
+    if (with_prop)
+        for (int p = 0; p < 2; ++p)
+            if (!g->prop[p] || !g->prop_mlp[p][0] || !g->prop_mlp[p][1])
+                return fail(SAMNERF_EINVAL, "rgb_train: null proposal gradient");
+    // gradients are overwritten: the grid tables are zero-filled and scattered
+    // into (torch accumulates into zeroed .grad), the MLP weights' written whole
+    // by k_rt_outer_sum
+    auto zero = [&](float* p, size_t floats) { return hipMemsetAsync(p, 0, floats * sizeof(float), s); };
+    bool ok = zero(g->grid, (size_t)m->grid.offsets_host[16] * 2) == hipSuccess;
+    if (with_prop)
+        for (int p = 0; p < 2; ++p)
+            ok = ok && zero(g->prop[p], (size_t)m->prop[p].offsets_host[5] * 2) == hipSuccess;
+    if (!ok) return fail(SAMNERF_ELAUNCH, "rgb_train: gradient zero-fill failed");
+    RtArgs& a = c.a;
+    a.grad_grid = g->grid;
+    k_rt_final_bwd_ray<<<div_up(N, 64), 64, 0, s>>>(a);
+    k_rt_final_bwd<<<div_up((uint64_t)kT * N, 256), 256, 0, s>>>(a);
+    const size_t S = (size_t)kT * N;
+    outer(a.dh1, a.feat, 64, 32, S, g->grid_mlp[0], w.slab, s);
+    outer(a.dh2, a.h1, 64, 64, S, g->grid_mlp[1], w.slab, s);
+    outer(a.dout, a.h2, 16, 64, S, g->grid_mlp[2], w.slab, s);
+    outer(a.dv1, a.fimg, 32, 31, N, g->view_mlp[0], w.slab, s);
+    outer(a.dv2, a.v1, 32, 32, N, g->view_mlp[1], w.slab, s);
+    outer(a.dz, a.v2, 3, 32, N, g->view_mlp[2], w.slab, s);
+    if (with_prop) {                      // proposal_loss only: the bins are detached
+        PropBwdArgs& pb = c.pb;
+        pb.g_loss = a.g_loss;
+        for (int st = 0; st < 2; ++st) {
+            rt_prop_stage(m, c, w, st);
+            pb.grad_grid = g->prop[st];
+            const uint32_t T = st ? 64u : 128u;
+            if (st) k_rt_prop_bwd<64, false><<<div_up((uint64_t)T * N, 256), 256, 0, s>>>(pb);
+            else k_rt_prop_bwd<128, true><<<div_up((uint64_t)T * N, 256), 256, 0, s>>>(pb);
+            outer(pb.dh, pb.feat, 16, 10, (size_t)T * N, g->prop_mlp[st][0], w.slab, s);
+            outer(pb.dx, pb.h, 1, 16, (size_t)T * N, g->prop_mlp[st][1], w.slab, s);
+        }
+    }
+    return SAMNERF_OK;
+}
+
+bool perturb_ok(const samnerf_model* m) { return !m->perturb[0] == !m->perturb[1] && !m->perturb[0] == !m->perturb[2]; }
+
+}  // namespace
+
+extern "C" {
+
+size_t samnerf_rgb_train_workspace_size(const samnerf_model* model, uint32_t N) {
+    if (!model) return 0;
+    return carve_rt(N, nullptr).bytes;
+}
+
+int samnerf_rgb_train_forward(const samnerf_model* m, const float* rays_o, const float* rays_d, uint32_t N,
+                              const float* cam_near_far, uint32_t n_cnf, float bg_color, int with_proposal,
+                              float* image, float* depth, float* weights_sum, float* losses, void* workspace,
+                              size_t workspace_bytes, samnerf_stream_t stream) {
+    if (!m) return fail(SAMNERF_EINVAL, "rgb_train_forward: null model");
+    if (N == 0) return SAMNERF_OK;
+    if (!rays_o || !rays_d || !image || !depth || !weights_sum || !losses)
+        return fail(SAMNERF_EINVAL, "rgb_train_forward: null pointer");
+    if (cam_near_far && n_cnf != 1 && n_cnf != N)
+        return fail(SAMNERF_EINVAL, "rgb_train_forward: cam_near_far must have 1 or N rows");
+    if (!perturb_ok(m))
+        return fail(SAMNERF_EINVAL, "rgb_train_forward: perturb needs all three position arrays or none");
+    RtWorkspace w = carve_rt(N, workspace);
+    if (!workspace || workspace_bytes < w.bytes)
+        return fail(SAMNERF_EWORKSPACE, "rgb_train_forward: workspace needs %zu bytes, got %zu", w.bytes,
+                    workspace_bytes);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    RtCall c;
+    int rc = rt_setup(m, rays_o, rays_d, N, bg_color, w, c);
+    if (rc) return rc;
+    if ((rc = rt_forward(m, rays_o, rays_d, N, cam_near_far, n_cnf, with_proposal != 0, image, depth,
+                         weights_sum, c, w, s)))
+        return rc;
+    k_rt_loss<<<1, 256, 0, s>>>(c.a.terms, N, 1, 2, 0.0f, 0.0f, 0.0f, 0, nullptr, losses);
+    return check_launch("rgb_train_forward");
+}
+
+int samnerf_rgb_train_backward(const samnerf_model* m, const float* rays_o, const float* rays_d, uint32_t N,
+                               float bg_color, int with_proposal, const float* grad_image,
+                               const float* grad_weights_sum, const float* grad_depth, const float* grad_losses,
+                               const samnerf_rgb_grads* grads, void* workspace, size_t workspace_bytes,
+                               samnerf_stream_t stream) {
+    if (!m) return fail(SAMNERF_EINVAL, "rgb_train_backward: null model");
+    if (N == 0) return SAMNERF_OK;
+    if (!rays_o || !rays_d || !grad_image) return fail(SAMNERF_EINVAL, "rgb_train_backward: null pointer");
+    if (with_proposal && !grad_losses)
+        return fail(SAMNERF_EINVAL, "rgb_train_backward: the proposal backward needs grad_losses");
+    RtWorkspace w = carve_rt(N, workspace);
+    if (!workspace || workspace_bytes < w.bytes)
+        return fail(SAMNERF_EWORKSPACE, "rgb_train_backward: workspace needs %zu bytes, got %zu", w.bytes,
+                    workspace_bytes);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    RtCall c;
+    int rc = rt_setup(m, rays_o, rays_d, N, bg_color, w, c);
+    if (rc) return rc;
+    c.a.image = nullptr;
+    c.a.depth = nullptr;
+    c.a.wsum = nullptr;
+    c.a.g_img = grad_image;
+    c.a.g_ws = grad_weights_sum;
+    c.a.g_depth = grad_depth;
+    c.a.g_loss = grad_losses;
+    if ((rc = rt_backward(m, N, with_proposal != 0, grads, c, w, s))) return rc;
+    return check_launch("rgb_train_backward");
+}
+
+int samnerf_rgb_train_step(const samnerf_model* m, const float* rays_o, const float* rays_d, uint32_t N,
+                           const float* cam_near_far, uint32_t n_cnf, const float* gt_rgb,
+                           const samnerf_rgb_train_opts* opts, float* image, float* depth,
+                           float* weights_sum, float* loss, const samnerf_rgb_grads* grads,
+                           void* workspace, size_t workspace_bytes, samnerf_stream_t stream) {
+    if (!m || !opts || !grads) return fail(SAMNERF_EINVAL, "rgb_train_step: null pointer");
+    if (N == 0) return SAMNERF_OK;
+    if (!rays_o || !rays_d || !gt_rgb || !image || !depth || !weights_sum || !loss)
+        return fail(SAMNERF_EINVAL, "rgb_train_step: null pointer");
+    if (cam_near_far && n_cnf != 1 && n_cnf != N)
+        return fail(SAMNERF_EINVAL, "rgb_train_step: cam_near_far must have 1 or N rows");
+    if (!perturb_ok(m))
+        return fail(SAMNERF_EINVAL, "rgb_train_step: perturb needs all three position arrays or none");
+    RtWorkspace w = carve_rt(N, workspace);
+    if (!workspace || workspace_bytes < w.bytes)
+        return fail(SAMNERF_EWORKSPACE, "rgb_train_step: workspace needs %zu bytes, got %zu", w.bytes,
+                    workspace_bytes);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool with_prop = opts->update_proposal && opts->lambda_proposal > 0.0f;
+    RtCall c;
+    int rc = rt_setup(m, rays_o, rays_d, N, opts->bg_color, w, c);
+    if (rc) return rc;
+    if ((rc = rt_forward(m, rays_o, rays_d, N, cam_near_far, n_cnf, with_prop, image, depth, weights_sum, c, w,
+                         s)))
+        return rc;
+    // the Trainer's loss (utils.py:917-931) and its upstream gradients
+    float* g_img = w.ray[9];
+    float* g_ws = g_img + 3 * (size_t)N;
+    float* g_loss = g_ws + N;
+    const float c_ent = opts->lambda_entropy > 0.0f ? (float)(opts->lambda_entropy / (double)N) : 0.0f;
+    k_rt_rgb_loss_grad<<<div_up(N, 256), 256, 0, s>>>(c.a, gt_rgb, c_ent, g_img, g_ws);
+    k_rt_set2<<<1, 1, 0, s>>>(g_loss, with_prop ? opts->lambda_proposal : 0.0f,
+                              opts->lambda_distort > 0.0f ? opts->lambda_distort : 0.0f);
+    k_rt_loss<<<1, 256, 0, s>>>(c.a.terms, N, 0, 4, opts->lambda_proposal, opts->lambda_distort,
+                                opts->lambda_entropy, with_prop ? 1 : 0, loss, nullptr);
+    c.a.g_img = g_img;
+    c.a.g_ws = g_ws;
+    c.a.g_depth = nullptr;
+    c.a.g_loss = g_loss;
+    if ((rc = rt_backward(m, N, with_prop, grads, c, w, s))) return rc;
     return check_launch("rgb_train_step");
 }
 

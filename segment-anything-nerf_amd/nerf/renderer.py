@@ -190,8 +190,24 @@ class NeRFRenderer(nn.Module):
                 and list(self.opt.num_steps) == [128, 64, 32]
                 and (not self.opt.with_sam or self.opt.sam_use_view_direction))
 
+    def _fused_train_ok(self, rays_o, bg_color, return_feats, return_mask):
+        """Train mode under grad for an RGB model (renderer.py:348-356's case):
+        the HIP training kernels (samnerf_amd.fused.render_rgb_train)."""
+        o = self.opt
+        return (self.fused and rays_o.is_cuda and self.training and torch.is_grad_enabled()
+                and not o.with_sam and not getattr(o, "with_mask", False)
+                and not getattr(o, "sum_after_mlp", False) and not return_feats and not return_mask
+                and o.background == "last_sample" and list(o.num_steps) == [128, 64, 32]
+                and (not torch.is_tensor(bg_color) or bg_color.numel() == 1))
+
     def run(self, rays_o, rays_d, bg_color=None, perturb=False, cam_near_far=None,
             update_proposal=True, return_feats=0, return_mask=0, H=None, W=None, **kwargs):
+        if self._fused_train_ok(rays_o, bg_color, return_feats, return_mask):
+            from samnerf_amd.fused import FusedRenderer, render_rgb_train
+            if self._fused is None or self._fused.net is not self:
+                self._fused = FusedRenderer(self)
+            return render_rgb_train(self._fused, rays_o, rays_d, cam_near_far, bg_color, perturb,
+                                    update_proposal)
         if self._fused_ok(rays_o, perturb, return_mask, kwargs):
             from samnerf_amd.fused import FusedRenderer
             if self._fused is None or self._fused.net is not self:

@@ -12,7 +12,7 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import SamnerfGrid, SamnerfModel, SamnerfTaps, check, lib
+from ._lib import SamnerfGrid, SamnerfModel, SamnerfRgbGrads, SamnerfTaps, check, lib
 from .ops import _ptr, _stream
 
 ROW = 164          # head-input row: f_sam 128 | f_image 31 | image 3 | depth 1 | pad
@@ -390,3 +390,114 @@ def render_sam_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None,
     else:
         samvit = _SamHeadTrain.apply(rows, renderer, *_head_params(net))
     return {"samvit": samvit, "image": image, "depth": depth, "weights_sum": wsum}
+
+
+# ------------------------------------------------------------ RGB training --
+def rgb_train_params(net, with_prop):
+    """The tensors the RGB training backward writes, in samnerf_rgb_grads order
+    (NeRFNetwork.get_params groups, network.py:201-206); the proposal networks'
+    only on the steps they train (renderer.py:290, utils.py:912-913)."""
+    ps = [net.grid.embeddings] + [net.grid_mlp.net[i].weight for i in range(3)] + \
+        [net.view_mlp.net[i].weight for i in range(3)]
+    if with_prop:
+        ps += [net.prop_encoders[0].embeddings, net.prop_encoders[1].embeddings] + \
+            [net.prop_mlp[p].net[i].weight for p in range(2) for i in range(2)]
+    return ps
+
+
+class _FusedRGBTrain(torch.autograd.Function):
+    """NeRFRenderer.run in train mode under grad for an RGB model
+    (renderer.py:221-362) as samnerf_rgb_train_forward / _backward: outputs
+    image, depth, weights_sum and the render's own losses (proposal_loss,
+    distort_loss), differentiable w.r.t. every trained tensor; the Trainer's
+    criterion and the entropy term stay torch ops on them."""
+
+    @staticmethod
+    def forward(ctx, renderer, rays_o, rays_d, cnf, bg, pert, with_prop, *params):
+        N = rays_o.shape[0]
+        dev = rays_o.device
+        m = renderer.model()
+        m.view_width = 0
+        m.with_mask = 0
+        need = lib().samnerf_rgb_train_workspace_size(ctypes.byref(m), N)
+        ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        image = torch.empty(N, 3, device=dev)
+        depth = torch.empty(N, device=dev)
+        wsum = torch.empty(N, device=dev)
+        losses = torch.zeros(2, device=dev)
+        n_cnf = 0 if cnf is None else cnf.shape[0]
+        try:
+            for i in range(3):
+                m.perturb[i] = None if pert is None else _param(pert[i], f"perturb[{i}]")
+            check(lib().samnerf_rgb_train_forward(
+                ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, _ptr(cnf), n_cnf, float(bg), int(with_prop),
+                _ptr(image), _ptr(depth), _ptr(wsum), _ptr(losses), _ptr(ws), need, _stream(rays_o)),
+                "rgb_train_forward")
+        finally:
+            for i in range(3):
+                m.perturb[i] = None
+        ctx.state = (renderer, m, rays_o, rays_d, bg, pert, with_prop, ws, need, list(renderer._keep))
+        ctx.shapes = [p.shape for p in params]
+        return image, depth, wsum, losses[0], losses[1]
+
+    @staticmethod
+    def backward(ctx, g_img, g_depth, g_wsum, g_prop, g_dist):
+        renderer, m, rays_o, rays_d, bg, pert, with_prop, ws, need, _ = ctx.state
+        dev = rays_o.device
+        N = rays_o.shape[0]
+        g_img = g_img.contiguous().float()
+        g_loss = torch.stack([g_prop.reshape(()), g_dist.reshape(())]).float().contiguous()
+        grads = [torch.empty(sh, device=dev) for sh in ctx.shapes]
+        g = SamnerfRgbGrads()
+        g.grid = grads[0].data_ptr()
+        for i in range(3):
+            g.grid_mlp[i] = grads[1 + i].data_ptr()
+            g.view_mlp[i] = grads[4 + i].data_ptr()
+        if with_prop:
+            g.prop[0], g.prop[1] = grads[7].data_ptr(), grads[8].data_ptr()
+            for q in range(2):
+                for i in range(2):
+                    g.prop_mlp[q][i] = grads[9 + 2 * q + i].data_ptr()
+        try:
+            for i in range(3):
+                m.perturb[i] = None if pert is None else _param(pert[i], f"perturb[{i}]")
+            check(lib().samnerf_rgb_train_backward(
+                ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, float(bg), int(with_prop), _ptr(g_img),
+                _ptr(g_wsum.contiguous().float()), _ptr(g_depth.contiguous().float()), _ptr(g_loss),
+                ctypes.byref(g), _ptr(ws), need, _stream(g_img)), "rgb_train_backward")
+        finally:
+            for i in range(3):
+                m.perturb[i] = None
+        return (None,) * 7 + tuple(grads)
+
+
+def render_rgb_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None, perturb=False,
+                     update_proposal=True):
+    """The results dict of NeRFRenderer.run for an RGB model in train mode with
+    grad (renderer.py:221-362): image, depth, weights_sum, num_points and --
+    when lambda_proposal > 0 and update_proposal -- proposal_loss, when
+    lambda_distort > 0 distort_loss, all differentiable on the HIP training
+    kernels (rgb_train.hip)."""
+    net = renderer.net
+    opt = net.opt
+    rays_o = rays_o.contiguous().float()
+    rays_d = rays_d.contiguous().float()
+    N = rays_o.shape[0]
+    bg = 1.0 if bg_color is None else (float(bg_color) if not torch.is_tensor(bg_color) else
+                                        float(bg_color.reshape(())))
+    m = renderer.model()
+    pert = None
+    if isinstance(perturb, (tuple, list)) or perturb:
+        pert = tuple(perturb) if isinstance(perturb, (tuple, list)) else \
+            perturbed_positions(N, list(m.num_steps), rays_o.device)
+        pert = tuple(t.contiguous().float() for t in pert)
+    cnf = None if cam_near_far is None else cam_near_far.contiguous().float()
+    with_prop = bool(update_proposal) and getattr(opt, "lambda_proposal", 0) > 0
+    image, depth, wsum, prop_loss, dist_loss = _FusedRGBTrain.apply(
+        renderer, rays_o, rays_d, cnf, bg, pert, with_prop, *rgb_train_params(net, with_prop))
+    out = {"num_points": N * int(m.num_steps[2]), "weights_sum": wsum, "depth": depth, "image": image}
+    if with_prop:
+        out["proposal_loss"] = prop_loss
+    if getattr(opt, "lambda_distort", 0) > 0:
+        out["distort_loss"] = dist_loss
+    return out

@@ -23,9 +23,15 @@ pytestmark = pytest.mark.gpu
 
 
 def _rgb_nets(cuda, seed=12, log2=(12, 10), devices=("cuda", "cpu")):
+    """Identical networks; every one after the first renders through the torch
+    path (fused = False: run_torch + autograd with the drop-in encoder kernels),
+    the reference's op sequence the fused step is checked against."""
     spec = synth.ModelSpec(with_sam=False, grid_log2=log2[0], s_grid_log2=10, prop_log2=log2[1])
     params = synth.make_params(spec, seed=seed, emb_scale=0.5)
-    return [make_net(spec, params, cuda if d == "cuda" else "cpu").train() for d in devices]
+    nets = [make_net(spec, params, cuda if d == "cuda" else "cpu").train() for d in devices]
+    for n in nets[1:]:
+        n.fused = False
+    return nets
 
 
 def _rays(n_side, rot, cuda=None):
@@ -191,3 +197,32 @@ def test_fused_rgb_step_deterministic_weight_gradients(hip_lib, cuda):
         else:
             err = ((res[0][k] - res[1][k]).norm() / res[1][k].norm().clamp_min(1e-30)).item()
             assert err < 1e-5, (k, err)
+
+
+def test_train_mode_render_runs_the_training_kernels(hip_lib, cuda):
+    """NeRFRenderer.run in train mode under grad (the reference Trainer's own
+    call, utils.py:913-931 + loss.backward()) dispatches to the HIP training
+    kernels through an autograd Function: the Trainer-shaped step
+    (rgb_train_step: render, criterion, extra losses, backward) equals the
+    one-call samnerf_rgb_train_step (float-atomic order aside) and the torch
+    path."""
+    from samnerf_amd.train import rgb_train_step, rgb_train_step_fused
+    a, b, c = _rgb_nets(cuda, seed=23, devices=("cuda", "cuda", "cuda"))
+    c.fused = True                                   # the autograd path
+    ro, rd = _rays(32, 8, cuda)
+    gt = torch.rand(1024, 3, generator=torch.Generator().manual_seed(9)).to(cuda)
+    torch.manual_seed(5)
+    _, loss_a, _ = rgb_train_step_fused(a, ro, rd, gt, global_step=1)
+    torch.manual_seed(5)
+    _, loss_b, _ = rgb_train_step(b, ro, rd, gt, global_step=1)
+    loss_b.backward()
+    torch.manual_seed(5)
+    img_c, loss_c, out_c = rgb_train_step(c, ro, rd, gt, global_step=1)
+    assert "proposal_loss" in out_c and "distort_loss" in out_c and out_c["num_points"] == 1024 * 32
+    assert img_c.requires_grad and loss_c.requires_grad
+    loss_c.backward()
+    assert abs(float(loss_c) - float(loss_a)) <= 1e-6 * abs(float(loss_a))
+    for (k, pa), (_, pc) in zip(a.named_parameters(), c.named_parameters()):
+        err = float((pa.grad - pc.grad).norm() / pa.grad.norm().clamp_min(1e-30))
+        assert err < 1e-5, (k, err)
+    _compare_grads(c, b)

@@ -199,9 +199,14 @@ def test_distillation_steps_reduce_loss(hip_lib, cuda):
 
 
 def _rgb_pair(cuda, seed=12):
+    """The GPU net renders through the torch path (fused = False: run_torch +
+    autograd + the drop-in encoder kernels) -- what these tests pin; the HIP
+    training kernels are tests/test_gpu_rgb_train.py's."""
     spec = synth.ModelSpec(with_sam=False, grid_log2=12, s_grid_log2=10, prop_log2=10)
     params = synth.make_params(spec, seed=seed, emb_scale=0.5)
-    return make_net(spec, params, cuda).train(), make_net(spec, params, "cpu").train()
+    gpu = make_net(spec, params, cuda).train()
+    gpu.fused = False
+    return gpu, make_net(spec, params, "cpu").train()
 
 
 def test_rgb_train_step_gradients_match_cpu_twin(hip_lib, cuda):

@@ -24,6 +24,7 @@ def run(N, fused, steps=20, warmup=5):
     spec = synth.ModelSpec(with_sam=False)
     net = make_net(spec, synth.make_params(spec, seed=1, emb_scale=0.5), dev).train()
     net.opt.adaptive_num_rays = False
+    net.fused = fused          # False: NeRFRenderer.run_torch under autograd
     opt = FusedAdam(net.get_params(1e-2), eps=1e-15)
     side = int(round(N ** 0.5))
     pose, intr = synth.gui_camera(side, side, rot=synth.random_rotation(1))

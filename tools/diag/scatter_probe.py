@@ -25,6 +25,7 @@ def main(N=8192):
     dev = torch.device("cuda:0")
     spec = synth.ModelSpec(with_sam=False)
     net = make_net(spec, synth.make_params(spec, seed=1, emb_scale=0.5), dev).train()
+    net.fused = False                     # the torch path: run_torch + autograd + drop-in kernels
     side = int(round(N ** 0.5))
     pose, intr = synth.gui_camera(side, side, rot=synth.random_rotation(1))
     ro, rd = ops.get_rays(pose, intr, side, side, device=dev)
