@@ -146,6 +146,9 @@ __device__ __forceinline__ void load_grid_mlp(const RtArgs& a, float* sw) {
 __device__ __forceinline__ void scatter_level_c2(float* __restrict__ gtab, const LevelDesc& d, float ux,
                                                  float uy, float uz, float g0, float g1, bool live,
                                                  float* stage) {
+    // a wave whose samples all carry a zero gradient adds nothing (samples
+    // behind the last weighted one, whole rays outside the scene)
+    if (!__any(live && (g0 != 0.0f || g1 != 0.0f))) return;
     uint32_t off[8];
     float cw[8];
     corner_rows<2>(d, ux, uy, uz, off, cw);
