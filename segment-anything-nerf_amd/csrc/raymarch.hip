@@ -1502,7 +1502,7 @@ template <int T>
 __global__ void __launch_bounds__(256)
 k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __restrict__ u_in,
                  const float* __restrict__ w_in, const float* __restrict__ grad, uint32_t gstride,
-                 float* __restrict__ gemb, uint32_t max_cells) {
+                 float* __restrict__ gemb, uint32_t max_cells, uint32_t run_res) {
     __shared__ float box[4][kBwdBoxCells * 8];           // per wave: cell x channel sums
     __shared__ uint32_t list[4][kBwdBoxCells];           // per wave: rows of the non-zero cells
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1522,6 +1522,18 @@ k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __rest
     // per-sample chain -- loads, box reductions, LDS sums, atomics -- is
     // latency-bound at 8 rays per wave)
     const int k0 = (int)(blockIdx.z * T / gridDim.z), k1 = (int)((blockIdx.z + 1) * T / gridDim.z);
+    // levels up to run_res: a lane walks its ray's samples in order, and the
+    // previous sample's 8 corner rows stay pending in registers -- a new corner
+    // on a pending row absorbs its sum, only rows the ray has left are added to
+    // memory (consecutive samples of a ray share cells at the coarse levels)
+    const bool run = max_cells == 0u && d.res <= run_res;     // block-uniform
+    uint32_t prow[8];
+    float pval[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        prow[c] = 0xFFFFFFFFu;
+        pval[c] = 0.0f;
+    }
     for (int k = k0; k < k1; ++k) {
         const float ux = u_in[((size_t)k * 3 + 0) * N + rr];
         const float uy = u_in[((size_t)k * 3 + 1) * N + rr];
@@ -1583,6 +1595,33 @@ k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __rest
                 }
             }
             wave_lds_sync();                                  // reads done before the next zeroing
+        } else if (run) {
+            uint32_t nrow[8];
+            float nval[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float wx = (c & 1) ? fx : 1.0f - fx;
+                const float wy = (c & 2) ? fy : 1.0f - fy;
+                const float wz = (c & 4) ? fz : 1.0f - fz;
+                nrow[c] = dense_or_hash_row((c & 1) ? nx : cx, (c & 2) ? ny : cy, (c & 4) ? nz : cz, d);
+                nval[c] = ((wx * wy) * wz) * wg;
+            }
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                bool hit = false;
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const bool h = !hit && prow[p] == nrow[c];
+                    nval[c] += h ? pval[p] : 0.0f;
+                    hit = hit || h;
+                }
+                if (!hit && live && prow[p] != 0xFFFFFFFFu) atomicAdd(base + (size_t)prow[p] * 8u, pval[p]);
+            }
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                prow[c] = nrow[c];
+                pval[c] = nval[c];
+            }
         } else {
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
@@ -1609,6 +1648,10 @@ k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __rest
             }
         }
     }
+    if (run && live)
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+            if (prow[c] != 0xFFFFFFFFu) atomicAdd(base + (size_t)prow[c] * 8u, pval[c]);
 }
 
 // ------------------------------------------------------- step kernels ----
@@ -2348,14 +2391,25 @@ int samnerf_sgrid_backward(const samnerf_model* m, const float* grad_fsam, uint3
     // slower than the per-corner atomics, 0.70 vs 0.56 ms per cfg-5 step, so
     // not the default); SAMNERF_SGRID_BWD_SPLIT: sample groups per ray
     // (blockIdx.z; 1 = the round-1 form, 4-16 measured no faster)
+    // SAMNERF_SGRID_BWD=run: the along-ray merge on every level
+    // (SAMNERF_SGRID_RUN_RES: up to this level resolution).  Measured slower on
+    // a cfg-5 step: 1.29 ms per step with the per-corner form, 1.62 with the
+    // merge on every level, 1.50 on levels up to res 64 (tools/r2/gpu_r2s3n.sh):
+    // a wave's 8 neighbouring rays share corner rows at one sample index (the
+    // butterfly) more often than consecutive samples of one ray do, and the
+    // merge gives the butterfly up.  Kept selectable and tested.
     const char* mode = getenv("SAMNERF_SGRID_BWD");
     const uint32_t max_cells = (mode && !strcmp(mode, "box")) ? kBwdBoxCells : 0u;
+    const char* rr = getenv("SAMNERF_SGRID_RUN_RES");
+    uint32_t run_res = rr ? (uint32_t)atoi(rr) : 0u;
+    if (mode && !strcmp(mode, "run") && !rr) run_res = 0xFFFFFFFFu;
     const char* sp = getenv("SAMNERF_SGRID_BWD_SPLIT");
     const uint32_t split = sp ? (uint32_t)std::max(1, std::min(32, atoi(sp))) : 1u;
     k_sgrid_backward<32><<<dim3(div_up((uint64_t)N * 8, 256), 16, split), 256, 0,
                            reinterpret_cast<hipStream_t>(stream)>>>(N, make_ray_tiles(N, m->view_width),
                                                                      gs, w.u_f, w.w_f, grad_fsam,
-                                                                     kRow, grad_embeddings, max_cells);
+                                                                     kRow, grad_embeddings, max_cells,
+                                                                     run_res);
     return check_launch("sgrid_backward");
 }
 

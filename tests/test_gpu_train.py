@@ -96,7 +96,9 @@ def test_distillation_step_matches_cpu_twin_full_tables(hip_lib, cuda):
 def test_sgrid_backward_box_matches_per_corner(hip_lib, cuda, monkeypatch):
     """The s_grid scatter's LDS-box aggregation (SAMNERF_SGRID_BWD=box; per
     wave and sample: corner sums in LDS, non-zero cells compacted, one atomic
-    per distinct row) against the default per-corner form on the full-size table, a
+    per distinct row) and the along-ray merge (SAMNERF_SGRID_BWD=run: a lane
+    keeps the previous sample's corner rows pending) against the default
+    per-corner form on the full-size table, a
     64x64 view and a ray set with scattered rays (boxes too big -> per-corner
     path inside the same launch): equal up to float-atomic order."""
     from samnerf_amd import ops
@@ -115,20 +117,23 @@ def test_sgrid_backward_box_matches_per_corner(hip_lib, cuda, monkeypatch):
     ws = out["_workspace"]
     g = torch.randn(N, ROW, device=cuda, generator=torch.Generator(device=cuda).manual_seed(2))
     grads = {}
-    for mode in ("box", "corner"):
+    for mode in ("box", "corner", "run"):
         monkeypatch.setenv("SAMNERF_SGRID_BWD", mode)
         ge = torch.zeros_like(net.s_grid.embeddings)
         fr.sgrid_backward(g, ws, ge)
         grads[mode] = ge
-    a, b = grads["box"], grads["corner"]
-    assert (a != 0).sum() > 10000
-    # another association of the same float sums (LDS first, then one atomic
-    # per row): relative to the tensor, not per element (rows whose
-    # contributions cancel carry no relative precision in either form)
-    rel = ((a - b).norm() / b.norm()).item()
-    mx = ((a - b).abs().max() / b.abs().max()).item()
-    print("box vs per-corner scatter:", rel, mx)
-    assert rel < 1e-5 and mx < 1e-5, (rel, mx)
+    b = grads["corner"]
+    for mode in ("box", "run"):
+        a = grads[mode]
+        assert (a != 0).sum() > 10000
+        # another association of the same float sums (LDS first / along the
+        # ray first, then one atomic per row): relative to the tensor, not per
+        # element (rows whose contributions cancel carry no relative precision
+        # in any form)
+        rel = ((a - b).norm() / b.norm()).item()
+        mx = ((a - b).abs().max() / b.abs().max()).item()
+        print(mode, "vs per-corner scatter:", rel, mx)
+        assert rel < 1e-5 and mx < 1e-5, (mode, rel, mx)
 
 
 @pytest.mark.parametrize("n", [4096, 1000, 37])
