@@ -375,8 +375,13 @@ def rgb_train_steps(dev, steps, warmup, fused=True, h=64, w=128):
     net.fused = fused          # False: NeRFRenderer.run_torch under autograd
     net.opt.adaptive_num_rays = False
     opt = FusedAdam(net.get_params(1e-2), eps=1e-15)
-    pose, intr = synth.gui_camera(w, h)
-    ro, rd = ops.get_rays(pose, intr, h, w, device=dev)
+    # the reference's training batch: N rays at random pixels of a view
+    # (utils.py:get_rays with N > 0, torch.randint over H * W), here of a 512^2
+    # GUI view -- not neighbours in the image, so the scatter merges along rays
+    pose, intr = synth.gui_camera(512, 512)
+    ro, rd = ops.get_rays(pose, intr, 512, 512, device=dev)
+    inds = torch.randint(0, 512 * 512, (h * w,), generator=torch.Generator().manual_seed(4)).to(dev)
+    ro, rd = ro[inds].contiguous(), rd[inds].contiguous()
     gt = torch.rand(ro.shape[0], 3, generator=torch.Generator().manual_seed(4)).to(dev)
 
     def step(i):
@@ -405,8 +410,8 @@ RGB_TRAIN_WHAT = {
              "hand-written backward; grid gradients by fp32 atomics)",
     "data": "synthetic parity-weight scene (embeddings U(+-0.5)) at the reference's table sizes, "
             "U(0,1) target colours",
-    "config": {"workload": "RGB training step (utils.py:897-937): 8192 rays (64x128), perturb, "
-                           "MSE + proposal + distortion losses, backward, Adam over all groups",
+    "config": {"workload": "RGB training step (utils.py:897-937): 8192 rays at random pixels of a 512x512 "
+                           "view, perturb, MSE + proposal + distortion losses, backward, Adam over all groups",
                "optimizer": "FusedAdam lr 1e-2 eps 1e-15"},
 }
 
