@@ -126,6 +126,18 @@ __device__ __forceinline__ void load_grid_mlp(const RtArgs& a, float* sw) {
     __syncthreads();
 }
 
+// Sum over the 64 lanes in a fixed order (DPP within rows of 16, then the row
+// broadcasts), as wave_box.h's reductions: wave-uniform result.
+__device__ __forceinline__ float wave_sum(float v) {
+    v += dpp_f<0xB1>(v);                                   // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E>(v);                                   // quad_perm [2,3,0,1]
+    v += dpp_f<0x141>(v);                                  // row_half_mirror
+    v += dpp_f<0x140>(v);                                  // row_mirror: row totals
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xa, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xc, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 // Scatter one sample's d(features) of a C = 2 level into the gradient table
 // (kernel_grid_backward's atomics, gridencoder.cu:252-349).  Float atomics
 // execute at the memory side, priced per 64-B request (MI355X_MICROARCH.md
@@ -549,6 +561,7 @@ __host__ __device__ constexpr uint32_t outer_chunk(size_t S) {
     return (uint32_t)(((S + 1023) / 1024 + 255) / 256 * 256);
 }
 
+template <bool V4>
 __global__ void __launch_bounds__(256) k_rt_outer(const float* __restrict__ A, const float* __restrict__ B,
                                                   uint32_t m, uint32_t n, size_t S, uint32_t chunk,
                                                   float* __restrict__ slab) {
@@ -559,26 +572,50 @@ __global__ void __launch_bounds__(256) k_rt_outer(const float* __restrict__ A, c
     float acc[4][4] = {};
     float* as = reinterpret_cast<float*>(As);
     float* bs = reinterpret_cast<float*>(Bs);
-    // 64 rows x 32 samples of each operand per tile: lane -> (row, sample),
-    // the sample fastest (128-B row segments); the next tile's loads are in
+    // 64 rows x 32 samples of each operand per tile, the sample fastest;
+    // V4 (S % 4 == 0): one 16-B load per lane and operand covers 4 samples of
+    // a row (2 per tile), else 8 scalar loads; the next tile's loads are in
     // flight while this one is multiplied
-    float pa[8], pb[8];
+    constexpr int NL = V4 ? 2 : 8;
+    float4 pa[NL], pb[NL];
     auto fetch = [&](size_t sb) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const uint32_t idx = tid + 256u * q, row = idx >> 5, kk = idx & 31u;
-            const size_t sc = sb + kk;
-            pa[q] = (row < m && sc < s1) ? A[(size_t)row * S + sc] : 0.0f;
-            pb[q] = (row < n && sc < s1) ? B[(size_t)row * S + sc] : 0.0f;
+        for (int q = 0; q < NL; ++q) {
+            if constexpr (V4) {
+                const uint32_t idx = tid + 256u * q, row = idx >> 3, k4 = (idx & 7u) * 4u;
+                const size_t sc = sb + k4;
+                const bool ok = sc < s1;                    // s1 and sc are multiples of 4
+                pa[q] = (row < m && ok) ? *reinterpret_cast<const float4*>(A + (size_t)row * S + sc)
+                                        : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                pb[q] = (row < n && ok) ? *reinterpret_cast<const float4*>(B + (size_t)row * S + sc)
+                                        : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            } else {
+                const uint32_t idx = tid + 256u * q, row = idx >> 5, kk = idx & 31u;
+                const size_t sc = sb + kk;
+                pa[q].x = (row < m && sc < s1) ? A[(size_t)row * S + sc] : 0.0f;
+                pb[q].x = (row < n && sc < s1) ? B[(size_t)row * S + sc] : 0.0f;
+            }
         }
     };
     fetch(s0);
     for (size_t sb = s0; sb < s1; sb += 32) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const uint32_t idx = tid + 256u * q, row = idx >> 5, kk = idx & 31u;
-            as[kk * 68 + row] = pa[q];
-            bs[kk * 68 + row] = pb[q];
+        for (int q = 0; q < NL; ++q) {
+            if constexpr (V4) {
+                const uint32_t idx = tid + 256u * q, row = idx >> 3, k4 = (idx & 7u) * 4u;
+                as[(k4 + 0) * 68 + row] = pa[q].x;
+                as[(k4 + 1) * 68 + row] = pa[q].y;
+                as[(k4 + 2) * 68 + row] = pa[q].z;
+                as[(k4 + 3) * 68 + row] = pa[q].w;
+                bs[(k4 + 0) * 68 + row] = pb[q].x;
+                bs[(k4 + 1) * 68 + row] = pb[q].y;
+                bs[(k4 + 2) * 68 + row] = pb[q].z;
+                bs[(k4 + 3) * 68 + row] = pb[q].w;
+            } else {
+                const uint32_t idx = tid + 256u * q, row = idx >> 5, kk = idx & 31u;
+                as[kk * 68 + row] = pa[q].x;
+                bs[kk * 68 + row] = pb[q].x;
+            }
         }
         __syncthreads();
         if (sb + 32 < s1) fetch(sb + 32);
@@ -604,14 +641,15 @@ __global__ void __launch_bounds__(256) k_rt_outer(const float* __restrict__ A, c
 
 // out[e] = sum over slab rows in a fixed order: 16 outputs x 16 row groups per
 // block, the groups combined in order through LDS
-__global__ void __launch_bounds__(256) k_rt_outer_sum(const float* __restrict__ slab, uint32_t mn,
-                                                      uint32_t blocks, float* __restrict__ out) {
+__global__ void __launch_bounds__(256) k_rt_outer_sum(const float* __restrict__ slab, uint32_t stride,
+                                                      uint32_t off, uint32_t mn, uint32_t blocks,
+                                                      float* __restrict__ out) {
     __shared__ float part[16][17];
     const uint32_t tid = threadIdx.x, eo = tid & 15u, g = tid >> 4, e = blockIdx.x * 16u + eo;
     float acc = 0.0f;
     if (e < mn) {
 #pragma unroll 8
-        for (uint32_t b = g; b < blocks; b += 16u) acc += slab[(size_t)b * mn + e];
+        for (uint32_t b = g; b < blocks; b += 16u) acc += slab[(size_t)b * stride + off + e];
     }
     part[g][eo] = acc;
     __syncthreads();
@@ -644,10 +682,7 @@ struct PropBwdArgs {
     float* dds;               // [T][N]
     float* terms;             // [4][N] (row 1 accumulates the proposal loss)
     // per sample s = T r + k: [channel][T N]
-    float* dh;                // [16]
-    float* feat;              // [10]
-    float* h;                 // [16]
-    float* dx;                // [1]
+    float* slab;              // [blocks][176] per-block prop_mlp gradient sums
     float* grad_grid;         // [rows][2]
 };
 
@@ -731,13 +766,24 @@ __global__ void __launch_bounds__(32) k_rt_prop_ray(PropBwdArgs a) {
 
 // One thread per proposal sample, ray-major (s = T r + k): the density network of
 // the stage (network.py:248-259) re-evaluated, then its backward.
+constexpr uint32_t kPropW = 176;            // prop_mlp gradients: [16,10] then [1,16]
+
 template <int T, bool FIRST>
 __global__ void __launch_bounds__(256) k_rt_prop_bwd(PropBwdArgs a) {
     __shared__ float sstage[4][384];
-    float* stage = sstage[threadIdx.x >> 6];
+    __shared__ float sred[4][kPropW];
+    const uint32_t wv = threadIdx.x >> 6;
+    float* stage = sstage[wv];
     const uint32_t N = a.N;
     const size_t S = (size_t)T * N, s0 = (size_t)blockIdx.x * 256u + threadIdx.x;
-    if ((s0 & ~(size_t)63) >= S) return;                    // whole wave past the end
+    if ((s0 & ~(size_t)63) >= S) {                          // whole wave past the end
+        for (uint32_t i = threadIdx.x & 63u; i < kPropW; i += 64u) sred[wv][i] = 0.0f;
+        __syncthreads();
+        if (threadIdx.x < kPropW)
+            a.slab[(size_t)blockIdx.x * kPropW + threadIdx.x] =
+                sred[0][threadIdx.x] + sred[1][threadIdx.x] + sred[2][threadIdx.x] + sred[3][threadIdx.x];
+        return;
+    }
     const bool live = s0 < S;                               // other lanes stay for the merges
     const size_t s = live ? s0 : S - 1u;                    // ray-major: s = T r + k
     const uint32_t r = (uint32_t)(s / T), k = (uint32_t)(s % T);
@@ -782,19 +828,29 @@ __global__ void __launch_bounds__(256) k_rt_prop_bwd(PropBwdArgs a) {
         for (int q = 0; q < 16; ++q) acc = __builtin_fmaf(a.P0[q * 10 + i], dh[q], acc);
         df[i] = acc;
     }
-    if (live) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            a.dh[q * S + s] = dh[q];
-            a.h[q * S + s] = h[q];
-        }
-#pragma unroll
-        for (int i = 0; i < 10; ++i) a.feat[i * S + s] = f[i];
-        a.dx[s] = dx;
-    }
 #pragma unroll
     for (int l = 0; l < 5; ++l)
         scatter_level_c2(a.grad_grid, a.grid.lv[l], ux, uy, uz, df[2 * l], df[2 * l + 1], live, stage);
+    // the prop_mlp weight gradients dP0 = sum dh f^T, dP1 = sum dx h^T: wave
+    // sums (fixed order), the block's four waves added in order into its slab
+    // row (k_rt_outer_sum adds the rows) -- no [16 + 10 + 16 + 1][T N] round trip
+    const float lv = live ? 1.0f : 0.0f;
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const float dq = dh[q] * lv;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            const float v = wave_sum(dq * f[i]);
+            if (lane == 0) sred[wv][q * 10 + i] = v;
+        }
+        const float v = wave_sum((dx * lv) * h[q]);
+        if (lane == 0) sred[wv][160 + q] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kPropW)
+        a.slab[(size_t)blockIdx.x * kPropW + threadIdx.x] =
+            sred[0][threadIdx.x] + sred[1][threadIdx.x] + sred[2][threadIdx.x] + sred[3][threadIdx.x];
 }
 
 // Means of the per-ray loss terms (fixed-order sums in double): terms rows
@@ -843,14 +899,12 @@ struct RtWorkspace {
     float* dds1;
     float* fin[10];          // pos feat h1 h2 out delta tmid dout dh1 dh2
     float* ray[10];          // w fimg v1 v2 sig dz dv1 dv2 terms, step scratch (g_img 3 | g_ws | g_loss 2)
-    float* prop[4];          // dh feat h dx (stage 0 size, reused by stage 1)
     float* slab;             // k_rt_outer partial sums
     size_t bytes;
 };
 
 constexpr int kFinCh[10] = {3, 32, 64, 64, 16, 1, 1, 16, 64, 64};
 constexpr int kRayCh[10] = {32, 31, 32, 32, 3, 3, 32, 32, 4, 6};
-constexpr int kPropCh[4] = {16, 10, 16, 1};
 
 RtWorkspace carve_rt(uint32_t N, void* base) {
     RtWorkspace w{};
@@ -873,12 +927,10 @@ RtWorkspace carve_rt(uint32_t N, void* base) {
     w.dds1 = take(64 * n);
     for (int i = 0; i < 10; ++i) w.fin[i] = take((size_t)kFinCh[i] * kT * n);
     for (int i = 0; i < 10; ++i) w.ray[i] = take((size_t)kRayCh[i] * n);
-    for (int i = 0; i < 4; ++i) w.prop[i] = take((size_t)kPropCh[i] * 128 * n);
     // the largest slab: grid_mlp.1 (64 x 64) over 32 N samples, or a proposal
     // MLP (16 x 10) over 128 N
     const size_t sf = (size_t)kT * n, sp = (size_t)128 * n;
-    const size_t sb = std::max((size_t)div_up(sf, outer_chunk(sf)) * 4096,
-                               (size_t)div_up(sp, outer_chunk(sp)) * 160);
+    const size_t sb = std::max((size_t)div_up(sf, outer_chunk(sf)) * 4096, (size_t)div_up(sp, 256) * kPropW);
     w.slab = take(sb);
     w.bytes = off;
     return w;
@@ -888,8 +940,9 @@ RtWorkspace carve_rt(uint32_t N, void* base) {
 void outer(const float* A, const float* B, uint32_t m, uint32_t n, size_t S, float* out, float* slab,
            hipStream_t s) {
     const uint32_t chunk = outer_chunk(S), blocks = div_up(S, chunk);
-    k_rt_outer<<<blocks, 256, 0, s>>>(A, B, m, n, S, chunk, slab);
-    k_rt_outer_sum<<<div_up(m * n, 16), 256, 0, s>>>(slab, m * n, blocks, out);
+    if (S % 4 == 0) k_rt_outer<true><<<blocks, 256, 0, s>>>(A, B, m, n, S, chunk, slab);
+    else k_rt_outer<false><<<blocks, 256, 0, s>>>(A, B, m, n, S, chunk, slab);
+    k_rt_outer_sum<<<div_up(m * n, 16), 256, 0, s>>>(slab, m * n, 0u, m * n, blocks, out);
 }
 
 
@@ -964,10 +1017,7 @@ int rt_setup(const samnerf_model* m, const float* rays_o, const float* rays_d, u
     pb.wf = a.w;
     pb.c_prop = (float)(1.0 / (32.0 * N));
     pb.terms = a.terms;
-    pb.dh = w.prop[0];
-    pb.feat = w.prop[1];
-    pb.h = w.prop[2];
-    pb.dx = w.prop[3];
+    pb.slab = w.slab;
     return SAMNERF_OK;
 }
 
@@ -1039,10 +1089,11 @@ int rt_backward(const samnerf_model* m, uint32_t N, bool with_prop, const samner
             rt_prop_stage(m, c, w, st);
             pb.grad_grid = g->prop[st];
             const uint32_t T = st ? 64u : 128u;
-            if (st) k_rt_prop_bwd<64, false><<<div_up((uint64_t)T * N, 256), 256, 0, s>>>(pb);
-            else k_rt_prop_bwd<128, true><<<div_up((uint64_t)T * N, 256), 256, 0, s>>>(pb);
-            outer(pb.dh, pb.feat, 16, 10, (size_t)T * N, g->prop_mlp[st][0], w.slab, s);
-            outer(pb.dx, pb.h, 1, 16, (size_t)T * N, g->prop_mlp[st][1], w.slab, s);
+            const uint32_t blocks = div_up((uint64_t)T * N, 256);
+            if (st) k_rt_prop_bwd<64, false><<<blocks, 256, 0, s>>>(pb);
+            else k_rt_prop_bwd<128, true><<<blocks, 256, 0, s>>>(pb);
+            k_rt_outer_sum<<<div_up(160, 16), 256, 0, s>>>(w.slab, kPropW, 0u, 160u, blocks, g->prop_mlp[st][0]);
+            k_rt_outer_sum<<<1, 256, 0, s>>>(w.slab, kPropW, 160u, 16u, blocks, g->prop_mlp[st][1]);
         }
     }
     return SAMNERF_OK;
