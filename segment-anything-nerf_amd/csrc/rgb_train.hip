@@ -10,7 +10,8 @@
 //   proposal stages     the fused render's own kernels (raymarch.hip
 //                       proposal_forward): ds, weights and bins of both stages
 //   k_rt_final_fwd      one thread per final sample: bins -> position ->
-//                       contract -> grid L16C2 gather -> grid_mlp (exact fp32,
+//                       contract -> grid L16C2 gather (packed / pair-load form,
+//                       bit-identical to the reference's) -> grid_mlp (exact fp32,
 //                       weights in LDS); saves u, grid features, both hidden
 //                       layers and the 16 outputs
 //   k_rt_composite      one thread per ray: compositing (renderer.py:309-335),
@@ -244,7 +245,7 @@ __global__ void __launch_bounds__(256) k_rt_final_fwd(RtArgs a) {
     a.tmid[s] = t;
     float f[32];
 #pragma unroll
-    for (int l = 0; l < 16; ++l) lookup_level3_ref<2>(a.grid.emb, a.grid.lv[l], ux, uy, uz, f + 2 * l);
+    for (int l = 0; l < 16; ++l) lookup_level3<2>(a.grid.emb, a.grid.lv[l], ux, uy, uz, f + 2 * l);
 #pragma unroll
     for (int i = 0; i < 32; ++i) a.feat[i * S + s] = f[i];
     float h[64];
@@ -803,7 +804,7 @@ __global__ void __launch_bounds__(256) k_rt_prop_bwd(PropBwdArgs a) {
     const float ux = gu(x), uy = gu(y), uz = gu(z);
     float f[10];
 #pragma unroll
-    for (int l = 0; l < 5; ++l) lookup_level3_ref<2>(a.grid.emb, a.grid.lv[l], ux, uy, uz, f + 2 * l);
+    for (int l = 0; l < 5; ++l) lookup_level3<2>(a.grid.emb, a.grid.lv[l], ux, uy, uz, f + 2 * l);
     float h[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
