@@ -331,7 +331,9 @@ size_t samnerf_rgb_train_workspace_size(const samnerf_model* model, uint32_t N);
  * grad (renderer.py:221-362), differentiable outputs image, depth, weights_sum and
  * the render's own losses (proposal_loss when with_proposal, distort_loss), the
  * Trainer's criterion left to the caller:
- *   forward: losses [2] (device) = (proposal_loss, distort_loss), unweighted; keeps
+ *   forward: weights [N,32] (or NULL) = the final samples' weights, results['weights']
+ *     of renderer.py:350 (not differentiable); losses [2] (device) = (proposal_loss,
+ *     distort_loss), unweighted; keeps
  *     what the backward reads in `workspace` (same model, rays, N, perturb arrays);
  *   backward: grad_image [N,3], grad_weights_sum [N] / grad_depth [N] (NULL = 0),
  *     grad_losses [2] (device; NULL = 0, required with with_proposal) -> the
@@ -339,7 +341,7 @@ size_t samnerf_rgb_train_workspace_size(const samnerf_model* model, uint32_t N);
 int samnerf_rgb_train_forward(const samnerf_model* model, const float* rays_o, const float* rays_d,
                               uint32_t N, const float* cam_near_far, uint32_t n_cnf, float bg_color,
                               int with_proposal, float* image, float* depth, float* weights_sum,
-                              float* losses, void* workspace, size_t workspace_bytes,
+                              float* weights, float* losses, void* workspace, size_t workspace_bytes,
                               samnerf_stream_t stream);
 int samnerf_rgb_train_backward(const samnerf_model* model, const float* rays_o, const float* rays_d,
                                uint32_t N, float bg_color, int with_proposal, const float* grad_image,

@@ -113,6 +113,7 @@ struct RtArgs {
     float* image;             // [N][3]
     float* depth;             // [N]
     float* wsum;              // [N]
+    float* weights;           // [N][32] the final weights as results['weights'] (renderer.py:350), or null
     float* grad_grid;         // [rows][2]
 };
 
@@ -303,6 +304,7 @@ __global__ void __launch_bounds__(256) k_rt_composite(RtArgs a) {
         const float sigma = expf(a.out[s]);                 // trunc_exp forward
         const float w = composite_step(a.delta[s] * sigma, cum, k == kT - 1);
         a.w[ks] = w;
+        if (a.weights) a.weights[(size_t)r * kT + k] = w;
         wsd += (double)w;
         dep += (double)(w * a.tmid[s]);
 #pragma unroll
@@ -1035,13 +1037,14 @@ void rt_prop_stage(const samnerf_model* m, RtCall& c, const RtWorkspace& w, int 
 // forward: proposal stages, final samples, compositing; with_prop: the
 // proposal loss and its (unit-weight) gradient through the stages' compositing
 int rt_forward(const samnerf_model* m, const float* rays_o, const float* rays_d, uint32_t N, const float* cnf,
-               uint32_t n_cnf, bool with_prop, float* image, float* depth, float* weights_sum, RtCall& c,
-               const RtWorkspace& w, hipStream_t s) {
+               uint32_t n_cnf, bool with_prop, float* image, float* depth, float* weights_sum, float* weights,
+               RtCall& c, const RtWorkspace& w, hipStream_t s) {
     int rc = proposal_forward(m, c.geo, rays_o, rays_d, N, cnf, n_cnf, w.p, s);
     if (rc) return rc;
     c.a.image = image;
     c.a.depth = depth;
     c.a.wsum = weights_sum;
+    c.a.weights = weights;
     k_rt_final_fwd<<<div_up((uint64_t)kT * N, 256), 256, 0, s>>>(c.a);
     k_rt_composite<<<div_up(N, 256), 256, 0, s>>>(c.a);
     if (with_prop) {
@@ -1113,8 +1116,8 @@ size_t samnerf_rgb_train_workspace_size(const samnerf_model* model, uint32_t N) 
 
 int samnerf_rgb_train_forward(const samnerf_model* m, const float* rays_o, const float* rays_d, uint32_t N,
                               const float* cam_near_far, uint32_t n_cnf, float bg_color, int with_proposal,
-                              float* image, float* depth, float* weights_sum, float* losses, void* workspace,
-                              size_t workspace_bytes, samnerf_stream_t stream) {
+                              float* image, float* depth, float* weights_sum, float* weights, float* losses,
+                              void* workspace, size_t workspace_bytes, samnerf_stream_t stream) {
     if (!m) return fail(SAMNERF_EINVAL, "rgb_train_forward: null model");
     if (N == 0) return SAMNERF_OK;
     if (!rays_o || !rays_d || !image || !depth || !weights_sum || !losses)
@@ -1132,7 +1135,7 @@ int samnerf_rgb_train_forward(const samnerf_model* m, const float* rays_o, const
     int rc = rt_setup(m, rays_o, rays_d, N, bg_color, w, c);
     if (rc) return rc;
     if ((rc = rt_forward(m, rays_o, rays_d, N, cam_near_far, n_cnf, with_proposal != 0, image, depth,
-                         weights_sum, c, w, s)))
+                         weights_sum, weights, c, w, s)))
         return rc;
     k_rt_loss<<<1, 256, 0, s>>>(c.a.terms, N, 1, 2, 0.0f, 0.0f, 0.0f, 0, nullptr, losses);
     return check_launch("rgb_train_forward");
@@ -1189,8 +1192,8 @@ int samnerf_rgb_train_step(const samnerf_model* m, const float* rays_o, const fl
     RtCall c;
     int rc = rt_setup(m, rays_o, rays_d, N, opts->bg_color, w, c);
     if (rc) return rc;
-    if ((rc = rt_forward(m, rays_o, rays_d, N, cam_near_far, n_cnf, with_prop, image, depth, weights_sum, c, w,
-                         s)))
+    if ((rc = rt_forward(m, rays_o, rays_d, N, cam_near_far, n_cnf, with_prop, image, depth, weights_sum, nullptr,
+                         c, w, s)))
         return rc;
     // the Trainer's loss (utils.py:917-931) and its upstream gradients
     float* g_img = w.ray[9];

@@ -424,6 +424,7 @@ class _FusedRGBTrain(torch.autograd.Function):
         image = torch.empty(N, 3, device=dev)
         depth = torch.empty(N, device=dev)
         wsum = torch.empty(N, device=dev)
+        weights = torch.empty(N, int(m.num_steps[2]), device=dev)
         losses = torch.zeros(2, device=dev)
         n_cnf = 0 if cnf is None else cnf.shape[0]
         try:
@@ -431,17 +432,19 @@ class _FusedRGBTrain(torch.autograd.Function):
                 m.perturb[i] = None if pert is None else _param(pert[i], f"perturb[{i}]")
             check(lib().samnerf_rgb_train_forward(
                 ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, _ptr(cnf), n_cnf, float(bg), int(with_prop),
-                _ptr(image), _ptr(depth), _ptr(wsum), _ptr(losses), _ptr(ws), need, _stream(rays_o)),
+                _ptr(image), _ptr(depth), _ptr(wsum), _ptr(weights), _ptr(losses), _ptr(ws), need,
+                _stream(rays_o)),
                 "rgb_train_forward")
         finally:
             for i in range(3):
                 m.perturb[i] = None
         ctx.state = (renderer, m, rays_o, rays_d, bg, pert, with_prop, ws, need, list(renderer._keep))
         ctx.shapes = [p.shape for p in params]
-        return image, depth, wsum, losses[0], losses[1]
+        ctx.mark_non_differentiable(weights)
+        return image, depth, wsum, losses[0], losses[1], weights
 
     @staticmethod
-    def backward(ctx, g_img, g_depth, g_wsum, g_prop, g_dist):
+    def backward(ctx, g_img, g_depth, g_wsum, g_prop, g_dist, _g_weights):
         renderer, m, rays_o, rays_d, bg, pert, with_prop, ws, need, _ = ctx.state
         dev = rays_o.device
         N = rays_o.shape[0]
@@ -493,9 +496,10 @@ def render_rgb_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None,
         pert = tuple(t.contiguous().float() for t in pert)
     cnf = None if cam_near_far is None else cam_near_far.contiguous().float()
     with_prop = bool(update_proposal) and getattr(opt, "lambda_proposal", 0) > 0
-    image, depth, wsum, prop_loss, dist_loss = _FusedRGBTrain.apply(
+    image, depth, wsum, prop_loss, dist_loss, weights = _FusedRGBTrain.apply(
         renderer, rays_o, rays_d, cnf, bg, pert, with_prop, *rgb_train_params(net, with_prop))
-    out = {"num_points": N * int(m.num_steps[2]), "weights_sum": wsum, "depth": depth, "image": image}
+    out = {"num_points": N * int(m.num_steps[2]), "weights": weights, "weights_sum": wsum, "depth": depth,
+           "image": image}
     if with_prop:
         out["proposal_loss"] = prop_loss
     if getattr(opt, "lambda_distort", 0) > 0:
