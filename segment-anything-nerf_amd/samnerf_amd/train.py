@@ -48,16 +48,6 @@ def rgb_train_step(model, rays_o, rays_d, gt_rgb, global_step, bg_color=None,
     return pred_rgb, loss, outputs
 
 
-def _rgb_grad_params(model):
-    """The trained tensors in samnerf_rgb_grads order, and which of them are the
-    proposal networks' (network.py:201-206 get_params groups)."""
-    main = [model.grid.embeddings] + [model.grid_mlp.net[i].weight for i in range(3)] + \
-        [model.view_mlp.net[i].weight for i in range(3)]
-    prop = [model.prop_encoders[0].embeddings, model.prop_encoders[1].embeddings] + \
-        [model.prop_mlp[p].net[i].weight for p in range(2) for i in range(2)]
-    return main, prop
-
-
 def rgb_train_step_fused(model, rays_o, rays_d, gt_rgb, global_step, bg_color=None,
                          cam_near_far=None, perturb=True):
     """rgb_train_step on the HIP training kernels (samnerf_rgb_train_step,
@@ -72,7 +62,7 @@ def rgb_train_step_fused(model, rays_o, rays_d, gt_rgb, global_step, bg_color=No
     import ctypes
 
     from ._lib import SamnerfRgbGrads, SamnerfRgbTrainOpts, check, lib
-    from .fused import FusedRenderer, perturbed_positions
+    from .fused import FusedRenderer, perturbed_positions, rgb_train_params
     from .ops import _ptr, _stream
 
     opt = model.opt
@@ -110,7 +100,8 @@ def rgb_train_step_fused(model, rays_o, rays_d, gt_rgb, global_step, bg_color=No
     o.update_proposal = int(bool(update_proposal))
     o.bg_color = float(bg_color)
     with_prop = bool(update_proposal) and o.lambda_proposal > 0
-    main, prop = _rgb_grad_params(model)
+    every = rgb_train_params(model, True)
+    main, prop = every[:7], every[7:]
     for p in main + (prop if with_prop else []):
         if p.grad is None or p.grad.shape != p.shape or not p.grad.is_contiguous():
             p.grad = torch.empty_like(p)
