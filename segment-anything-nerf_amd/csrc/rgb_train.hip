@@ -3,34 +3,42 @@
 // lambda_proposal * proposal_loss + lambda_distort * distort_loss (+
 // lambda_entropy * entropy), backward) as gfx950 kernels: the forward keeps
 // what the backward needs, the backward is written out by hand -- no autograd
-// graph, no [N, T, C] temporaries, ~17 launches instead of the ~700 ATen
-// kernels of the torch path (nerf/renderer.py run_torch + autograd).
+// graph, no [N, T, C] temporaries, ~25 launches instead of the ~700 ATen
+// kernels of the torch path (nerf/renderer.py run_torch + autograd).  Entry
+// points: samnerf_rgb_train_forward / _backward (an autograd pair: the train-
+// mode NeRFRenderer.run) and samnerf_rgb_train_step (both plus the Trainer's
+// MSE / entropy terms in one call).
 //
 // Forward
 //   proposal stages     the fused render's own kernels (raymarch.hip
 //                       proposal_forward): ds, weights and bins of both stages
-//   k_rt_final_fwd      one thread per final sample: bins -> position ->
-//                       contract -> grid L16C2 gather (packed / pair-load form,
-//                       bit-identical to the reference's) -> grid_mlp (exact fp32,
-//                       weights in LDS); saves u, grid features, both hidden
-//                       layers and the 16 outputs
+//   k_rt_final_fwd      one thread per final sample (ray-major): bins ->
+//                       position -> contract -> grid L16C2 gather (packed /
+//                       pair-load form, bit-identical to the reference's) ->
+//                       grid_mlp (exact fp32, weights in LDS); saves u, grid
+//                       features, both hidden layers and the 16 outputs
 //   k_rt_composite      one thread per ray: compositing (renderer.py:309-335),
 //                       SH(4), f_image, view_mlp, sigmoid, background; the
-//                       per-ray loss terms (MSE, distortion, entropy)
+//                       per-ray distortion term
+//   k_rt_prop_ray<T>    per ray and stage: proposal_loss (renderer.py:30-57)
+//                       and its gradient w.r.t. the stage's weights (the final
+//                       stage's are detached) through the stage's compositing
+//                       (unit loss weight; the backward scales it)
 // Backward
-//   k_rt_final_bwd_ray  per ray: loss -> image -> view_mlp -> f_image ->
-//                       weights (+ distortion, entropy, background terms) ->
-//                       delta*sigma (reverse scan) -> trunc_exp -> d(grid_mlp out)
+//   k_rt_final_bwd_ray  per ray: d(image), d(weights_sum), d(depth) -> view_mlp
+//                       -> f_image -> weights (+ distortion) -> delta*sigma
+//                       (reverse scan) -> trunc_exp -> d(grid_mlp out)
 //   k_rt_final_bwd      per sample: grid_mlp backward, d(grid features) scattered
 //                       into grid.embeddings' gradient (float atomics, as
-//                       kernel_grid_backward, gridencoder.cu:252-349)
-//   k_rt_prop_ray<T>    per ray and stage: proposal_loss (renderer.py:30-57)
-//                       w.r.t. the stage's weights (the final stage's are
-//                       detached), then the stage's compositing backward
-//   k_rt_prop_bwd<T>    per proposal sample: prop_mlp backward + prop grid scatter
-//   k_rt_outer          weight gradients dW = sum_s dY[:, s] X[:, s]^T (split-K,
-//                       LDS tiles, one atomic per output and chunk)
-//   k_rt_loss           the loss terms, fixed-order reductions
+//                       kernel_grid_backward, gridencoder.cu:252-349; shaped
+//                       per wave: run merge, lane quads, zero-wave skip)
+//   k_rt_prop_bwd<T>    per proposal sample: prop_mlp backward, prop grid
+//                       scatter, prop_mlp weight gradients as wave sums
+//   k_rt_outer          grid_mlp / view_mlp weight gradients dW = sum_s dY[:, s]
+//                       X[:, s]^T (split-K, 4 x 4 register tiles, slab rows
+//                       summed in a fixed order by k_rt_outer_sum)
+//   k_rt_rgb_loss_grad, k_rt_loss   the one-call step's MSE / entropy terms and
+//                       their upstream gradients; fixed-order loss means
 // Arithmetic is fp32 throughout (the reference's precision); the forward
 // repeats the fused render's op order (bins, positions, gathers, compositing),
 // so its proposal stages are bit-identical to samnerf_render_forward's.
