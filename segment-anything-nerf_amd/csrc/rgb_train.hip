@@ -17,7 +17,7 @@
 //                       pair-load form, bit-identical to the reference's) ->
 //                       grid_mlp (exact fp32, weights in LDS); saves u, grid
 //                       features, both hidden layers and the 16 outputs
-//   k_rt_composite      one thread per ray: compositing (renderer.py:309-335),
+//   k_rt_composite_h    a half-wave per ray: compositing (renderer.py:309-335),
 //                       SH(4), f_image, view_mlp, sigmoid, background; the
 //                       per-ray distortion term
 //   k_rt_prop_ray_w<T>  per ray (a wave) and stage: proposal_loss (renderer.py:30-57)
@@ -25,7 +25,7 @@
 //                       stage's are detached) through the stage's compositing
 //                       (unit loss weight; the backward scales it)
 // Backward
-//   k_rt_final_bwd_ray  per ray: d(image), d(weights_sum), d(depth) -> view_mlp
+//   k_rt_final_bwd_ray_h  a half-wave per ray: d(image), d(weights_sum), d(depth) -> view_mlp
 //                       -> f_image -> weights (+ distortion) -> delta*sigma
 //                       (reverse scan) -> trunc_exp -> d(grid_mlp out)
 //   k_rt_final_bwd      per sample: grid_mlp backward, d(grid features) scattered
@@ -58,7 +58,6 @@ namespace {
 constexpr int kT = 32;                                    // final samples per ray
 constexpr int kG0 = 64 * 32, kG1 = 64 * 64, kG2 = 16 * 64; // grid_mlp [64,32] [64,64] [16,64]
 constexpr int kGW = kG0 + kG1 + kG2;
-constexpr int kV1 = 32 * 31, kV2 = kV1 + 32 * 32, kVW = kV2 + 3 * 32;   // view_mlp in LDS
 
 // torch.linspace(start, end, steps) on the CPU (samnerf_linspace_host; the
 // same formula as raymarch.hip's stage-0 bins)
@@ -294,80 +293,6 @@ __device__ __forceinline__ void ray_sh(const RtArgs& a, uint32_t r, float* sh) {
     sh_values<4>(dx, dy, dz, sh);
 }
 
-// One thread per ray: renderer.py:309-358 (last_sample background) plus the
-// per-ray loss terms of utils.py:917-931.
-__global__ void __launch_bounds__(256) k_rt_composite(RtArgs a) {
-    const uint32_t N = a.N, r = blockIdx.x * 256u + threadIdx.x;
-    if (r >= N) return;
-    const size_t S = (size_t)kT * N;
-    double cum = 0.0, wsd = 0.0, dep = 0.0;
-    float fg[15];
-#pragma unroll
-    for (int j = 0; j < 15; ++j) fg[j] = 0.0f;
-    float W = 0.0f, WM = 0.0f, bi = 0.0f, uni = 0.0f;     // distortion (renderer.py:17-27)
-    float b0 = a.bins2[r];
-#pragma unroll 2
-    for (int k = 0; k < kT; ++k) {
-        const size_t s = (size_t)r * kT + k, ks = (size_t)k * N + r;
-        const float sigma = expf(a.out[s]);                 // trunc_exp forward
-        const float w = composite_step(a.delta[s] * sigma, cum, k == kT - 1);
-        a.w[ks] = w;
-        if (a.weights) a.weights[(size_t)r * kT + k] = w;
-        wsd += (double)w;
-        dep += (double)(w * a.tmid[s]);
-#pragma unroll
-        for (int j = 0; j < 15; ++j) fg[j] = fg[j] + w * a.out[(size_t)(1 + j) * S + s];
-        const float b1 = a.bins2[ks + N];
-        const float iv = b1 - b0, mid = b0 + iv / 2.0f;
-        b0 = b1;
-        uni = uni + iv * (w * w);
-        const float wm = w * mid;
-        if (k > 0) bi = bi + (wm * W - w * WM);
-        W = W + w;
-        WM = WM + wm;
-    }
-    const float ws = (float)wsd;
-    float sh[16];
-    ray_sh(a, r, sh);
-    float fi[31];
-#pragma unroll
-    for (int j = 0; j < 15; ++j) fi[j] = fg[j];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) fi[15 + j] = sh[j] * ws;
-#pragma unroll
-    for (int j = 0; j < 31; ++j) a.fimg[(size_t)j * N + r] = fi[j];
-    float v1[32], v2[32];
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 31; ++i) acc = __builtin_fmaf(a.V[0][q * 31 + i], fi[i], acc);
-        v1[q] = fmaxf(acc, 0.0f);
-        a.v1[(size_t)q * N + r] = v1[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 32; ++i) acc = __builtin_fmaf(a.V[1][q * 32 + i], v1[i], acc);
-        v2[q] = fmaxf(acc, 0.0f);
-        a.v2[(size_t)q * N + r] = v2[q];
-    }
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 32; ++i) acc = __builtin_fmaf(a.V[2][c * 32 + i], v2[i], acc);
-        const float sg = sigmoidf(acc);
-        a.sig[(size_t)c * N + r] = sg;
-        a.image[(size_t)r * 3 + c] = sg + (1.0f - ws) * a.bg;
-    }
-    a.depth[r] = (float)dep;
-    a.wsum[r] = ws;
-    a.terms[N + r] = 0.0f;
-    a.terms[2 * N + r] = 2.0f * bi + uni / 3.0f;
-}
-
 // The Trainer's own terms for the one-call step (utils.py:917, 926-929): per
 // ray MSE and entropy, and their gradients w.r.t. image and weights_sum -- the
 // upstream gradients a torch criterion would hand the render's backward.
@@ -392,22 +317,115 @@ __global__ void __launch_bounds__(256) k_rt_rgb_loss_grad(RtArgs a, const float*
                                                                       : 0.0f;
 }
 
-// ------------------------------------------------------------ backward --
+// Half-wave (32-lane) helpers: lane k of a half = sample k of its ray.
+template <class V>
+__device__ __forceinline__ V half_sum(V v) {
+#pragma unroll
+    for (int m = 1; m < 32; m <<= 1) v += __shfl_xor(v, m, 32);
+    return v;
+}
+template <class V>
+__device__ __forceinline__ V half_incl_scan(V v, uint32_t k) {
+#pragma unroll
+    for (uint32_t sd = 1; sd < 32u; sd <<= 1) {
+        const V o = __shfl_up(v, sd, 32);
+        if (k >= sd) v += o;
+    }
+    return v;
+}
+template <class V>
+__device__ __forceinline__ V half_incl_suffix(V v, uint32_t k) {
+#pragma unroll
+    for (uint32_t sd = 1; sd < 32u; sd <<= 1) {
+        const V o = __shfl_down(v, sd, 32);
+        if (k + sd < 32u) v += o;
+    }
+    return v;
+}
 
-// One thread per ray (64 per block): d(loss) -> d(image) -> view_mlp ->
-// f_image -> weights -> delta*sigma -> d(grid_mlp output) of every final
-// sample.  The per-sample terms of the reverse scan live in LDS ([k][lane]:
-// no bank conflicts), not in 96 registers.
-__global__ void __launch_bounds__(64) k_rt_final_bwd_ray(RtArgs a) {
-    __shared__ float sdw[kT][64], sraw[kT][64], sev[kT][64];
-    __shared__ float sv[kVW];
-    for (int i = threadIdx.x; i < 32 * 31; i += 64) sv[i] = a.V[0][i];
-    for (int i = threadIdx.x; i < 32 * 32; i += 64) sv[kV1 + i] = a.V[1][i];
-    for (int i = threadIdx.x; i < 3 * 32; i += 64) sv[kV2 + i] = a.V[2][i];
-    __syncthreads();
-    const uint32_t N = a.N, lane = threadIdx.x, r = blockIdx.x * 64u + lane;
+// Compositing with one half-wave per ray (8 rays per block; renderer.py:309-358,
+// last_sample background, plus the per-ray distortion term): lane k
+// composites sample k (the exclusive double cumsum of delta * sigma as a scan,
+// as composite_step orders it), the ray's sums are half-wave reductions, and
+// the view MLP runs unit-per-lane (v1 / v2 unit q on lane q).  (The first form,
+// one thread per ray, ran 128 waves for 8K rays: it and its backward took
+// 0.25 ms of the step; these 0.02.)
+__global__ void __launch_bounds__(256) k_rt_composite_h(RtArgs a) {
+    const uint32_t N = a.N, k = threadIdx.x & 31u;
+    const uint32_t r0 = blockIdx.x * 8u + (threadIdx.x >> 5);
+    if (r0 >= N) return;                                   // whole half (no barriers below)
+    const uint32_t r = r0;
+    const size_t S = (size_t)kT * N, s = (size_t)r * kT + k, ks = (size_t)k * N + r;
+    const bool last = k == (uint32_t)kT - 1u;
+    const float sigma = expf(a.out[s]);                    // trunc_exp forward
+    const float ds = last ? INFINITY : a.delta[s] * sigma;
+    const double dsd = last ? 0.0 : (double)ds;
+    const double cum = half_incl_scan(dsd, k) - dsd;       // before sample k
+    const float w = nan_to_num((1.0f - expf(-ds)) * expf(-(float)cum));
+    a.w[ks] = w;
+    if (a.weights) a.weights[s] = w;
+    const double wsd = half_sum((double)w);
+    const double dep = half_sum((double)(w * a.tmid[s]));
+    float fg[15];
+#pragma unroll
+    for (int j = 0; j < 15; ++j) fg[j] = half_sum(w * a.out[(size_t)(1 + j) * S + s]);
+    // distortion (renderer.py:17-27 via eff_distloss): per sample
+    // w_k m_k W_<k - w_k WM_<k, and s_k w_k^2
+    const float b0 = a.bins2[ks], b1 = a.bins2[ks + N];
+    const float iv = b1 - b0, mid = b0 + iv / 2.0f, wm = w * mid;
+    const float Wx = half_incl_scan(w, k) - w, WMx = half_incl_scan(wm, k) - wm;
+    const float bi = half_sum(k > 0 ? (wm * Wx - w * WMx) : 0.0f);
+    const float uni = half_sum(iv * (w * w));
+    const float ws = (float)wsd;
+    float sh[16];
+    ray_sh(a, r, sh);
+    float fi[31];
+#pragma unroll
+    for (int j = 0; j < 15; ++j) fi[j] = fg[j];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) fi[15 + j] = sh[j] * ws;
+#pragma unroll
+    for (int j = 0; j < 31; ++j)
+        if (k == (uint32_t)j) a.fimg[(size_t)j * N + r] = fi[j];
+    // view MLP, unit q on lane q
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 31; ++i) acc = __builtin_fmaf(a.V[0][k * 31 + i], fi[i], acc);
+    const float v1 = fmaxf(acc, 0.0f);
+    a.v1[(size_t)k * N + r] = v1;
+    acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) acc = __builtin_fmaf(a.V[1][k * 32 + i], __shfl(v1, i, 32), acc);
+    const float v2 = fmaxf(acc, 0.0f);
+    a.v2[(size_t)k * N + r] = v2;
+    float z[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) z[c] = half_sum(a.V[2][c * 32 + k] * v2);
+    if (k < 3u) {
+        const float zc = k == 0 ? z[0] : k == 1 ? z[1] : z[2];
+        const float sg = sigmoidf(zc);
+        a.sig[(size_t)k * N + r] = sg;
+        a.image[(size_t)r * 3 + k] = sg + (1.0f - ws) * a.bg;
+    }
+    if (k == 0) {
+        a.depth[r] = (float)dep;
+        a.wsum[r] = ws;
+        a.terms[N + r] = 0.0f;
+        a.terms[2 * N + r] = 2.0f * bi + uni / 3.0f;
+    }
+}
+
+// The per-ray backward with one half-wave per ray: d(image), d(weights_sum),
+// d(depth) -> sigmoid -> the view MLP backward
+// unit-per-lane (dv2 / dv1 unit on its lane, d f_image component j on lane j),
+// then sample k on lane k: d(loss)/d(w_k), the distortion terms from prefix
+// scans, and the compositing reverse scan as a suffix scan.
+__global__ void __launch_bounds__(256) k_rt_final_bwd_ray_h(RtArgs a) {
+    const uint32_t N = a.N, k = threadIdx.x & 31u;
+    const uint32_t r = blockIdx.x * 8u + (threadIdx.x >> 5);
     if (r >= N) return;
-    const size_t S = (size_t)kT * N;
+    const size_t S = (size_t)kT * N, s = (size_t)r * kT + k, ks = (size_t)k * N + r;
+    const bool last = k == (uint32_t)kT - 1u;
     float dimg[3], dz[3], dws = a.g_ws ? a.g_ws[r] : 0.0f;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -415,102 +433,71 @@ __global__ void __launch_bounds__(64) k_rt_final_bwd_ray(RtArgs a) {
         dws = dws - dimg[c] * a.bg;                         // image += (1 - weights_sum) * bg
         const float sg = a.sig[(size_t)c * N + r];
         dz[c] = dimg[c] * (1.0f - sg) * sg;                 // sigmoid backward
-        a.dz[(size_t)c * N + r] = dz[c];
     }
+    if (k < 3u) a.dz[(size_t)k * N + r] = k == 0 ? dz[0] : k == 1 ? dz[1] : dz[2];
     const float gdep = a.g_depth ? a.g_depth[r] : 0.0f;     // depth = sum_k w_k t_k
     const float c_dist = a.g_loss ? a.g_loss[1] * a.inv_n : 0.0f;
-    // transposed products as row sweeps (W^T g = sum_q g_q W[q, :]), the same
-    // ascending-q accumulation order per output
-    float dv2[32], dv1[32], dfi[31];
+    // view MLP backward: unit q on lane q (ascending-q sums as the VALU form)
+    float acc = 0.0f;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) dv2[i] = 0.0f;
+    for (int c = 0; c < 3; ++c) acc = __builtin_fmaf(a.V[2][c * 32 + k], dz[c], acc);
+    const float dv2 = a.v2[(size_t)k * N + r] > 0.0f ? acc : 0.0f;
+    a.dv2[(size_t)k * N + r] = dv2;
+    acc = 0.0f;
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
+    for (int q = 0; q < 32; ++q) acc = __builtin_fmaf(a.V[1][q * 32 + k], __shfl(dv2, q, 32), acc);
+    const float dv1 = a.v1[(size_t)k * N + r] > 0.0f ? acc : 0.0f;
+    a.dv1[(size_t)k * N + r] = dv1;
+    acc = 0.0f;
+    const uint32_t jj = k < 31u ? k : 30u;
 #pragma unroll
-        for (int i = 0; i < 32; ++i) dv2[i] = __builtin_fmaf(sv[kV2 + c * 32 + i], dz[c], dv2[i]);
+    for (int q = 0; q < 32; ++q) acc = __builtin_fmaf(a.V[0][q * 31 + jj], __shfl(dv1, q, 32), acc);
+    const float dfi_k = acc;                               // d f_image[k], k < 31
+    float dfi[31];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        dv2[i] = a.v2[(size_t)i * N + r] > 0.0f ? dv2[i] : 0.0f;
-        a.dv2[(size_t)i * N + r] = dv2[i];
-        dv1[i] = 0.0f;
-    }
-#pragma unroll 2
-    for (int q = 0; q < 32; ++q)
-#pragma unroll
-        for (int i = 0; i < 32; ++i) dv1[i] = __builtin_fmaf(sv[kV1 + q * 32 + i], dv2[q], dv1[i]);
-#pragma unroll
-    for (int i = 0; i < 31; ++i) dfi[i] = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        dv1[i] = a.v1[(size_t)i * N + r] > 0.0f ? dv1[i] : 0.0f;
-        a.dv1[(size_t)i * N + r] = dv1[i];
-    }
-#pragma unroll 2
-    for (int q = 0; q < 32; ++q)
-#pragma unroll
-        for (int j = 0; j < 31; ++j) dfi[j] = __builtin_fmaf(sv[q * 31 + j], dv1[q], dfi[j]);
+    for (int j = 0; j < 31; ++j) dfi[j] = __shfl(dfi_k, j, 32);
     float sh[16];
     ray_sh(a, r, sh);
-    float shdot = 0.0f;                                     // d f_image[15:] / d w_k = sh
+    float g = dws;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) shdot = __builtin_fmaf(dfi[15 + j], sh[j], shdot);
-    // distortion totals (suffix sums below)
-    float Wt = 0.0f, WMt = 0.0f;
-    if (c_dist != 0.0f)
-        for (int k = 0; k < kT; ++k) {
-            const size_t ks = (size_t)k * N + r;
-            const float b0 = a.bins2[ks], b1 = a.bins2[ks + N], iv = b1 - b0, w = a.w[ks];
-            Wt = Wt + w;
-            WMt = WMt + w * (b0 + iv / 2.0f);
-        }
-    // forward pass: transmittance, raw weights, d(loss)/d(w_k)
-    double cum = 0.0;
-    float W = 0.0f, WM = 0.0f;
-#pragma unroll 1
-    for (int k = 0; k < kT; ++k) {
-        const size_t s = (size_t)r * kT + k, ks = (size_t)k * N + r;
-        const float ds = k == kT - 1 ? INFINITY : a.delta[s] * expf(a.out[s]);
-        const float e = expf(-ds), T = expf(-(float)cum);
-        cum += (double)ds;
-        const float raw = (1.0f - e) * T;
-        const float w = nan_to_num(raw);
-        float g = __builtin_fmaf(gdep, a.tmid[s], shdot + dws);
+    for (int j = 0; j < 16; ++j) g = __builtin_fmaf(dfi[15 + j], sh[j], g);   // d f_image[15:] / d w_k = sh
+    // this sample: forward again, d(loss)/d(w_k)
+    const float ds = last ? INFINITY : a.delta[s] * expf(a.out[s]);
+    const double dsd = last ? 0.0 : (double)ds;
+    const double cum = half_incl_scan(dsd, k) - dsd;
+    const float e = expf(-ds), Tk = expf(-(float)cum);
+    const float raw = (1.0f - e) * Tk;
+    const float w = nan_to_num(raw);
+    g = __builtin_fmaf(gdep, a.tmid[s], g);
 #pragma unroll
-        for (int j = 0; j < 15; ++j) {
-            const size_t q = (size_t)(1 + j) * S + s;
-            g = __builtin_fmaf(dfi[j], a.out[q], g);
-            a.dout[q] = w * dfi[j];
-        }
-        if (c_dist != 0.0f) {
-            const float b0 = a.bins2[ks], b1 = a.bins2[ks + N], iv = b1 - b0, m = b0 + iv / 2.0f;
-            W = W + w;
-            WM = WM + w * m;
-            // d/dw_k [2 sum_i sum_{j<i} w_i w_j (m_i - m_j) + 1/3 sum_i s_i w_i^2]
-            const float before = m * (W - w) - (WM - w * m);
-            const float after = (WMt - WM) - m * (Wt - W);
-            g = __builtin_fmaf(c_dist, 2.0f * (before + after) + (2.0f / 3.0f) * iv * w, g);
-        }
-        const bool fin = isfinite(raw);                     // nan_to_num_ backward
-        sdw[k][lane] = fin ? g : 0.0f;
-        sraw[k][lane] = fin ? raw : 0.0f;
-        sev[k][lane] = e * T;
+    for (int j = 0; j < 15; ++j) {
+        const size_t q = (size_t)(1 + j) * S + s;
+        g = __builtin_fmaf(dfi[j], a.out[q], g);
+        a.dout[q] = w * dfi[j];
     }
-    // reverse pass: d(ds_j) = dw_j e^-ds_j T_j - sum_{k>j} dw_k raw_k; the last
-    // sample's ds is the constant +inf
-    float acc = 0.0f;
-#pragma unroll 1
-    for (int k = kT - 1; k >= 0; --k) {
-        const size_t s = (size_t)r * kT + k;
-        float dx = 0.0f;
-        if (k < kT - 1) {
-            const float dds = sdw[k][lane] * sev[k][lane] - acc;
-            const float x = a.out[s];
-            dx = (dds * a.delta[s]) * expf(fminf(fmaxf(x, -15.0f), 15.0f));   // trunc_exp backward
-        }
-        acc = __builtin_fmaf(sdw[k][lane], sraw[k][lane], acc);
-        a.dout[s] = dx;
+    if (c_dist != 0.0f) {
+        const float b0 = a.bins2[ks], b1 = a.bins2[ks + N], iv = b1 - b0, m = b0 + iv / 2.0f, wm = w * m;
+        const float Wi = half_incl_scan(w, k), WMi = half_incl_scan(wm, k);
+        const float Wt = __shfl(Wi, 31, 32), WMt = __shfl(WMi, 31, 32);
+        // d/dw_k [2 sum_i sum_{j<i} w_i w_j (m_i - m_j) + 1/3 sum_i s_i w_i^2]
+        const float before = m * (Wi - w) - (WMi - wm);
+        const float after = (WMt - WMi) - m * (Wt - Wi);
+        g = __builtin_fmaf(c_dist, 2.0f * (before + after) + (2.0f / 3.0f) * iv * w, g);
     }
+    const bool fin = isfinite(raw);                        // nan_to_num_ backward
+    const float dw = fin ? g : 0.0f;
+    const float dr = fin ? dw * raw : 0.0f;
+    const float after_k = half_incl_suffix(dr, k) - dr;    // sum_{j>k} dw_j raw_j
+    float dx = 0.0f;
+    if (!last) {
+        const float dds = dw * (e * Tk) - after_k;
+        const float x = a.out[s];
+        dx = (dds * a.delta[s]) * expf(fminf(fmaxf(x, -15.0f), 15.0f));   // trunc_exp backward
+    }
+    a.dout[s] = dx;
 }
+
+// ------------------------------------------------------------ backward --
 
 // One thread per final sample: grid_mlp backward (ReLU masks from the saved
 // activations) and the grid scatter.
@@ -1118,7 +1105,7 @@ int rt_forward(const samnerf_model* m, const float* rays_o, const float* rays_d,
     c.a.wsum = weights_sum;
     c.a.weights = weights;
     k_rt_final_fwd<<<div_up((uint64_t)kT * N, 256), 256, 0, s>>>(c.a);
-    k_rt_composite<<<div_up(N, 256), 256, 0, s>>>(c.a);
+    k_rt_composite_h<<<div_up(N, 8), 256, 0, s>>>(c.a);
     if (with_prop) {
         rt_prop_stage(m, c, w, 0);
         k_rt_prop_ray_w<128, true><<<div_up(N, 4), 256, 0, s>>>(c.pb);
@@ -1149,7 +1136,7 @@ int rt_backward(const samnerf_model* m, uint32_t N, bool with_prop, const samner
     if (!ok) return fail(SAMNERF_ELAUNCH, "rgb_train: gradient zero-fill failed");
     RtArgs& a = c.a;
     a.grad_grid = g->grid;
-    k_rt_final_bwd_ray<<<div_up(N, 64), 64, 0, s>>>(a);
+    k_rt_final_bwd_ray_h<<<div_up(N, 8), 256, 0, s>>>(a);
     k_rt_final_bwd<<<div_up((uint64_t)kT * N, 256), 256, 0, s>>>(a);
     const size_t S = (size_t)kT * N;
     outer(a.dh1, a.feat, 64, 32, S, g->grid_mlp[0], w.slab, s);
