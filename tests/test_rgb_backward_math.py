@@ -3,7 +3,7 @@
 autograd of the reference's own expressions (nerf/renderer.py:17-57, 309-326
 as restated in segment-anything-nerf_amd/nerf/renderer.py) on the CPU:
 
-  * compositing (k_rt_final_bwd_ray, k_rt_prop_ray): w_k = (1 - e^-ds_k) T_k,
+  * compositing (k_rt_final_bwd_ray_h, k_rt_prop_ray_w): w_k = (1 - e^-ds_k) T_k,
     T_k = exp(-sum_{j<k} ds_j), last ds = +inf (no gradient), nan_to_num_:
     d ds_j = dw_j e^-ds_j T_j - sum_{k>j} dw_k w_k   (reverse scan);
   * distortion (eff_distloss): d/dw_k = 2 (m_k W_<k - WM_<k + WM_>k - m_k W_>k)
