@@ -44,6 +44,7 @@
 // so its proposal stages are bit-identical to samnerf_render_forward's.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "raymarch_device.h"
@@ -122,6 +123,8 @@ struct RtArgs {
     float* wsum;              // [N]
     float* weights;           // [N][32] the final weights as results['weights'] (renderer.py:350), or null
     float* grad_grid;         // [rows][2]
+    float* grad_rep;          // [kRep][rep_floats]: the coarse levels' gradient, one copy per XCD
+    uint32_t rep_levels, rep_floats;
 };
 
 __device__ __forceinline__ float grid_u(const RtArgs& a, float x) {
@@ -219,6 +222,34 @@ __device__ __forceinline__ void scatter_level_c2(float* __restrict__ gtab, const
         }
         wave_lds_sync();
     }
+}
+
+// The coarse levels' rows are hot: every ray crosses them, so their adds
+// queue at the memory side on a few addresses (skipping the scatter of final
+// levels 0-1 saves 190 us of k_rt_final_bwd's 1.2 ms for 6 % of its atomic
+// requests; proposal level 0, 100 us per stage for 7 %;
+// tools/r2/gpu_r2s4b.sh).  Those levels scatter into kRep copies of their
+// rows instead, the copy picked by the block's XCD (blocks are dealt to the 8
+// XCDs round-robin), and k_rt_rep_sum adds the copies in a fixed order.
+#ifndef RT_KREP
+#define RT_KREP 8   // diagnostics may build other copy counts (a power of two)
+#endif
+constexpr uint32_t kRep = RT_KREP, kRepRows = 600000;
+
+__device__ __forceinline__ float* level_table(float* grad, float* rep, uint32_t rep_levels, uint32_t rep_floats,
+                                              int l) {
+    return (uint32_t)l < rep_levels ? rep + (blockIdx.x & (kRep - 1u)) * rep_floats : grad;
+}
+
+// grad[i] = sum_c rep[c][i] for i < n (the coarse rows get no other adds)
+__global__ void __launch_bounds__(256) k_rt_rep_sum(const float* __restrict__ rep, uint32_t n,
+                                                    float* __restrict__ grad) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    float acc = 0.0f;
+#pragma unroll
+    for (uint32_t c = 0; c < kRep; ++c) acc += rep[(size_t)c * n + i];
+    grad[i] = acc;
 }
 
 // ------------------------------------------------------------- forward --
@@ -541,7 +572,11 @@ __global__ void __launch_bounds__(256) k_rt_final_bwd(RtArgs a) {
             df0 = __builtin_fmaf(sw[q * 32 + 2 * l], g1[q], df0);
             df1 = __builtin_fmaf(sw[q * 32 + 2 * l + 1], g1[q], df1);
         }
-        scatter_level_c2(a.grad_grid, a.grid.lv[l], ux, uy, uz, df0, df1, live, stage);
+#ifdef RT_DIAG_LMASK   // diagnostics only (tools/diag): scatter a subset of the levels
+        if (!((RT_DIAG_LMASK >> l) & 1)) continue;
+#endif
+        scatter_level_c2(level_table(a.grad_grid, a.grad_rep, a.rep_levels, a.rep_floats, l), a.grid.lv[l], ux,
+                         uy, uz, df0, df1, live, stage);
     }
 }
 
@@ -682,6 +717,8 @@ struct PropBwdArgs {
     // per sample s = T r + k: [channel][T N]
     float* slab;              // [blocks][176] per-block prop_mlp gradient sums
     float* grad_grid;         // [rows][2]
+    float* grad_rep;          // as RtArgs
+    uint32_t rep_levels, rep_floats;
 };
 
 template <int T, bool FIRST>
@@ -892,7 +929,11 @@ __global__ void __launch_bounds__(256) k_rt_prop_bwd(PropBwdArgs a) {
     }
 #pragma unroll
     for (int l = 0; l < 5; ++l)
-        scatter_level_c2(a.grad_grid, a.grid.lv[l], ux, uy, uz, df[2 * l], df[2 * l + 1], live, stage);
+#ifdef RT_DIAG_PMASK   // diagnostics only (tools/diag)
+        if ((RT_DIAG_PMASK >> l) & 1)
+#endif
+        scatter_level_c2(level_table(a.grad_grid, a.grad_rep, a.rep_levels, a.rep_floats, l), a.grid.lv[l], ux,
+                         uy, uz, df[2 * l], df[2 * l + 1], live, stage);
     // the prop_mlp weight gradients dP0 = sum dh f^T, dP1 = sum dx h^T: wave
     // sums (fixed order), the block's four waves added in order into its slab
     // row (k_rt_outer_sum adds the rows) -- no [16 + 10 + 16 + 1][T N] round trip
@@ -919,22 +960,42 @@ __global__ void __launch_bounds__(256) k_rt_prop_bwd(PropBwdArgs a) {
 // 0..3 = mse (sum of 3 channels), proposal, distortion, entropy.  loss5 (or
 // null) = the four means and the total of utils.py:917-931; loss2 (or null) =
 // (proposal, distortion), the render's own loss outputs.  nt = rows to reduce.
-__global__ void __launch_bounds__(256) k_rt_loss(const float* terms, uint32_t N, int t0, int nt, float lp,
-                                                 float ld, float le, int with_prop, float* loss5, float* loss2) {
-    __shared__ double red[256];
+__global__ void __launch_bounds__(1024) k_rt_loss(const float* terms, uint32_t N, int t0, int nt, float lp,
+                                                  float ld, float le, int with_prop, float* loss5, float* loss2) {
+    // one block of 1024: every row's strided partial sums in independent
+    // chains, then one tree over the rows together (a single block is all
+    // there is, so the loads must not wait on each other)
+    __shared__ double red[4][1024];
     __shared__ float mean[4];
-    for (int t = t0; t < t0 + nt; ++t) {
-        double acc = 0.0;
-        for (uint32_t r = threadIdx.x; r < N; r += 256u) acc += (double)terms[(size_t)t * N + r];
-        red[threadIdx.x] = acc;
-        __syncthreads();
-        for (int w = 128; w > 0; w >>= 1) {
-            if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-            __syncthreads();
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    uint32_t r = threadIdx.x;
+    for (; r + 3072u < N; r += 4096u) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (t >= nt) break;
+            const float* row = terms + (size_t)(t0 + t) * N + r;
+            const float v0 = row[0], v1 = row[1024], v2 = row[2048], v3 = row[3072];
+            acc[t] += ((double)v0 + (double)v1) + ((double)v2 + (double)v3);
         }
-        if (threadIdx.x == 0) mean[t] = (float)(red[0] / (double)N / (t == 0 ? 3.0 : 1.0));
+    }
+    for (; r < N; r += 1024u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (t < nt) acc[t] += (double)terms[(size_t)(t0 + t) * N + r];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) red[t][threadIdx.x] = acc[t];
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) red[t][threadIdx.x] += red[t][threadIdx.x + w];
         __syncthreads();
     }
+    if ((int)threadIdx.x < nt) {
+        const int t = t0 + (int)threadIdx.x;
+        mean[t] = (float)(red[threadIdx.x][0] / (double)N / (t == 0 ? 3.0 : 1.0));
+    }
+    __syncthreads();
     if (threadIdx.x != 0) return;
     if (loss2) {
         loss2[0] = mean[1];
@@ -962,13 +1023,31 @@ struct RtWorkspace {
     float* fin[10];          // pos feat h1 h2 out delta tmid dout dh1 dh2
     float* ray[10];          // w fimg v1 v2 sig dz dv1 dv2 terms, step scratch (g_img 3 | g_ws | g_loss 2)
     float* slab;             // k_rt_outer partial sums
+    float* rep;              // kRep copies of the coarse levels' gradient rows
+    uint32_t rep_levels[3], rep_floats[3];   // final grid, proposal grids 0 and 1
     size_t bytes;
 };
 
 constexpr int kFinCh[10] = {3, 32, 64, 64, 16, 1, 1, 16, 64, 64};
 constexpr int kRayCh[10] = {32, 31, 32, 32, 3, 3, 32, 32, 4, 6};
 
-RtWorkspace carve_rt(uint32_t N, void* base) {
+// the leading levels whose rows fit kRepRows (SAMNERF_RT_REP_ROWS overrides it: A/B timing)
+uint32_t rep_rows_cap() {
+    static const uint32_t cap = [] {
+        const char* e = std::getenv("SAMNERF_RT_REP_ROWS");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : kRepRows;
+    }();
+    return cap;
+}
+
+void rep_span(const int32_t* offsets, int levels, uint32_t& n_levels, uint32_t& floats) {
+    n_levels = 0;
+    const uint32_t cap = rep_rows_cap();
+    while ((int)n_levels < levels && offsets && (uint32_t)offsets[n_levels + 1] <= cap) ++n_levels;
+    floats = n_levels ? (uint32_t)offsets[n_levels] * 2u : 0u;
+}
+
+RtWorkspace carve_rt(const samnerf_model* m, uint32_t N, void* base) {
     RtWorkspace w{};
     char* p = static_cast<char*>(base);
     size_t off = 0;
@@ -994,6 +1073,9 @@ RtWorkspace carve_rt(uint32_t N, void* base) {
     const size_t sf = (size_t)kT * n, sp = (size_t)128 * n;
     const size_t sb = std::max((size_t)div_up(sf, outer_chunk(sf)) * 4096, (size_t)div_up(sp, 256) * kPropW);
     w.slab = take(sb);
+    rep_span(m->grid.offsets_host, 16, w.rep_levels[0], w.rep_floats[0]);
+    for (int p = 0; p < 2; ++p) rep_span(m->prop[p].offsets_host, 5, w.rep_levels[1 + p], w.rep_floats[1 + p]);
+    w.rep = take((size_t)kRep * std::max(w.rep_floats[0], std::max(w.rep_floats[1], w.rep_floats[2])));
     w.bytes = off;
     return w;
 }
@@ -1134,10 +1216,23 @@ int rt_backward(const samnerf_model* m, uint32_t N, bool with_prop, const samner
         for (int p = 0; p < 2; ++p)
             ok = ok && zero(g->prop[p], (size_t)m->prop[p].offsets_host[5] * 2) == hipSuccess;
     if (!ok) return fail(SAMNERF_ELAUNCH, "rgb_train: gradient zero-fill failed");
+    // the coarse levels through kRep copies (k_rt_rep_sum writes their rows)
+    auto rep_scatter = [&](uint32_t levels, uint32_t floats, float*& rep, uint32_t& rl, uint32_t& rf) {
+        rep = w.rep;
+        rl = levels;
+        rf = floats;
+        return !floats || zero(w.rep, (size_t)kRep * floats) == hipSuccess;
+    };
+    auto rep_sum = [&](uint32_t floats, float* grad) {
+        if (floats) k_rt_rep_sum<<<div_up(floats, 256), 256, 0, s>>>(w.rep, floats, grad);
+    };
     RtArgs& a = c.a;
     a.grad_grid = g->grid;
+    if (!rep_scatter(w.rep_levels[0], w.rep_floats[0], a.grad_rep, a.rep_levels, a.rep_floats))
+        return fail(SAMNERF_ELAUNCH, "rgb_train: gradient zero-fill failed");
     k_rt_final_bwd_ray_h<<<div_up(N, 8), 256, 0, s>>>(a);
     k_rt_final_bwd<<<div_up((uint64_t)kT * N, 256), 256, 0, s>>>(a);
+    rep_sum(w.rep_floats[0], g->grid);
     const size_t S = (size_t)kT * N;
     outer(a.dh1, a.feat, 64, 32, S, g->grid_mlp[0], w.slab, s);
     outer(a.dh2, a.h1, 64, 64, S, g->grid_mlp[1], w.slab, s);
@@ -1151,10 +1246,13 @@ int rt_backward(const samnerf_model* m, uint32_t N, bool with_prop, const samner
         for (int st = 0; st < 2; ++st) {
             rt_prop_stage(m, c, w, st);
             pb.grad_grid = g->prop[st];
+            if (!rep_scatter(w.rep_levels[1 + st], w.rep_floats[1 + st], pb.grad_rep, pb.rep_levels, pb.rep_floats))
+                return fail(SAMNERF_ELAUNCH, "rgb_train: gradient zero-fill failed");
             const uint32_t T = st ? 64u : 128u;
             const uint32_t blocks = div_up((uint64_t)T * N, 256);
             if (st) k_rt_prop_bwd<64, false><<<blocks, 256, 0, s>>>(pb);
             else k_rt_prop_bwd<128, true><<<blocks, 256, 0, s>>>(pb);
+            rep_sum(w.rep_floats[1 + st], g->prop[st]);
             k_rt_outer_sum<<<div_up(160, 16), 256, 0, s>>>(w.slab, kPropW, 0u, 160u, blocks, g->prop_mlp[st][0]);
             k_rt_outer_sum<<<1, 256, 0, s>>>(w.slab, kPropW, 160u, 16u, blocks, g->prop_mlp[st][1]);
         }
@@ -1170,7 +1268,7 @@ extern "C" {
 
 size_t samnerf_rgb_train_workspace_size(const samnerf_model* model, uint32_t N) {
     if (!model) return 0;
-    return carve_rt(N, nullptr).bytes;
+    return carve_rt(model, N, nullptr).bytes;
 }
 
 int samnerf_rgb_train_forward(const samnerf_model* m, const float* rays_o, const float* rays_d, uint32_t N,
@@ -1185,7 +1283,7 @@ int samnerf_rgb_train_forward(const samnerf_model* m, const float* rays_o, const
         return fail(SAMNERF_EINVAL, "rgb_train_forward: cam_near_far must have 1 or N rows");
     if (!perturb_ok(m))
         return fail(SAMNERF_EINVAL, "rgb_train_forward: perturb needs all three position arrays or none");
-    RtWorkspace w = carve_rt(N, workspace);
+    RtWorkspace w = carve_rt(m, N, workspace);
     if (!workspace || workspace_bytes < w.bytes)
         return fail(SAMNERF_EWORKSPACE, "rgb_train_forward: workspace needs %zu bytes, got %zu", w.bytes,
                     workspace_bytes);
@@ -1196,7 +1294,7 @@ int samnerf_rgb_train_forward(const samnerf_model* m, const float* rays_o, const
     if ((rc = rt_forward(m, rays_o, rays_d, N, cam_near_far, n_cnf, with_proposal != 0, image, depth,
                          weights_sum, weights, c, w, s)))
         return rc;
-    k_rt_loss<<<1, 256, 0, s>>>(c.a.terms, N, 1, 2, 0.0f, 0.0f, 0.0f, 0, nullptr, losses);
+    k_rt_loss<<<1, 1024, 0, s>>>(c.a.terms, N, 1, 2, 0.0f, 0.0f, 0.0f, 0, nullptr, losses);
     return check_launch("rgb_train_forward");
 }
 
@@ -1210,7 +1308,7 @@ int samnerf_rgb_train_backward(const samnerf_model* m, const float* rays_o, cons
     if (!rays_o || !rays_d || !grad_image) return fail(SAMNERF_EINVAL, "rgb_train_backward: null pointer");
     if (with_proposal && !grad_losses)
         return fail(SAMNERF_EINVAL, "rgb_train_backward: the proposal backward needs grad_losses");
-    RtWorkspace w = carve_rt(N, workspace);
+    RtWorkspace w = carve_rt(m, N, workspace);
     if (!workspace || workspace_bytes < w.bytes)
         return fail(SAMNERF_EWORKSPACE, "rgb_train_backward: workspace needs %zu bytes, got %zu", w.bytes,
                     workspace_bytes);
@@ -1242,7 +1340,7 @@ int samnerf_rgb_train_step(const samnerf_model* m, const float* rays_o, const fl
         return fail(SAMNERF_EINVAL, "rgb_train_step: cam_near_far must have 1 or N rows");
     if (!perturb_ok(m))
         return fail(SAMNERF_EINVAL, "rgb_train_step: perturb needs all three position arrays or none");
-    RtWorkspace w = carve_rt(N, workspace);
+    RtWorkspace w = carve_rt(m, N, workspace);
     if (!workspace || workspace_bytes < w.bytes)
         return fail(SAMNERF_EWORKSPACE, "rgb_train_step: workspace needs %zu bytes, got %zu", w.bytes,
                     workspace_bytes);
@@ -1262,7 +1360,7 @@ int samnerf_rgb_train_step(const samnerf_model* m, const float* rays_o, const fl
     k_rt_rgb_loss_grad<<<div_up(N, 256), 256, 0, s>>>(c.a, gt_rgb, c_ent, g_img, g_ws);
     k_rt_set2<<<1, 1, 0, s>>>(g_loss, with_prop ? opts->lambda_proposal : 0.0f,
                               opts->lambda_distort > 0.0f ? opts->lambda_distort : 0.0f);
-    k_rt_loss<<<1, 256, 0, s>>>(c.a.terms, N, 0, 4, opts->lambda_proposal, opts->lambda_distort,
+    k_rt_loss<<<1, 1024, 0, s>>>(c.a.terms, N, 0, 4, opts->lambda_proposal, opts->lambda_distort,
                                 opts->lambda_entropy, with_prop ? 1 : 0, loss, nullptr);
     c.a.g_img = g_img;
     c.a.g_ws = g_ws;
