@@ -1510,6 +1510,9 @@ k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __rest
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t level = blockIdx.y;
     if (((t & ~(uint64_t)63) >> 3) >= N) return;          // whole wave past the end
+#ifdef SG_DIAG_MINLEVEL   // diagnostics only (tools/r2/gpu_r2s4h.sh): scatter levels >= this
+    if (level < SG_DIAG_MINLEVEL) return;
+#endif
     const bool live = r < N;                                // lanes stay for the reductions
     const uint32_t rr = live ? r : N - 1;
     const LevelDesc d = g.lv[level];

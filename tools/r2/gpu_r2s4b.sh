@@ -1,7 +1,8 @@
 #!/bin/bash
 # Which grid levels the RGB training scatters' atomic requests come from:
 # builds that skip some levels' scatter (tools/diag/build_variant.sh with
-# RT_DIAG_LMASK / RT_DIAG_PMASK), per build the kernel times and the atomic
+# RT_DIAG_LMASK / RT_DIAG_PMASK, built first with e.g. `bash tools/diag/build_variant.sh
+# lm0003 -DRT_DIAG_LMASK=0xFFFC`), per build the kernel times and the atomic
 # request count of one bench --mode rgbtrain run.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/r2s4b
