@@ -34,6 +34,8 @@
 //                       per wave: run merge, lane quads, zero-wave skip)
 //   k_rt_prop_bwd<T>    per proposal sample: prop_mlp backward, prop grid
 //                       scatter, prop_mlp weight gradients as wave sums
+//   k_rt_rep_sum        the coarse levels (hot rows) scatter into per-XCD
+//                       copies of their rows; this adds the copies in order
 //   k_rt_outer          grid_mlp / view_mlp weight gradients dW = sum_s dY[:, s]
 //                       X[:, s]^T (split-K, 4 x 4 register tiles, slab rows
 //                       summed in a fixed order by k_rt_outer_sum)
