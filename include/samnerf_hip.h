@@ -326,6 +326,9 @@ typedef struct {
     float* prop[2];               /* prop_encoders.{0,1}.embeddings */
     float* prop_mlp[2][2];        /* [16,10] [1,16] each */
 } samnerf_rgb_grads;
+/* Workspace for N rays of this model: the saved activations plus 8 per-XCD
+ * copies of the leading grid levels' gradient rows (those within 600 K rows), so
+ * it depends on the model's table offsets as well as on N. */
 size_t samnerf_rgb_train_workspace_size(const samnerf_model* model, uint32_t N);
 /* The same step as an autograd pair -- NeRFRenderer.run in train mode under
  * grad (renderer.py:221-362), differentiable outputs image, depth, weights_sum and
