@@ -259,7 +259,17 @@ __global__ void __launch_bounds__(256) k_rt_rep_sum(const float* __restrict__ re
 // One thread per final sample, ray-major (s = 32 r + k).
 // renderer.py:278-286 (bins -> position -> contract), network.py:221-229
 // (grid -> grid_mlp; trunc_exp is applied by the compositing kernel).
-__global__ void __launch_bounds__(256) k_rt_final_fwd(RtArgs a) {
+#ifndef RT_FWD_WAVES   // diagnostics: waves per SIMD asked of k_rt_final_fwd (0 = the compiler's choice)
+#define RT_FWD_WAVES 0
+#endif
+#ifndef RT_BWD_WAVES   // the same for k_rt_final_bwd
+#define RT_BWD_WAVES 0
+#endif
+__global__ void __launch_bounds__(256)
+#if RT_FWD_WAVES
+__attribute__((amdgpu_waves_per_eu(RT_FWD_WAVES, RT_FWD_WAVES)))
+#endif
+k_rt_final_fwd(RtArgs a) {
     __shared__ float sw[kGW];
     load_grid_mlp(a, sw);
     const uint32_t N = a.N;
@@ -534,7 +544,11 @@ __global__ void __launch_bounds__(256) k_rt_final_bwd_ray_h(RtArgs a) {
 
 // One thread per final sample: grid_mlp backward (ReLU masks from the saved
 // activations) and the grid scatter.
-__global__ void __launch_bounds__(256) k_rt_final_bwd(RtArgs a) {
+__global__ void __launch_bounds__(256)
+#if RT_BWD_WAVES
+__attribute__((amdgpu_waves_per_eu(RT_BWD_WAVES, RT_BWD_WAVES)))
+#endif
+k_rt_final_bwd(RtArgs a) {
     __shared__ float sw[kGW];
     __shared__ float sstage[4][384];
     float* stage = sstage[threadIdx.x >> 6];
