@@ -259,8 +259,11 @@ __global__ void __launch_bounds__(256) k_rt_rep_sum(const float* __restrict__ re
 // One thread per final sample, ray-major (s = 32 r + k).
 // renderer.py:278-286 (bins -> position -> contract), network.py:221-229
 // (grid -> grid_mlp; trunc_exp is applied by the compositing kernel).
-#ifndef RT_FWD_WAVES   // diagnostics: waves per SIMD asked of k_rt_final_fwd (0 = the compiler's choice)
-#define RT_FWD_WAVES 0
+// 3 waves per SIMD (168 VGPRs, no spills) instead of the compiler's 186 VGPRs
+// and 2: the gathers' latency hides better, 240 -> 216 us per 8K-ray step
+// (tools/r2/gpu_r2s4m.sh); 4 waves spill 150 VGPRs.  Builds may override it.
+#ifndef RT_FWD_WAVES
+#define RT_FWD_WAVES 3
 #endif
 #ifndef RT_BWD_WAVES   // the same for k_rt_final_bwd
 #define RT_BWD_WAVES 0

@@ -1,5 +1,5 @@
 #!/bin/bash
-# k_rt_final_fwd at 3 waves per SIMD (tools/diag/lib/fw3.so: -DRT_FWD_WAVES=3,
+# k_rt_final_fwd at 3 waves per SIMD (now the default; fw3.so was built with -DRT_FWD_WAVES=3,
 # 168 VGPRs, no spills) vs the compiler's 186 VGPRs (2 waves)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
