@@ -574,7 +574,11 @@ k_rt_final_bwd(RtArgs a) {
         if (live) a.dh2[i * S + s] = g2[i];
     }
     float g1[64];
+#ifdef RT_BWD_G1_UNROLL   // diagnostics: g1 in registers (fully unrolled) instead of scratch
+#pragma unroll
+#else
 #pragma unroll 4
+#endif
     for (int i = 0; i < 64; ++i) {
         float acc = 0.0f;
 #pragma unroll
