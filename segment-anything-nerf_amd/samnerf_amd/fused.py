@@ -448,7 +448,12 @@ class _FusedRGBTrain(torch.autograd.Function):
         renderer, m, rays_o, rays_d, bg, pert, with_prop, ws, need, _ = ctx.state
         dev = rays_o.device
         N = rays_o.shape[0]
+        # every converted gradient is bound to a local so that it stays alive
+        # until the C call returns (a temporary's block could otherwise be
+        # handed to the next conversion by the caching allocator)
         g_img = g_img.contiguous().float()
+        g_ws = g_wsum.contiguous().float()
+        g_dp = g_depth.contiguous().float()
         g_loss = torch.stack([g_prop.reshape(()), g_dist.reshape(())]).float().contiguous()
         grads = [torch.empty(sh, device=dev) for sh in ctx.shapes]
         g = SamnerfRgbGrads()
@@ -466,7 +471,7 @@ class _FusedRGBTrain(torch.autograd.Function):
                 m.perturb[i] = None if pert is None else _param(pert[i], f"perturb[{i}]")
             check(lib().samnerf_rgb_train_backward(
                 ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, float(bg), int(with_prop), _ptr(g_img),
-                _ptr(g_wsum.contiguous().float()), _ptr(g_depth.contiguous().float()), _ptr(g_loss),
+                _ptr(g_ws), _ptr(g_dp), _ptr(g_loss),
                 ctypes.byref(g), _ptr(ws), need, _stream(g_img)), "rgb_train_backward")
         finally:
             for i in range(3):

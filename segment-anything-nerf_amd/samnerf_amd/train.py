@@ -58,7 +58,9 @@ def rgb_train_step_fused(model, rays_o, rays_d, gt_rgb, global_step, bg_color=No
     the steps the reference does not update them, utils.py:912-913).  Returns
     (pred_rgb, loss, outputs) like rgb_train_step; loss is a detached 0-d
     tensor, outputs holds image / depth / weights_sum / num_points and the
-    unweighted loss terms."""
+    unweighted loss terms.  Gradients accumulate into an existing .grad as
+    loss.backward() does (proposal tensors: not touched on the steps they do
+    not train)."""
     import ctypes
 
     from ._lib import SamnerfRgbGrads, SamnerfRgbTrainOpts, check, lib
@@ -102,22 +104,26 @@ def rgb_train_step_fused(model, rays_o, rays_d, gt_rgb, global_step, bg_color=No
     with_prop = bool(update_proposal) and o.lambda_proposal > 0
     every = rgb_train_params(model, True)
     main, prop = every[:7], every[7:]
-    for p in main + (prop if with_prop else []):
-        if p.grad is None or p.grad.shape != p.shape or not p.grad.is_contiguous():
-            p.grad = torch.empty_like(p)
-    if not with_prop:
-        for p in prop:
-            p.grad = None
+    trained = main + (prop if with_prop else [])
+    # the kernels OVERWRITE their gradient buffers: they write into fresh
+    # buffers, which become .grad where it is None and are added into an
+    # existing .grad otherwise (loss.backward()'s accumulation)
+    for p in trained:
+        if p.grad is not None and (p.grad.dtype != torch.float32 or p.grad.device != p.device
+                                   or p.grad.shape != p.shape):
+            raise RuntimeError("rgb_train_step_fused: existing .grad must be float32, on the "
+                               "parameter's device and of its shape")
+    scratch = [torch.empty_like(p, memory_format=torch.contiguous_format) for p in trained]
     g = SamnerfRgbGrads()
-    g.grid = main[0].grad.data_ptr()
+    g.grid = scratch[0].data_ptr()
     for i in range(3):
-        g.grid_mlp[i] = main[1 + i].grad.data_ptr()
-        g.view_mlp[i] = main[4 + i].grad.data_ptr()
+        g.grid_mlp[i] = scratch[1 + i].data_ptr()
+        g.view_mlp[i] = scratch[4 + i].data_ptr()
     if with_prop:
-        g.prop[0], g.prop[1] = prop[0].grad.data_ptr(), prop[1].grad.data_ptr()
+        g.prop[0], g.prop[1] = scratch[7].data_ptr(), scratch[8].data_ptr()
         for q in range(2):
             for i in range(2):
-                g.prop_mlp[q][i] = prop[2 + 2 * q + i].grad.data_ptr()
+                g.prop_mlp[q][i] = scratch[9 + 2 * q + i].data_ptr()
     need = lib().samnerf_rgb_train_workspace_size(ctypes.byref(m), N)
     ws = getattr(fr, "_rt_ws", None)
     if ws is None or ws.device != dev or ws.numel() < need:
@@ -138,6 +144,11 @@ def rgb_train_step_fused(model, rays_o, rays_d, gt_rgb, global_step, bg_color=No
     finally:
         for i in range(3):
             m.perturb[i] = None
+    for p, t in zip(trained, scratch):
+        if p.grad is None:
+            p.grad = t
+        else:
+            p.grad.add_(t)
     outputs = {"image": image, "depth": depth, "weights_sum": wsum, "num_points": N * int(m.num_steps[2]),
                "mse": loss[0], "proposal_loss": loss[1], "distort_loss": loss[2], "entropy": loss[3]}
     if opt.adaptive_num_rays:

@@ -151,6 +151,7 @@ def test_fused_rgb_training_reduces_loss(hip_lib, cuda):
     gt = torch.full((256, 3), 0.25, device=cuda)
     losses = []
     for step in range(1, 9):
+        opt.zero_grad(set_to_none=True)
         _, loss, _ = rgb_train_step_fused(net, ro, rd, gt, global_step=step)
         opt.step()
         losses.append(float(loss))
@@ -189,6 +190,7 @@ def test_fused_rgb_step_deterministic_weight_gradients(hip_lib, cuda):
     gt = torch.rand(1024, 3, generator=torch.Generator().manual_seed(6)).to(cuda)
     res = []
     for _ in range(2):
+        net.zero_grad(set_to_none=True)
         rgb_train_step_fused(net, ro, rd, gt, global_step=1, perturb=False)
         res.append({k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None})
     for k in res[0]:
@@ -228,3 +230,40 @@ def test_train_mode_render_runs_the_training_kernels(hip_lib, cuda):
         err = float((pa.grad - pc.grad).norm() / pa.grad.norm().clamp_min(1e-30))
         assert err < 1e-5, (k, err)
     _compare_grads(c, b)
+
+
+def test_fused_rgb_step_accumulates_into_existing_grad(hip_lib, cuda):
+    """Like loss.backward(), a second fused step adds into .grad: two steps
+    on the same batch leave twice the gradient of one."""
+    from samnerf_amd.train import rgb_train_step_fused
+    (net,) = _rgb_nets(cuda, seed=29, devices=("cuda",))
+    ro, rd = _rays(16, 3, cuda)
+    gt = torch.rand(256, 3, generator=torch.Generator().manual_seed(4)).to(cuda)
+    rgb_train_step_fused(net, ro, rd, gt, global_step=1, perturb=False)
+    one = {k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None}
+    rgb_train_step_fused(net, ro, rd, gt, global_step=1, perturb=False)
+    for k, p in net.named_parameters():
+        if k in one:
+            err = ((p.grad - 2 * one[k]).norm() / one[k].norm().clamp_min(1e-30)).item()
+            assert err < 1e-5, (k, err)
+
+
+def test_autograd_rgb_step_with_depth_and_weights_sum_loss(hip_lib, cuda):
+    """A loss on depth.mean() + weights_sum.mean() (their gradients arrive as
+    expanded, non-contiguous tensors) through the autograd Function equals the
+    torch path's gradients (the converted gradients must stay alive
+    through the C call)."""
+    a, b = _rgb_nets(cuda, seed=31, devices=("cuda", "cuda"))
+    a.fused = True
+    ro, rd = _rays(16, 4, cuda)
+    outs = []
+    for n in (a, b):
+        torch.manual_seed(7)
+        o = n.render(ro, rd, staged=False, bg_color=1, perturb=False, update_proposal=True,
+                     return_feats=0)
+        loss = (o["image"].mean() + 0.3 * o["depth"].mean() + 2.0 * o["weights_sum"].mean()
+                + o["proposal_loss"])
+        loss.backward()
+        outs.append(float(loss))
+    assert abs(outs[0] - outs[1]) <= 1e-5 * abs(outs[1])
+    _compare_grads(a, b)
