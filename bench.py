@@ -73,17 +73,18 @@ GATHER_ADDR_PER_RAY = {"prop0": 128 * 28, "prop1": 64 * 32, "final": 32 * 112}
 # SAM head (network.py:36-75): 163->256, 256->256, 419->256, 256->256, 256->256
 HEAD_FLOP_PER_RAY = 2 * 256 * (163 + 256 + 419 + 256 + 256)  # 691,200
 # MFMA issue of the head per 32 rays (one wave): 86 k-blocks of 16 (K padded
-# 176 + 256 + 432 + 256 + 256) x 8 output tiles x 3 bf16 products
-# (v_mfma_f32_32x32x16_bf16, 32 cycles); exact mode: 688 k-steps of 2 x 8
-# tiles on v_mfma_f32_32x32x2_f32 (64 cycles).
+# 176 + 256 + 432 + 256 + 256) x 8 output tiles x 3 fp16 products of the f16x3
+# form (v_mfma_f32_32x32x16_f16, 32 cycles, the bf16 rate); exact mode: 688
+# k-steps of 2 x 8 tiles on v_mfma_f32_32x32x2_f32 (64 cycles).
 HEAD_MFMA_CYCLES_PER_32 = {0: 86 * 8 * 3 * 32, 1: 688 * 8 * 64}
-BF16_MFMA_PEAK_TFS = 2500.0    # MI355X_MICROARCH.md: dense BF16 ~2.5 PF
+BF16_MFMA_PEAK_TFS = 2500.0    # MI355X_MICROARCH.md: dense BF16/F16 ~2.5 PF
 F32_MFMA_PEAK_TFS = 157.3      # MI355X_MICROARCH.md: F32 matrix = vector peak
-DTYPE = {0: "fp32 in the reference's op order for everything that decides a discrete result "
-            "(near/far, bins, proposal grids + MLPs, compositing, sample_pdf); grid_mlp "
-            "(32->64->64->16 per sample), the SAM head (163->256x5) and the mask head (143->256->256->K "
-            "per sample) on bf16x3 split-precision MFMA with fp32 accumulate (~1e-5 relative); "
-            "view_mlp on fp32 MFMA",
+DTYPE = {0: "fp32-equivalent: fp32 in the reference's op order for everything that decides a "
+            "discrete result (near/far, bins, proposal grids + MLPs, compositing, sample_pdf); "
+            "grid_mlp (32->64->64->16 per sample), the SAM head (163->256x5) and the mask head "
+            "(143->256->256->K per sample) as f16x3: each fp32 product as three fp16 MFMA products on "
+            "power-of-two scaled operands, fp32 accumulate -- error vs float64 at the level of exact "
+            "fp32 GEMMs (csrc/f16x3.h, tests/test_gpu_render.py); view_mlp on fp32 MFMA",
          1: "fp32 throughout: grid_mlp, view_mlp, the SAM head and the mask head on fp32 MFMA "
             "(v_mfma_f32_32x32x2_f32), the rest in the reference's op order"}
 
@@ -103,7 +104,8 @@ def parse():
                     help="rays of the view rendered by run_torch, the reference's unfused op "
                          "sequence on the same GPU (0 = skip)")
     ap.add_argument("--head-mode", type=int, default=0,
-                    help="0 = bf16x3 split-precision grid_mlp + SAM head (default), 1 = exact fp32 MFMA")
+                    help="0 = f16x3 (fp32-equivalent) grid_mlp + SAM / mask heads (default), "
+                         "1 = exact fp32 MFMA")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the side measurements after the headline (exact-fp32 precision at "
                          "N=1, q16 transport at N>1)")
@@ -429,7 +431,7 @@ def rgb_train_main(args, dev):
 
 TRAIN_WHAT = {
     "optimizer": "FusedAdam: one-pass HIP Adam (train_optim.hip), torch.optim.Adam semantics",
-    "dtype": "fp32 (fused render forward: grid_mlp bf16x3 MFMA; SAM head forward + backward on exact "
+    "dtype": "fp32 (fused render forward: grid_mlp f16x3 MFMA (fp32-equivalent); SAM head forward + backward on exact "
              "fp32 MFMA, sam_head_train.hip; s_grid scatter fp32 atomics)",
     "data": "synthetic (default-init weights, N(0,1) target)",
     "config": {"workload": "cfg5: 64x64 rays, with_sam, RGB frozen", "optimizer": "Adam lr 1e-2 eps 1e-15"},
@@ -445,7 +447,7 @@ def train_main(args, dev):
     if args.torch_adam:
         rec["optimizer"] = "torch.optim.Adam (foreach)"
     if os.environ.get("SAMNERF_TRAIN_HEAD", "hip") == "torch":
-        rec["dtype"] = "fp32 (fused render forward: grid_mlp bf16x3 MFMA; SAM head torch autograd)"
+        rec["dtype"] = "fp32 (fused render forward: grid_mlp f16x3 MFMA; SAM head torch autograd)"
     print(json.dumps(rec), flush=True)
 
 
@@ -484,7 +486,7 @@ def gui_main(args, dev):
         "metric": "GUI frame: 512x512 RGB + 64x64 SAM-feature render (frames/s)", "value": 1.0 / dt,
         "unit": "frames/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt * 1e3, "higher_is_better": True, "rays_per_s": rays / dt,
-        "dtype": "fp32 (SAM head: bf16x3 split-precision MFMA, fp32 accumulate)",
+        "dtype": "fp32-equivalent (SAM head: f16x3 MFMA, fp32 accumulate)",
         "data": "synthetic (random-init weights of the reference architecture, GUI camera)",
         "config": {"workload": f"{H}x{W} RGB (features skipped) + 64x64 with 256-d SAM features",
                    "reference": "readme.md:5: 5 FPS on V100 incl. the SAM decoder"},
@@ -628,8 +630,8 @@ def rooflines(stage_avg, band_rays, head_mode, band_traffic):
             "bound": "mfma", "unit": "TFLOP/s", "frac": frac,
             "achieved_fp32_equiv": HEAD_FLOP_PER_RAY * band_rays / (ms * 1e-3) / 1e12,
             "peak": F32_MFMA_PEAK_TFS if head_mode == 1 else BF16_MFMA_PEAK_TFS,
-            "basis": "MFMA issue cycles of the head's structure (bf16x3: 86 k-blocks x 8 tiles x 3 "
-                     "v_mfma_f32_32x32x16_bf16 per 32 rays) / (1024 SIMDs x 2.4 GHz x time)"}
+            "basis": "MFMA issue cycles of the head's structure (f16x3: 86 k-blocks x 8 tiles x 3 "
+                     "v_mfma_f32_32x32x16_f16 per 32 rays) / (1024 SIMDs x 2.4 GHz x time)"}
     if stage_avg.get("s_grid", 0) > 0:
         ms = stage_avg["s_grid"]
         alg = ALG_BYTES_PER_RAY["s_grid"] * band_rays
@@ -722,7 +724,7 @@ def main():
         other = 1 - args.head_mode
         r3 = ViewRunner(args, FusedRenderer(net, head_mode=other), 1, dev, H, W, pose, intr, r0, r1, codec)
         dt3, last3, st3, _ = r3.run(max(3, args.steps // 2), 2)
-        side["precision_" + ("exact_fp32" if other == 1 else "bf16x3")] = {
+        side["precision_" + ("exact_fp32" if other == 1 else "f16x3")] = {
             "value": n_total * max(3, args.steps // 2) / dt3, "unit": "rays/s",
             "ms_per_step": dt3 * 1e3 / max(3, args.steps // 2), "stage_ms": st3, "dtype": DTYPE[other],
             "max_abs_samvit_vs_headline": float((last3["samvit"] - last["samvit"]).abs().max())

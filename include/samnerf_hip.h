@@ -170,10 +170,11 @@ typedef struct {
     float grid_bound;             /* 2 under contract (renderer.py:152-153) */
     float min_near;               /* main.py:69 */
     uint32_t num_steps[3];        /* (128, 64, 32), main.py:79-80 */
-    int head_mode;                /* precision of the GEMMs -- grid_mlp (per sample) and the
-                                     SAM head: 0 = bf16x3 split precision on bf16 MFMA with
-                                     fp32 accumulate (~1e-5 relative, default); 1 = exact
-                                     fp32 MFMA (v_mfma_f32_32x32x2_f32) for both */
+    int head_mode;                /* precision of the GEMMs -- grid_mlp (per sample), the SAM
+                                     head and the mask head: 0 = f16x3, each fp32 product as
+                                     three fp16 MFMA products on power-of-two scaled operands
+                                     with fp32 accumulate (fp32-equivalent, default); 1 = exact
+                                     fp32 MFMA (v_mfma_f32_32x32x2_f32) */
     float t_thresh;               /* N1, a flagged NON-PARITY mode: 0 = off (the
                                      reference's semantics, default); t in (0, 1): a wave of 32
                                      rays stops marching the final stage once every ray's
@@ -235,6 +236,18 @@ int samnerf_render_forward(const samnerf_model* model, const float* rays_o,
                            uint32_t n_cnf, float bg_color, float* image, float* depth,
                            float* weights_sum, float* samvit, float* feature_rows,
                            void* workspace, size_t workspace_bytes, samnerf_stream_t stream);
+
+/* The SAM head alone (samvit_mlp = SkipConnMLP(163, 256 x 5) + LayerNorm(256),
+ * nerf/network.py:36-75, :120-123) on given head-input rows [N,164] (the
+ * feature_rows layout of samnerf_render_forward: cat(f_sam, f_image, image,
+ * depth) + 1 pad column) -> samvit [N,256], at model->head_mode's precision
+ * (0 = f16x3, the default; 1 = exact fp32 MFMA).  The render runs the same
+ * kernels on its own rows; this entry point serves callers that hold rows
+ * (the reference's samvit_mlp call on a feature batch, renderer.py:384-388). */
+size_t samnerf_sam_head_workspace_size(void);
+int samnerf_sam_head_forward(const samnerf_model* model, const float* rows, uint32_t N,
+                             float* samvit, void* workspace, size_t workspace_bytes,
+                             samnerf_stream_t stream);
 
 /* instance_mask_logits [N, mask_out] (renderer.py:392-395, :451-452):
  * sum_k w_k * mask_mlp(cat(m_grid(x_k), geo_feat_k)) over the final samples, the

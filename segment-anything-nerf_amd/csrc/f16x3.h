@@ -1,0 +1,97 @@
+// f16x3.h -- fp32-equivalent GEMM operands on the fp16 matrix cores.
+//
+// The MLPs of the path (grid_mlp, the SAM head, the mask head) are fp32 in
+// the reference (nerf/network.py:9-75).  gfx950 runs fp32-input MFMA at 1/16
+// of the fp16 rate, so these GEMMs run as three fp16 products per fp32
+// product ("f16x3"): each operand x is split x = hi + lo with
+//   hi = f16_rne(x),  lo = f16_rne(x - hi)       (x - hi is exact in fp32)
+// and A.B = A_lo.B_hi + A_hi.B_lo + A_hi.B_hi on v_mfma_f32_32x32x16_f16
+// (fp32 accumulate; the dropped A_lo.B_lo is 2^-22 of the product).  hi + lo
+// carries 22 significant bits, so each product is within ~2^-21 of the exact
+// one -- below the fp32 rounding of the accumulation it feeds over K = 16..419
+// terms (tools/f16x3_error.py: the same max error against float64 as an exact
+// fp32 MFMA GEMM, 36x below the bf16 split it replaces).
+//
+// fp16's narrow exponent range (normal from 2^-14, max 65504) is handled by
+// exact power-of-two scaling: every weight ROW is scaled so its largest
+// |w| lies in [2^14, 2^15) (packing time, inverse kept per row), and every
+// activation COLUMN (one ray or sample) the same way at run time, from the max
+// over the column's K inputs.  Scaling by 2^e commutes with rounding, so the
+// scaled product is the unscaled one times 2^(e_row + e_col) exactly; the
+// consumer multiplies the accumulator by the two inverse scales.  With the
+// column maximum at 2^14, elements down to 2^-28 of it stay normal fp16 and the
+// absolute error floor is 2^-39 of the maximum.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace samnerf {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// Power-of-two scale s and its inverse for a column (or row) whose largest
+// magnitude is `maxabs` (>= 0): maxabs * s in [2^14, 2^15).  The exponent is
+// clamped so that both s and 1/s are normal floats (all-zero or tiny columns
+// get s = 2^126; inf / NaN columns s = 2^-114 and stay inf / NaN).
+struct Scale2 {
+    float s, inv;
+};
+__host__ __device__ __forceinline__ Scale2 scale_of_max(float maxabs) {
+    uint32_t e = __builtin_bit_cast(uint32_t, maxabs) >> 23;          // biased exponent (sign bit clear)
+    e = e < 15u ? 15u : (e > 255u ? 255u : e);
+    Scale2 r;
+    r.s = __builtin_bit_cast(float, (268u - e) << 23);             // 2^(141 - e)
+    r.inv = __builtin_bit_cast(float, (e - 14u) << 23);             // 2^(e - 141)
+    return r;
+}
+
+// The same as an exponent k (s = 2^k, k in [-114, 126]) and 2^k as a float
+// for any k (clamped to the normal range): scales tracked across layers.
+__device__ __forceinline__ int scale_exp_of_max(float maxabs) {
+    uint32_t e = __builtin_bit_cast(uint32_t, maxabs) >> 23;
+    e = e < 15u ? 15u : (e > 255u ? 255u : e);
+    return 141 - (int)e;
+}
+__device__ __forceinline__ float exp2i(int k) {
+    k = k < -126 ? -126 : (k > 127 ? 127 : k);
+    return __builtin_bit_cast(float, (uint32_t)(k + 127) << 23);
+}
+
+// hi / lo halves of two (already scaled) values, packed as two f16 each
+__device__ __forceinline__ void split_pair_f16(float x, float y, uint32_t& hi, uint32_t& lo) {
+    const f16x2v h = __builtin_convertvector((f32x2v){x, y}, f16x2v);
+    const f32x2v hf = __builtin_convertvector(h, f32x2v);
+    const f16x2v l = __builtin_convertvector((f32x2v){x - hf.x, y - hf.y}, f16x2v);
+    hi = __builtin_bit_cast(uint32_t, h);
+    lo = __builtin_bit_cast(uint32_t, l);
+}
+
+// 8 values (times the scale s) -> one B (or A) fragment pair
+__device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
+    split_pair_f16(v[0] * s, v[1] * s, hi.x, lo.x);
+    split_pair_f16(v[2] * s, v[3] * s, hi.y, lo.y);
+    split_pair_f16(v[4] * s, v[5] * s, hi.z, lo.z);
+    split_pair_f16(v[6] * s, v[7] * s, hi.w, lo.w);
+}
+
+// C += A.B in f16x3 (small terms first)
+__device__ __forceinline__ floatx16 mfma_f16x3(uint4 ah, uint4 al, uint4 bh, uint4 bl, floatx16 c) {
+    const f16x8 Ah = __builtin_bit_cast(f16x8, ah), Al = __builtin_bit_cast(f16x8, al);
+    const f16x8 Bh = __builtin_bit_cast(f16x8, bh), Bl = __builtin_bit_cast(f16x8, bl);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(Al, Bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ah, Bl, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(Ah, Bh, c, 0, 0, 0);
+}
+
+// max |x| of a wave-wide reduction over the 64 lanes (for weight rows)
+__device__ __forceinline__ float wave_max64(float m) {
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) m = fmaxf(m, __shfl_xor(m, k));
+    return m;
+}
+
+}  // namespace samnerf

@@ -17,35 +17,28 @@
 // B operands of layer 0 (lane half h of k-block kb < 8 = level 2 kb + h, its 8
 // channels = one 32-B corner row per corner: lookup_level3<8>), k-block 8 =
 // geo_feat (k_final stores it per sample when the model has a mask head).
-// Orientation and weight stream are k_sam_head_bf3's (sam_head.hip):
-// out^T[256 units x 32 rays] = W . act^T, 8 accumulator tiles per wave whose
-// registers are the next layer's B operands, weights in 16 KiB steps through
-// a 4-deep LDS ring by direct DMA, shared by the 4 waves.  27 steps per sample:
+// Orientation is k_sam_head_h16's (sam_head.hip): out^T[256 units x 32 rays] =
+// W . act^T, 8 accumulator tiles per wave whose registers are the next layer's
+// B operands, weights in 16 KiB steps through LDS shared by the 4 waves.  27
+// steps per sample:
 // layer 0 (9 k-blocks x 8 tiles), layer 1 (16 x 8), layer 2 (16 k-blocks x
 // the one output tile, 8 per step).  The weighted sum over samples stays in
 // the output tile's registers.
 //
-// Weight stream (round 2): first through LDS-DMA like the SAM head (3-, then
-// 4-deep ring), measured DMA-throughput-bound; now staged through VGPRs by
-// ordinary loads (MaskStager, 392 VGPRs, no spills): 512^2 mask view 10.1 ->
-// 8.75 ms.
-//
-// Precision (head_mode): 0 = bf16x3 split precision (3 bf16 MFMAs per 16-deep
-// k-block, ~1e-5 relative); 1 = exact fp32 (8 v_mfma_f32_32x32x2_f32 per
-// k-block, the step holds the fp32 weights in the same 32 B per lane and
-// tile).
+// Precision (head_mode): 0 = f16x3 (f16x3.h: 3 fp16 MFMAs per 16-deep k-block
+// on power-of-two scaled operands, fp32-equivalent: per-tensor weight scales,
+// per-sample-column activation scales); 1 = exact fp32 (8
+// v_mfma_f32_32x32x2_f32 per k-block, the step holds the fp32 weights in the
+// same 32 B per lane and tile).
 #include <algorithm>
 
+#include "f16x3.h"
 #include "samnerf_common.h"
 
 using namespace samnerf;
 
 namespace {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-typedef float float2v __attribute__((ext_vector_type(2)));
 
 constexpr int kMIn = 143;                     // 128 m_grid features + 15 geo
 constexpr int kL0kb = 9;                      // 8 level pairs + geo (15 + 1 pad)
@@ -54,46 +47,20 @@ constexpr int kStepsPerSample = kL0kb + kHkb + 2;   // 27
 constexpr int kStepVec = 2 * 8 * 64;          // uint4 per step
 constexpr int kSlots = 128;                   // ray slots per workgroup
 constexpr int kT = 32;                        // final samples per ray
-// weight ring depth (LDS steps); the DMA runs kRing - 1 steps ahead.  4
-// (137 KB of LDS with the operand stage): 8.92 -> 8.35 ms per 512^2 view
-// against 3; the stream alone (no gathers, no MFMAs) is the same at both
-// depths, 9.2 ms -- a DMA throughput limit (~1.15 us per 16 KiB step per CU),
-// not its latency
-#ifndef SAMNERF_MASK_RING
-#define SAMNERF_MASK_RING 4
-#endif
-constexpr uint32_t kRing = SAMNERF_MASK_RING;
-#define MASK_STR2(x) #x
-#define MASK_STR(x) MASK_STR2(x)
-#define MASK_VMCNT_AHEAD "s_waitcnt vmcnt(" MASK_STR(SAMNERF_MASK_VMCNT) ")"
-#ifndef SAMNERF_MASK_VMCNT
-#define SAMNERF_MASK_VMCNT 8                          // 4 DMA instructions per step x (kRing - 2)
-#endif
-static_assert(SAMNERF_MASK_VMCNT == 4 * (SAMNERF_MASK_RING - 2), "vmcnt of the ring depth");
-
 __device__ __forceinline__ int rho(int q) { return (q & 3) + 8 * (q >> 2); }
 __device__ __forceinline__ int hidden_unit(int kb, int h, int m) {
     return 32 * (kb >> 1) + rho(8 * (kb & 1) + m) + 4 * h;
 }
 
-__device__ __forceinline__ void split_pair(float x, float y, uint32_t& hi, uint32_t& lo) {
-    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v){x, y}, bf16x2v));
-    const float hx = __uint_as_float(hi << 16), hy = __uint_as_float(hi & 0xffff0000u);
-    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v){x - hx, y - hy}, bf16x2v));
-}
-
-// 8 values of one lane's k-block as the B operand pair: bf16x3 hi / lo, or
-// (EXACT) the fp32 values themselves, 4 in each uint4
+// 8 values of one lane's k-block as the B operand pair: f16x3 hi / lo of the
+// values times s, or (EXACT) the fp32 values themselves, 4 in each uint4
 template <bool EXACT>
-__device__ __forceinline__ void to_operand(const float* v, uint4& a, uint4& b) {
+__device__ __forceinline__ void to_operand(const float* v, float s, uint4& a, uint4& b) {
     if constexpr (EXACT) {
         a = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
         b = make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7]));
     } else {
-        split_pair(v[0], v[1], a.x, b.x);
-        split_pair(v[2], v[3], a.y, b.y);
-        split_pair(v[4], v[5], a.z, b.z);
-        split_pair(v[6], v[7], a.w, b.w);
+        split8_f16(v, s, a, b);
     }
 }
 
@@ -112,11 +79,7 @@ __device__ __forceinline__ floatx16 kblock(uint4 a0, uint4 a1, uint4 b0, uint4 b
                                                     s < 4 ? u4f(b0, s) : u4f(b1, s - 4), c, 0, 0, 0);
         return c;
     } else {
-        const bf16x8 Ah = __builtin_bit_cast(bf16x8, a0), Al = __builtin_bit_cast(bf16x8, a1);
-        const bf16x8 Bh = __builtin_bit_cast(bf16x8, b0), Bl = __builtin_bit_cast(bf16x8, b1);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Al, Bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Ah, Bl, c, 0, 0, 0);
-        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(Ah, Bh, c, 0, 0, 0);
+        return mfma_f16x3(a0, a1, b0, b1, c);
     }
 }
 
@@ -126,34 +89,79 @@ __device__ __forceinline__ floatx16 kblock(uint4 a0, uint4 a1, uint4 b0, uint4 b
 // of k-block kb: W[32 t + i][input (kb, h, m)], input = 16 kb + 8 h + m for
 // layer 0 (m_grid level 2 kb + h channel m; kb 8: geo 8 h + m at column 128 +
 // 8 h + m, column 143 = padding), hidden_unit(kb, h, m) for layers 1-2.
-template <bool EXACT>
+__device__ __forceinline__ float mask_weight(const float* __restrict__ w0, const float* __restrict__ w1,
+                                             const float* __restrict__ w2, uint32_t K, int step, int slot,
+                                             int lane, int m) {
+    const int i = lane & 31, h = lane >> 5;
+    if (step < kL0kb) {                                   // layer 0: tile = slot
+        const int col = 16 * step + 8 * h + m;
+        return col < kMIn ? w0[(32 * slot + i) * kMIn + col] : 0.0f;
+    }
+    if (step < kL0kb + kHkb) {                            // layer 1
+        const int kb = step - kL0kb;
+        return w1[(32 * slot + i) * 256 + hidden_unit(kb, h, m)];
+    }
+    const int kb = 8 * (step - kL0kb - kHkb) + slot;      // layer 2: one tile
+    return (uint32_t)i < K ? w2[i * 256 + hidden_unit(kb, h, m)] : 0.0f;
+}
+
+__device__ __forceinline__ int step_layer(int step) { return step < kL0kb ? 0 : step < kL0kb + kHkb ? 1 : 2; }
+
+// exact fp32 weights (head_mode 1), one thread per (step, slot, lane)
 __global__ void __launch_bounds__(256)
-k_mask_pack(const float* __restrict__ w0, const float* __restrict__ w1, const float* __restrict__ w2,
-            uint32_t K, uint4* __restrict__ packed) {
+k_mask_pack_f32(const float* __restrict__ w0, const float* __restrict__ w1, const float* __restrict__ w2,
+                uint32_t K, uint4* __restrict__ packed) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (uint32_t)kStepsPerSample * 8u * 64u) return;
     const int lane = (int)(t & 63u), slot = (int)((t >> 6) & 7u), step = (int)(t >> 9);
-    const int i = lane & 31, h = lane >> 5;
     float v[8];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        float w;
-        if (step < kL0kb) {                               // layer 0: tile = slot
-            const int col = 16 * step + 8 * h + m;
-            w = col < kMIn ? w0[(32 * slot + i) * kMIn + col] : 0.0f;
-        } else if (step < kL0kb + kHkb) {                 // layer 1
-            const int kb = step - kL0kb;
-            w = w1[(32 * slot + i) * 256 + hidden_unit(kb, h, m)];
-        } else {                                          // layer 2: one tile
-            const int kb = 8 * (step - kL0kb - kHkb) + slot;
-            w = (uint32_t)i < K ? w2[i * 256 + hidden_unit(kb, h, m)] : 0.0f;
-        }
-        v[m] = w;
-    }
+    for (int m = 0; m < 8; ++m) v[m] = mask_weight(w0, w1, w2, K, step, slot, lane, m);
     uint4 a, b;
-    to_operand<EXACT>(v, a, b);
+    to_operand<true>(v, 1.0f, a, b);
     packed[(size_t)step * kStepVec + slot * 64 + lane] = a;
     packed[(size_t)step * kStepVec + 512 + slot * 64 + lane] = b;
+}
+
+// f16x3 weights (head_mode 0): one workgroup finds each tensor's max |w|, then
+// packs the fragments scaled by that tensor's power of two; kexp[3] (after
+// the fragments) = the tensors' log2 scales
+__global__ void __launch_bounds__(1024)
+k_mask_pack_h16(const float* __restrict__ w0, const float* __restrict__ w1, const float* __restrict__ w2,
+                uint32_t K, uint4* __restrict__ packed) {
+    __shared__ float wm[3][16];
+    __shared__ int ke[3];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float m0 = 0.0f, m1 = 0.0f, m2 = 0.0f;
+    for (int i = tid; i < 256 * kMIn; i += 1024) m0 = fmaxf(m0, fabsf(w0[i]));
+    for (int i = tid; i < 256 * 256; i += 1024) m1 = fmaxf(m1, fabsf(w1[i]));
+    for (int i = tid; i < (int)K * 256; i += 1024) m2 = fmaxf(m2, fabsf(w2[i]));
+    m0 = wave_max64(m0);
+    m1 = wave_max64(m1);
+    m2 = wave_max64(m2);
+    if (lane == 0) {
+        wm[0][wave] = m0;
+        wm[1][wave] = m1;
+        wm[2][wave] = m2;
+    }
+    __syncthreads();
+    if (tid < 3) {
+        float m = 0.0f;
+        for (int w = 0; w < 16; ++w) m = fmaxf(m, wm[tid][w]);
+        ke[tid] = scale_exp_of_max(m);
+    }
+    __syncthreads();
+    for (int t = tid; t < kStepsPerSample * 8 * 64; t += 1024) {
+        const int lane2 = t & 63, slot = (t >> 6) & 7, step = t >> 9;
+        float v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[m] = mask_weight(w0, w1, w2, K, step, slot, lane2, m);
+        uint4 a, b;
+        to_operand<false>(v, exp2i(ke[step_layer(step)]), a, b);
+        packed[(size_t)step * kStepVec + slot * 64 + lane2] = a;
+        packed[(size_t)step * kStepVec + 512 + slot * 64 + lane2] = b;
+    }
+    if (tid < 3) reinterpret_cast<int*>(packed + (size_t)kStepsPerSample * kStepVec)[tid] = ke[tid];
 }
 
 struct MaskArgs {
@@ -164,95 +172,19 @@ struct MaskArgs {
     uint32_t N, K;
     RayTiles tiles;
     const uint4* packed;
+    const int* kexp;         // f16x3: the three weight tensors' log2 scales
     float* out;              // [N][K] (ray order)
 };
 
-// The weight stream of sam_head.hip's HeadStepper (DMA from inline asm into a
-// kRing-step LDS ring, kRing - 1 steps ahead, counted vmcnt): the gathers issued at the
-// start of each sample are ordinary loads younger or older than the DMAs, and
-// either way only make those counted waits wait longer.
-struct MaskStepper {
-    const uint4* __restrict__ packed;
-    uint4* Wb;
-    int wave, lane;
-    uint32_t step;                                        // global step (sample * 27 + s)
-    uint32_t total;
-
-    __device__ __forceinline__ void issue(uint32_t s) {
-#ifdef SAMNERF_DIAG_MASK_NODMA
-        return;
-#endif
-        const uint4* src = packed + (size_t)(s % kStepsPerSample) * kStepVec + wave * 256 + lane;
-        const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(Wb + (s % kRing) * kStepVec + wave * 256);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t d = __builtin_amdgcn_readfirstlane(dst + c * 1024u);
-            uint32_t keep;
-            asm volatile(
-                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                : "=&s"(keep)
-                : "v"(src + c * 64), "s"(d)
-                : "memory");
-        }
-    }
-
-    __device__ __forceinline__ void finish() {
-        if (step + kRing - 1 < total) asm volatile(MASK_VMCNT_AHEAD ::: "memory");   // step + 1 landed
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#ifndef SAMNERF_DIAG_MASK_NOBARRIER
-        __builtin_amdgcn_s_barrier();
-#endif
-        ++step;
-    }
-
-    // one k-block for all 8 output tiles
-    template <bool EXACT>
-    __device__ __forceinline__ void run8(floatx16 (&acc)[8], const uint4& b0, const uint4& b1) {
-        if (step + kRing - 1 < total) issue(step + kRing - 1);
-        const uint4* cur = Wb + (step % kRing) * kStepVec + lane;
-        uint4 f0[8], f1[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            f0[t] = cur[t * 64];
-            f1[t] = cur[512 + t * 64];
-        }
-#ifdef SAMNERF_DIAG_MASK_NOMFMA
-#pragma unroll
-        for (int t = 0; t < 8; ++t) acc[t][0] += __uint_as_float(f0[t].x ^ f1[t].y ^ b0.x ^ b1.w);
-#else
-#pragma unroll
-        for (int t = 0; t < 8; ++t) acc[t] = kblock<EXACT>(f0[t], f1[t], b0, b1, acc[t]);
-#endif
-        finish();
-    }
-
-    // eight k-blocks of the one output tile
-    template <bool EXACT>
-    __device__ __forceinline__ void run1(floatx16& acc, const uint4* b0, const uint4* b1) {
-        if (step + kRing - 1 < total) issue(step + kRing - 1);
-        const uint4* cur = Wb + (step % kRing) * kStepVec + lane;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc = kblock<EXACT>(cur[k * 64], cur[512 + k * 64], b0[k], b1[k], acc);
-        finish();
-    }
-};
-
-// SAMNERF_MASK_STAGE=1: the weight stream through VGPRs instead of LDS-DMA.
-// Steps go in groups of kGroup: the block's 256 threads load the next group
-// (kGroup x 16 KiB, four 16-B loads per thread and step) at the start of a
-// group, write it to the other half of a 2-group LDS ring after the group's
-// MFMAs, then one barrier per group.  Ordinary loads and stores whose waits
-// the compiler places itself.
-#ifndef SAMNERF_MASK_STAGE
-#define SAMNERF_MASK_STAGE 1
-#endif
-#ifndef SAMNERF_MASK_GROUP
-#define SAMNERF_MASK_GROUP 1          // 2: 512 VGPRs and 52-93 spilled (vs 392, none).
-#endif                                // Two register stages (load two steps ahead,
-                                      // parity-selected): 8.75 -> 13.7 ms per view.
-constexpr uint32_t kGroup = SAMNERF_MASK_GROUP;
+// The weight stream, staged through VGPRs: steps go in groups of kGroup; the
+// block's 256 threads load the next group (kGroup x 16 KiB, four 16-B loads
+// per thread and step) at the start of a group, write it to the other half of
+// a 2-group LDS ring after the group's MFMAs, then one barrier per group.
+// Ordinary loads and stores whose waits the compiler places itself.  (Round
+// 2: the SAM head's LDS-DMA ring (3- and 4-deep) measured DMA-throughput-bound
+// here, 10.1 / 8.92 ms per 512^2 view against 8.75 ms for this form; two steps
+// per group spilled 52-93 VGPRs; two register stages 13.7 ms.)
+constexpr uint32_t kGroup = 1;
 struct MaskStager {
     const uint4* __restrict__ packed;
     uint4* Wb;            // [2][kGroup][kStepVec]
@@ -315,17 +247,32 @@ struct MaskStager {
 __device__ __forceinline__ float leaky(float x) { return x < 0.0f ? x * 0.01f : x; }
 
 // leaky_relu on the accumulators, then the next layer's B operands (k-block
-// kb = 2t + s <- registers 8s..8s+7 of tile t, hidden_unit order)
+// kb = 2t + s <- registers 8s..8s+7 of tile t, hidden_unit order).  f16x3:
+// scaled by 2^k, k from the sample column's max |value| (both half-waves);
+// returns k (leaky_relu is positively homogeneous, so the raw accumulators'
+// scale carries through it)
 template <bool EXACT>
-__device__ __forceinline__ void epilogue(const floatx16 (&acc)[8], uint4 (&a0)[kHkb], uint4 (&a1)[kHkb]) {
+__device__ __forceinline__ int epilogue(floatx16 (&acc)[8], uint4 (&a0)[kHkb], uint4 (&a1)[kHkb]) {
+    float m = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            acc[t][q] = leaky(acc[t][q]);
+            if constexpr (!EXACT) m = fmaxf(m, fabsf(acc[t][q]));
+        }
+    int k = 0;
+    if constexpr (!EXACT) k = scale_exp_of_max(fmaxf(m, __shfl_xor(m, 32)));
+    const float s = EXACT ? 1.0f : exp2i(k);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         float v[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) v[q] = leaky(acc[t][q]);
-        to_operand<EXACT>(v, a0[2 * t], a1[2 * t]);
-        to_operand<EXACT>(v + 8, a0[2 * t + 1], a1[2 * t + 1]);
+        for (int q = 0; q < 16; ++q) v[q] = acc[t][q];
+        to_operand<EXACT>(v, s, a0[2 * t], a1[2 * t]);
+        to_operand<EXACT>(v + 8, s, a0[2 * t + 1], a1[2 * t + 1]);
     }
+    return k;
 }
 
 constexpr int kXVec = kL0kb * 2 * 64;          // uint4 per wave: layer-0 B operands [kb][part][lane]
@@ -340,7 +287,7 @@ k_mask_head(MaskArgs a) {
     // activations: with them the kernel spilled ~350 registers) | the m_grid
     // level descriptors (read per lane: a select between two kernel-argument
     // descriptors became per-lane loads from the kernarg segment)
-    constexpr uint32_t kRingUsed = SAMNERF_MASK_STAGE ? 2u * kGroup : kRing;
+    constexpr uint32_t kRingUsed = 2u * kGroup;
     __shared__ uint4 smem[kRingUsed * kStepVec + 4 * kXVec + kDescVec];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int j = lane & 31, h = lane >> 5;
@@ -351,20 +298,14 @@ k_mask_head(MaskArgs a) {
     LevelDesc* const sLv = reinterpret_cast<LevelDesc*>(smem + kRingUsed * kStepVec + 4 * kXVec);
     if (tid < 16) sLv[tid] = a.grid.lv[tid];
 
-#if SAMNERF_MASK_STAGE
     MaskStager st{a.packed, smem, tid, lane, 0u, (uint32_t)kT * kStepsPerSample, {}};
     st.begin();
-#else
-    MaskStepper st{a.packed, smem, wave, lane, 0u, (uint32_t)kT * kStepsPerSample};
-#pragma unroll
-    for (uint32_t i = 0; i + 1 < kRing; ++i) st.issue(i);
-    asm volatile(MASK_VMCNT_AHEAD ::: "memory");              // step 0 landed
-    __syncthreads();
-#endif
 
     floatx16 sum = {};                                       // sum_k w_k * logits_k
     floatx16 acc[8];
     uint4 a0[kHkb], a1[kHkb];
+    // f16x3: log2 scales of the weight tensors (uniform)
+    const int kw0 = EXACT ? 0 : a.kexp[0], kw1 = EXACT ? 0 : a.kexp[1], kw2 = EXACT ? 0 : a.kexp[2];
 #pragma unroll 1
     for (int k = 0; k < kT; ++k) {
         // inputs of sample k.  `ko` is opaque so that the per-sample addresses
@@ -375,21 +316,22 @@ k_mask_head(MaskArgs a) {
         const float* up = a.u_in + (size_t)ko * 3u * N + ss;
         const float ux = up[0], uy = up[N], uz = up[2u * N];
         const float w = live ? a.w_in[(size_t)ko * N + ss] : 0.0f;
-        // the m_grid gathers: lane half h of k-block kb = level 2 kb + h
+        // the m_grid gathers: lane half h of k-block kb = level 2 kb + h; Xw
+        // holds the fp32 values (8 per lane and k-block, as two uint4), split
+        // into B operands as each k-block is consumed (f16x3: at the scale of
+        // the column's max over all 143 inputs)
+        float xm = 0.0f;
 #pragma unroll
         for (int kb = 0; kb < 8; ++kb) {
             float f[8];
             const LevelDesc d = sLv[2 * kb + h];
-#ifdef SAMNERF_DIAG_MASK_NOGATHER
-#pragma unroll
-            for (int m = 0; m < 8; ++m) f[m] = ux * (float)(m + 1) + d.fres * uy;
-#else
             lookup_level3<8>(a.grid.emb, d, ux, uy, uz, f);
-#endif
             uint4 xa, xb;
-            to_operand<EXACT>(f, xa, xb);
+            to_operand<true>(f, 1.0f, xa, xb);
             Xw[(2 * kb) * 64 + lane] = xa;
             Xw[(2 * kb + 1) * 64 + lane] = xb;
+#pragma unroll
+            for (int m = 0; m < 8; ++m) xm = fmaxf(xm, fabsf(f[m]));
         }
         {
             float g[8];
@@ -397,28 +339,41 @@ k_mask_head(MaskArgs a) {
             for (int m = 0; m < 8; ++m) {
                 const int gi = 8 * h + m;                    // geo_feat index; 15 = padding
                 g[m] = gi < 15 ? a.geo_in[((size_t)ko * 16u + gi + 1) * N + ss] : 0.0f;
+                xm = fmaxf(xm, fabsf(g[m]));
             }
             uint4 xa, xb;
-            to_operand<EXACT>(g, xa, xb);
+            to_operand<true>(g, 1.0f, xa, xb);
             Xw[16 * 64 + lane] = xa;
             Xw[17 * 64 + lane] = xb;
         }
+        const int k0 = EXACT ? 0 : scale_exp_of_max(fmaxf(xm, __shfl_xor(xm, 32)));
+        const float s0 = EXACT ? 1.0f : exp2i(k0);
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] = floatx16{};
 #pragma unroll
-        for (int kb = 0; kb < kL0kb; ++kb)
-            st.run8<EXACT>(acc, Xw[(2 * kb) * 64 + lane], Xw[(2 * kb + 1) * 64 + lane]);
-        epilogue<EXACT>(acc, a0, a1);
+        for (int kb = 0; kb < kL0kb; ++kb) {
+            uint4 b0 = Xw[(2 * kb) * 64 + lane], b1 = Xw[(2 * kb + 1) * 64 + lane];
+            if constexpr (!EXACT) {
+                const float v[8] = {__uint_as_float(b0.x), __uint_as_float(b0.y), __uint_as_float(b0.z),
+                                    __uint_as_float(b0.w), __uint_as_float(b1.x), __uint_as_float(b1.y),
+                                    __uint_as_float(b1.z), __uint_as_float(b1.w)};
+                to_operand<false>(v, s0, b0, b1);
+            }
+            st.run8<EXACT>(acc, b0, b1);
+        }
+        const int k1 = epilogue<EXACT>(acc, a0, a1);
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] = floatx16{};
 #pragma unroll
         for (int kb = 0; kb < kHkb; ++kb) st.run8<EXACT>(acc, a0[kb], a1[kb]);
-        epilogue<EXACT>(acc, a0, a1);
+        const int k2 = epilogue<EXACT>(acc, a0, a1);
         floatx16 o = {};
         st.run1<EXACT>(o, a0, a1);
         st.run1<EXACT>(o, a0 + 8, a1 + 8);
+        // f16x3: o carries 2^(k0 + kw0 + k1 + kw1 + k2 + kw2); w * 2^-e is exact
+        const float wo = EXACT ? w : w * exp2i(-(k0 + kw0 + k1 + kw1 + k2 + kw2));
 #pragma unroll
-        for (int q = 0; q < 16; ++q) sum[q] = __builtin_fmaf(w, o[q], sum[q]);
+        for (int q = 0; q < 16; ++q) sum[q] = __builtin_fmaf(wo, o[q], sum[q]);
     }
     if (!live) return;
     float* dst = a.out + (size_t)a.tiles(slot) * a.K;
@@ -433,7 +388,7 @@ k_mask_head(MaskArgs a) {
 
 namespace samnerf {
 
-size_t mask_head_packed_floats() { return (size_t)kStepsPerSample * kStepVec * 4; }
+size_t mask_head_packed_floats() { return (size_t)kStepsPerSample * kStepVec * 4 + 4; }
 
 int mask_head_forward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
                       const float* geo_f, uint32_t N, float* out, RayTiles tiles, float* packed,
@@ -449,14 +404,14 @@ int mask_head_forward(const samnerf_model* m, const GridDesc<16>& grid, const fl
     a.K = m->mask_out;
     a.tiles = tiles;
     a.packed = pk;
+    a.kexp = reinterpret_cast<const int*>(pk + (size_t)kStepsPerSample * kStepVec);
     a.out = out;
     if (m->head_mode == 1) {
-        k_mask_pack<true><<<div_up(nfrag, 256), 256, 0, s>>>(m->mask_w[0], m->mask_w[1], m->mask_w[2],
-                                                             m->mask_out, pk);
+        k_mask_pack_f32<<<div_up(nfrag, 256), 256, 0, s>>>(m->mask_w[0], m->mask_w[1], m->mask_w[2],
+                                                           m->mask_out, pk);
         k_mask_head<true><<<div_up(N, (uint32_t)kSlots), 256, 0, s>>>(a);
     } else {
-        k_mask_pack<false><<<div_up(nfrag, 256), 256, 0, s>>>(m->mask_w[0], m->mask_w[1], m->mask_w[2],
-                                                              m->mask_out, pk);
+        k_mask_pack_h16<<<1, 1024, 0, s>>>(m->mask_w[0], m->mask_w[1], m->mask_w[2], m->mask_out, pk);
         k_mask_head<false><<<div_up(N, (uint32_t)kSlots), 256, 0, s>>>(a);
     }
     return check_launch("mask_head");

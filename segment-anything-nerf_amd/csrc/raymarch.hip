@@ -26,6 +26,7 @@
 #include <cstring>
 #include <type_traits>
 
+#include "f16x3.h"
 #include "raymarch_device.h"
 #include "samnerf_common.h"
 #include "sh_device.h"
@@ -489,6 +490,8 @@ struct FinalArgs {
     const float* G0;   // grid_mlp [64,32]
     const float* G1;   // [64,64]
     const float* G2;   // [16,64]
+    const uint4* gpack;     // f16x3: the grid_mlp fragments [hi / lo][kFSlots][64] (k_pack_grid_mlp)
+    const int* gexp;        // f16x3: log2 scale of G0 / G1 / G2's fragments
     const float* V0;   // view_mlp [32,31]
     const float* V1;   // [32,32]
     const float* V2;   // [3,32]
@@ -515,26 +518,21 @@ struct FinalArgs {
 
 constexpr int kAeff = 240;          // columns of the adaptive heads' effective matrix
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-// ---- grid_mlp on bf16x3 MFMAs (v_mfma_f32_32x32x16_bf16, fp32 accumulate).
+// ---- grid_mlp on f16x3 MFMAs (v_mfma_f32_32x32x16_f16, fp32 accumulate).
 // Transposed orientation: A = weights (rows = hidden units), B = activations
 // (columns = 32 rays), so a layer's accumulator is the next layer's B operand
 // as it stands.  Lane (j, h) of a 32x32 accumulator holds rows rho(q) + 4h,
 // rho(q) = (q&3) + 8(q>>2); k-block kb of a 64-wide input takes registers
 // 8(kb&1)..8(kb&1)+7 of tile kb>>1, and the weights are stored permuted to
-// match (hidden_unit).  Each product is split x = hi + lo (bf16 RNE) and
-// A.B ~= A_lo.B_hi + A_hi.B_lo + A_hi.B_hi: ~2^-16 relative error per product
-// against the 1e-3 output budget, at 3 MFMAs of 32 cycles per 16-deep k-block
+// match (hidden_unit).  Each product is split x = hi + lo (fp16 RNE, on
+// power-of-two scaled operands) and A.B = A_lo.B_hi + A_hi.B_lo + A_hi.B_hi
+// (f16x3.h): fp32-equivalent, at 3 MFMAs of 32 cycles per 16-deep k-block
 // instead of 8 fp32 MFMAs of 64.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-typedef float float2v __attribute__((ext_vector_type(2)));
 
 constexpr int kF1 = 0;               // grid_mlp.0: slot kb*2 + ob      (kb < 2)  W[64,32]
 constexpr int kF2 = 4;               // grid_mlp.1: slot 4 + kb*2 + ob  (kb < 4)  W[64,64]
 constexpr int kF3 = 12;              // grid_mlp.2: slot 12 + kb        (kb < 4)  W[16,64]
-constexpr int kFSlots = 16;          // x 64 lanes x (8 bf16 hi + 8 bf16 lo)
+constexpr int kFSlots = 16;          // x 64 lanes x (8 f16 hi + 8 f16 lo)
 // view_mlp on v_mfma_f32_32x32x2_f32 (once per ray): [q 16][lane] each
 constexpr int kV1 = 0;               // view_mlp.0  q<8: geo acc rows, q>=8: sh pairs
 constexpr int kV2 = 1024;            // view_mlp.1  W[32,32]
@@ -608,28 +606,44 @@ __device__ float grid_weight_exact(const FinalArgs& a, int step, int lane) {
     return i < 16 ? a.G2[i * 64 + t * 32 + rho(q) + 4 * h] : 0.0f;
 }
 
-__device__ __forceinline__ void split_pair(float x, float y, uint32_t& hi, uint32_t& lo) {
-    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v){x, y}, bf16x2v));
-    const float hx = __uint_as_float(hi << 16), hy = __uint_as_float(hi & 0xffff0000u);
-    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v){x - hx, y - hy}, bf16x2v));
-}
-
-__device__ __forceinline__ void split8(const float* v, uint4& hi, uint4& lo) {
-    split_pair(v[0], v[1], hi.x, lo.x);
-    split_pair(v[2], v[3], hi.y, lo.y);
-    split_pair(v[4], v[5], hi.z, lo.z);
-    split_pair(v[6], v[7], hi.w, lo.w);
-}
-
 #define MFMA32(A, B, C) __builtin_amdgcn_mfma_f32_32x32x2f32((A), (B), (C), 0, 0, 0)
-#define MFMA_BF16(A, B, C) __builtin_amdgcn_mfma_f32_32x32x16_bf16((A), (B), (C), 0, 0, 0)
 
-__device__ __forceinline__ floatx16 mfma3(uint4 ah, uint4 al, uint4 bh, uint4 bl, floatx16 c) {
-    const bf16x8 Ah = __builtin_bit_cast(bf16x8, ah), Al = __builtin_bit_cast(bf16x8, al);
-    const bf16x8 Bh = __builtin_bit_cast(bf16x8, bh), Bl = __builtin_bit_cast(bf16x8, bl);
-    c = MFMA_BF16(Al, Bh, c);
-    c = MFMA_BF16(Ah, Bl, c);
-    return MFMA_BF16(Ah, Bh, c);
+// grid_mlp fragments for the f16x3 form (head_mode 0, f16x3.h), once per
+// render (one workgroup): each weight tensor scaled by the power of two that
+// puts its max |w| in [2^14, 2^15), in grid_weight's slot layout, hi then lo;
+// gexp[l] = log2 of tensor l's scale.  (A per-tensor scale: the scaled
+// accumulators of a sample column then differ from the true values by one
+// factor, so each layer's outputs are rescaled straight from their max.)
+__global__ void __launch_bounds__(256) k_pack_grid_mlp(FinalArgs a, uint4* gpack, int* gexp) {
+    __shared__ float wm[3][4];
+    __shared__ int ke[3];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float m0 = 0.0f, m1 = 0.0f, m2 = 0.0f;
+    for (int i = tid; i < 64 * 32; i += 256) m0 = fmaxf(m0, fabsf(a.G0[i]));
+    for (int i = tid; i < 64 * 64; i += 256) m1 = fmaxf(m1, fabsf(a.G1[i]));
+    for (int i = tid; i < 16 * 64; i += 256) m2 = fmaxf(m2, fabsf(a.G2[i]));
+    m0 = wave_max64(m0);
+    m1 = wave_max64(m1);
+    m2 = wave_max64(m2);
+    if (lane == 0) {
+        wm[0][wave] = m0;
+        wm[1][wave] = m1;
+        wm[2][wave] = m2;
+    }
+    __syncthreads();
+    if (tid < 3) {
+        const float m = fmaxf(fmaxf(wm[tid][0], wm[tid][1]), fmaxf(wm[tid][2], wm[tid][3]));
+        ke[tid] = scale_exp_of_max(m);
+        gexp[tid] = ke[tid];
+    }
+    __syncthreads();
+    for (int idx = tid; idx < kFSlots * 64; idx += 256) {
+        const int slot = idx >> 6, layer = slot < kF2 ? 0 : slot < kF3 ? 1 : 2;
+        float v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[m] = grid_weight(a, slot, idx & 63, m);
+        split8_f16(v, exp2i(ke[layer]), gpack[idx], gpack[kFSlots * 64 + idx]);
+    }
 }
 
 // Trilinear lookup of both channels of NL L16C2 levels whose descriptors
@@ -788,7 +802,7 @@ __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const Leve
 // levels final_level(kb, h, 0..3) = 8kb + h, 8kb + 2 + h, .. -- exactly its B
 // operand of the first layer (grid_weight permutes the weight columns to
 // match) -- so the hash grid feeds the matrix cores
-// with no data movement.  grid_mlp 32->64->64->16 runs on bf16x3 MFMAs,
+// with no data movement.  grid_mlp 32->64->64->16 runs on f16x3 MFMAs,
 // view_mlp 31->32->32->3 (once per ray) on fp32 MFMAs.  Compositing: each
 // step the S slots of a ray exchange their optical depths by shuffle and
 // every lane forms the ray's exclusive cumulative sum in sample order (the
@@ -829,9 +843,9 @@ k_final(FinalArgs a) {
     static_assert(AD == 0 || (S == 1 && !PF), "adaptive mask forms: one segment, no prefetch");
     static_assert(AD != 2 || SA, "the 'rgb' adaptive head reads the per-sample view MLP (sum_after_mlp)");
     static_assert(S == 1 || S == 2 || S == 4, "segments per ray");
-    static_assert(kXSteps * 64 == 2 * kFSlots * 64 * 4, "exact weights reuse the bf16x3 slots");
+    static_assert(kXSteps * 64 == 2 * kFSlots * 64 * 4, "exact weights reuse the f16x3 slots");
     constexpr int R = 32 / S, TS = T / S;
-    __shared__ uint4 Fbuf[2 * kFSlots * 64];          // bf16x3: hi | lo fragments; exact: fp32 steps
+    __shared__ uint4 Fbuf[2 * kFSlots * 64];          // f16x3: hi | lo fragments; exact: fp32 steps
     __shared__ float Vl[kVTotal];
     __shared__ LevelDesc sLv[16];
     if (threadIdx.x < 16) sLv[threadIdx.x] = a.grid.lv[threadIdx.x];
@@ -842,14 +856,11 @@ k_final(FinalArgs a) {
         for (int idx = threadIdx.x; idx < kXSteps * 64; idx += 256)
             Fx[idx] = grid_weight_exact(a, idx >> 6, idx & 63);
     } else {
-        for (int idx = threadIdx.x; idx < kFSlots * 64; idx += 256) {
-            float v[8];
-#pragma unroll
-            for (int m = 0; m < 8; ++m) v[m] = grid_weight(a, idx >> 6, idx & 63, m);
-            split8(v, Fh[idx], Fl[idx]);
-        }
+        for (int idx = threadIdx.x; idx < 2 * kFSlots * 64; idx += 256) Fbuf[idx] = a.gpack[idx];
     }
     for (int idx = threadIdx.x; idx < kVTotal; idx += 256) Vl[idx] = view_weight(a, idx);
+    // f16x3: log2 scales of the three weight tensors' fragments
+    const int ke0 = EXACT ? 0 : a.gexp[0], ke1 = EXACT ? 0 : a.gexp[1], ke2 = EXACT ? 0 : a.gexp[2];
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -981,6 +992,16 @@ k_final(FinalArgs a) {
 
         floatx16 h1a = {}, h1b = {};
         float fk[AD ? 16 : 1];                           // AD: this sample's grid features (by k-block)
+        // f16x3 (f16x3.h): each layer's B operands are scaled by the power of
+        // two that puts the sample column's max |input| in [2^14, 2^15);
+        // e_h1 / e_h2 / e_o3 = log2 of the factor a layer's accumulators carry
+        // over the true values (input scales + weight-tensor scales).  Layer 1
+        // takes its two k-blocks one at a time (holding the first block's
+        // features through the second gather costs ~50 VGPRs): the running
+        // scale is the first block's, lowered -- and the accumulators rescaled
+        // by the same exact power of two -- when the second block's max is
+        // larger.
+        int k1 = 0, e_h1 = 0, e_h2 = 0;
 #pragma unroll
         for (int kbi = 0; kbi < 2; ++kbi) {
             const int kb = kbi == 0 ? kPre : 1 - kPre;
@@ -1003,12 +1024,29 @@ k_final(FinalArgs a) {
                     h1b = MFMA32(FX[(16 + kb * 8 + m) * 64], f[m], h1b);
                 }
             } else {
+                float m = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(f[e]));
+                m = fmaxf(m, __shfl_xor(m, 32));
+                const int kk = scale_exp_of_max(m);
+                if (kbi == 0) {
+                    k1 = kk;
+                } else if (kk < k1) {                    // lanes of one column agree (both halves)
+                    const float r = exp2i(kk - k1);
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        h1a[q] *= r;
+                        h1b[q] *= r;
+                    }
+                    k1 = kk;
+                }
                 uint4 bh, bl;
-                split8(f, bh, bl);
-                h1a = mfma3(FH[(kF1 + 2 * kb) * 64], FL[(kF1 + 2 * kb) * 64], bh, bl, h1a);
-                h1b = mfma3(FH[(kF1 + 2 * kb + 1) * 64], FL[(kF1 + 2 * kb + 1) * 64], bh, bl, h1b);
+                split8_f16(f, exp2i(k1), bh, bl);
+                h1a = mfma_f16x3(FH[(kF1 + 2 * kb) * 64], FL[(kF1 + 2 * kb) * 64], bh, bl, h1a);
+                h1b = mfma_f16x3(FH[(kF1 + 2 * kb + 1) * 64], FL[(kF1 + 2 * kb + 1) * 64], bh, bl, h1b);
             }
         }
+        if constexpr (!EXACT) e_h1 = k1 + ke0;
         if constexpr (PF) {
             if (i + 1 < TS) {
                 LevelDesc dl[4];
@@ -1017,6 +1055,16 @@ k_final(FinalArgs a) {
                 position(i + 1, p_rbp, p_rbn, p_ux, p_uy, p_uz);
                 gather_issue_c2<4>(emb, dl, p_ux, p_uy, p_uz, pre, pf_kinds(kPre));
             }
+        }
+        float s2 = 1.0f;
+        if constexpr (!EXACT) {                          // max of relu(h1): the raw max, floored at 0
+            float m = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) m = fmaxf(m, fmaxf(h1a[i], h1b[i]));
+            m = fmaxf(m, __shfl_xor(m, 32));
+            const int k2 = scale_exp_of_max(m);
+            s2 = exp2i(k2);
+            e_h2 = e_h1 + k2 + ke1;
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -1042,11 +1090,22 @@ k_final(FinalArgs a) {
 #pragma unroll
                 for (int m = 0; m < 8; ++m) v[m] = (kb >> 1) ? h1b[8 * (kb & 1) + m] : h1a[8 * (kb & 1) + m];
                 uint4 bh, bl;
-                split8(v, bh, bl);
-                h2a = mfma3(FH[(kF2 + 2 * kb) * 64], FL[(kF2 + 2 * kb) * 64], bh, bl, h2a);
-                h2b = mfma3(FH[(kF2 + 2 * kb + 1) * 64], FL[(kF2 + 2 * kb + 1) * 64], bh, bl, h2b);
+                split8_f16(v, s2, bh, bl);
+                h2a = mfma_f16x3(FH[(kF2 + 2 * kb) * 64], FL[(kF2 + 2 * kb) * 64], bh, bl, h2a);
+                h2b = mfma_f16x3(FH[(kF2 + 2 * kb + 1) * 64], FL[(kF2 + 2 * kb + 1) * 64], bh, bl, h2b);
                 __builtin_amdgcn_sched_barrier(0);
             }
+        }
+        float s3 = 1.0f;
+        int e_o3 = 0;
+        if constexpr (!EXACT) {
+            float m = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) m = fmaxf(m, fmaxf(h2a[i], h2b[i]));
+            m = fmaxf(m, __shfl_xor(m, 32));
+            const int k3 = scale_exp_of_max(m);
+            s3 = exp2i(k3);
+            e_o3 = e_h2 + k3 + ke2;
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -1068,10 +1127,14 @@ k_final(FinalArgs a) {
 #pragma unroll
                 for (int m = 0; m < 8; ++m) v[m] = (kb >> 1) ? h2b[8 * (kb & 1) + m] : h2a[8 * (kb & 1) + m];
                 uint4 bh, bl;
-                split8(v, bh, bl);
-                o3 = mfma3(FH[(kF3 + kb) * 64], FL[(kF3 + kb) * 64], bh, bl, o3);
+                split8_f16(v, s3, bh, bl);
+                o3 = mfma_f16x3(FH[(kF3 + kb) * 64], FL[(kF3 + kb) * 64], bh, bl, o3);
                 __builtin_amdgcn_sched_barrier(0);
             }
+            // back to the true outputs (rows 0..15 = registers 0..7 of both halves)
+            const float inv = exp2i(-e_o3);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) o3[q] = o3[q] * inv;
         }
 
         // sigma pre-activation = row 0, held by the lower half-wave
@@ -1097,12 +1160,14 @@ k_final(FinalArgs a) {
         if constexpr (AD > 0) {
 #pragma unroll
             for (int m = 0; m < 16; ++m) gacc[m] = gacc[m] + w * fk[m];
+            // f16x3: the accumulators carry 2^e_h1 / 2^e_h2 (w * 2^-e is exact)
+            const float w1 = EXACT ? w : w * exp2i(-e_h1), w2 = EXACT ? w : w * exp2i(-e_h2);
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                h1acc[q] = h1acc[q] + w * h1a[q];
-                h1acc[16 + q] = h1acc[16 + q] + w * h1b[q];
-                h2acc[q] = h2acc[q] + w * h2a[q];
-                h2acc[16 + q] = h2acc[16 + q] + w * h2b[q];
+                h1acc[q] = h1acc[q] + w1 * h1a[q];
+                h1acc[16 + q] = h1acc[16 + q] + w1 * h1b[q];
+                h2acc[q] = h2acc[q] + w2 * h2a[q];
+                h2acc[16 + q] = h2acc[16 + q] + w2 * h2b[q];
             }
         }
         if (GEO && live) {                               // rows rho(q) + 4 hh of this sample
@@ -1756,6 +1821,8 @@ struct Workspace {
     float* w_f;
     float* rows;
     float* packed;
+    uint4* gpack;      // f16x3 grid_mlp fragments [2][kFSlots][64] (head_mode 0)
+    int* gexp;         // their tensors' log2 scales [3]
     float* geo_f;      // [32][16][N] grid_mlp output rows per sample (with_mask, kind 0)
     float* mpacked;    // mask head weight stream (with_mask, kind 0)
     float* aeff;       // [K][240] adaptive heads' effective matrix (with_mask, kinds 1-2)
@@ -1951,6 +2018,8 @@ Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
     w.w_f = take((size_t)m->num_steps[2] * n);
     w.rows = take((size_t)kRow * n);
     w.packed = take(m->with_sam ? sam_head_packed_floats() : 0);
+    w.gpack = reinterpret_cast<uint4*>(take((size_t)2 * kFSlots * 64 * 4));
+    w.gexp = reinterpret_cast<int*>(take(4));
     const bool mdef = m->with_mask && m->mask_kind == 0, madapt = m->with_mask && m->mask_kind > 0;
     w.geo_f = take(mdef ? (size_t)16 * m->num_steps[2] * n : 0);
     w.mpacked = take(mdef ? mask_head_packed_floats() : 0);
@@ -2300,8 +2369,14 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     if (m->sum_after_mlp && (m->t_thresh > 0.0f || sam_rows))
         return fail(SAMNERF_EINVAL, "render_forward: sum_after_mlp renders RGB (+ mask) only: no SAM "
                     "features (the reference's branch crashes, SURVEY 0.2) and no t_thresh");
-    if (m->head_mode == 1) launch_final<true>(seg, pf, N, s, fa, m->sum_after_mlp != 0, ad);
-    else launch_final<false>(seg, pf, N, s, fa, m->sum_after_mlp != 0, ad);
+    if (m->head_mode == 1) {
+        launch_final<true>(seg, pf, N, s, fa, m->sum_after_mlp != 0, ad);
+    } else {
+        fa.gpack = w.gpack;
+        fa.gexp = w.gexp;
+        k_pack_grid_mlp<<<1, 256, 0, s>>>(fa, w.gpack, w.gexp);
+        launch_final<false>(seg, pf, N, s, fa, m->sum_after_mlp != 0, ad);
+    }
 
     if (sam_rows) {
         SgridArgs sa{};

@@ -6,7 +6,8 @@
 //
 // fp32 in / fp32 accumulate on v_mfma_f32_32x32x2_f32 (exact f32 FMA chains,
 // cdna_hip_programming.md section 3 "FP32-input MFMA") so the head keeps the
-// 1e-3 parity budget that bf16 operands would spend.
+// 1e-3 parity budget that bf16 operands would spend.  This is
+// head_mode 1; the default (head_mode 0) is the f16x3 head below.
 //   * one workgroup = 32 rays x all 256 output columns, 4 waves, each wave two
 //     32x32 accumulator tiles;
 //   * activations live in LDS (odd row strides: conflict-free ds_read_b32 for
@@ -16,8 +17,7 @@
 //     of one 32-column tile) is one contiguous 1 KiB wave load (16 B per lane)
 //     from L2.
 #include "samnerf_common.h"
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
+#include "f16x3.h"
 
 namespace samnerf {
 
@@ -206,33 +206,30 @@ __global__ void __launch_bounds__(256) k_sam_head(HeadArgs a) {
 }
 
 
-// ===================================================================== bf16x3
-// Split-precision head (default): x = x_hi + x_lo with x_hi = bf16(x), x_lo =
-// bf16(x - x_hi); A.B ~= A_lo.B_hi + A_hi.B_lo + A_hi.B_hi on
-// v_mfma_f32_32x32x16_bf16 (fp32 accumulate).  Relative error per product
-// ~2^-16 (the dropped A_lo.B_lo term and the rounding of the lo parts), i.e.
-// ~1e-5 on the head output against the 1e-3 budget, at 3 bf16 MFMAs per
-// 16-deep k-block instead of 8 fp32 ones.
+// ===================================================================== f16x3
+// fp32-equivalent head (default, f16x3.h): each fp32 product as three fp16
+// MFMA products on power-of-two scaled operands -- weight rows scaled at
+// packing (k_pack_h16, inverse kept per row), each ray's activations at run
+// time from their max over the layer's inputs.  Error against float64 at the
+// level of an exact fp32 GEMM (tools/f16x3_error.py), at 3 v_mfma_f32_32x32x16_f16
+// per 16-deep k-block instead of 8 fp32 MFMAs of twice the cycles.
 //
 // Orientation: out^T[256 units x 32 rays] = W . act^T -- A = weights (rows =
 // output units, 8 tiles of 32), B = activations (columns = the wave's 32
 // rays).  A 32x32 accumulator holds, in lane (j, h) register q, unit
 // rho(q) + 4h of ray j, rho(q) = (q&3) + 8(q>>2); k-block kb of a 256-wide
-// input takes registers 8(kb&1)..+7 of tile kb>>1, so after bias/activation
-// and the hi/lo split a layer's accumulators ARE the next layer's B operands
-// (weights are packed permuted to match, hidden_unit()).  Activations never
-// leave the registers; the x input (needed again by the skip layer) stays
-// resident as bf16 hi/lo.  Weights stream through LDS: one "step" = one
-// k-block of one layer for all 8 output tiles = 16 KiB of hi/lo fragments,
-// double-buffered and shared by the block's 4 waves (one per SIMD).
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-typedef float float2v __attribute__((ext_vector_type(2)));
-
+// input takes registers 8(kb&1)..+7 of tile kb>>1, so after bias/activation,
+// scaling and the hi/lo split a layer's accumulators ARE the next layer's B
+// operands (weights are packed permuted to match, hidden_unit()).  Activations
+// never leave the registers; the x input (needed again by the skip layer) is
+// re-read from the rows.  Weights stream through LDS: one "step" = one k-block
+// of one layer for all 8 output tiles = 16 KiB of hi/lo fragments, three
+// buffers shared by the block's 4 waves (one per SIMD).
 constexpr int kXkb = 11;                      // 163 inputs -> 11 k-blocks of 16
 constexpr int kHkb = 16;                      // 256 -> 16 k-blocks
 // step segments in consumption order: L0 (x) | L1 (h) | L2 x-part | L2 h-part | L3 | L4
 constexpr int kSegKb[6] = {kXkb, kHkb, kXkb, kHkb, kHkb, kHkb};
+constexpr int kSegLayer[6] = {0, 1, 2, 2, 3, 4};
 constexpr int segBase(int seg) {
     int b = 0;
     for (int i = 0; i < seg; ++i) b += kSegKb[i];
@@ -241,79 +238,73 @@ constexpr int segBase(int seg) {
 constexpr int kSteps = segBase(6);            // 86
 constexpr int kStepVec = 2 * 8 * 64;          // uint4 per step: [hi/lo][tile][lane]
 constexpr int kRaysV5 = 128;                  // 4 waves x 32 rays
+constexpr int kPackedVec = kSteps * kStepVec; // uint4 of fragments; then rinv [5][256] floats
 
 __device__ __forceinline__ int rho(int q) { return (q & 3) + 8 * (q >> 2); }
 __device__ __forceinline__ int hidden_unit(int kb, int h, int m) {
     return 32 * (kb >> 1) + rho(8 * (kb & 1) + m) + 4 * h;
 }
 
-__device__ __forceinline__ void split_pair(float x, float y, uint32_t& hi, uint32_t& lo) {
-    hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v){x, y}, bf16x2v));
-    const float hx = __uint_as_float(hi << 16), hy = __uint_as_float(hi & 0xffff0000u);
-    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v){x - hx, y - hy}, bf16x2v));
-}
-__device__ __forceinline__ void split8(const float* v, uint4& hi, uint4& lo) {
-    split_pair(v[0], v[1], hi.x, lo.x);
-    split_pair(v[2], v[3], hi.y, lo.y);
-    split_pair(v[4], v[5], hi.z, lo.z);
-    split_pair(v[6], v[7], hi.w, lo.w);
-}
-
-// packed[step 86][hi/lo][tile 8][lane 64] : 8 bf16 (16 B) each
-__global__ void __launch_bounds__(256)
-k_pack_bf3(const float* __restrict__ w0, const float* __restrict__ w1, const float* __restrict__ w2,
-           const float* __restrict__ w3, const float* __restrict__ w4, uint4* __restrict__ packed) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;   // one (step, tile, lane)
-    if (t >= (uint32_t)kSteps * 8u * 64u) return;
-    const int lane = (int)(t & 63u), tile = (int)((t >> 6) & 7u), step = (int)(t >> 9);
-    int seg = 0;
-    while (seg < 5 && step >= segBase(seg + 1)) ++seg;
-    const int kb = step - segBase(seg);
-    const int i = lane & 31, h = lane >> 5, unit = tile * 32 + i;
-    float v[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        const int kx = 16 * kb + 8 * h + m;           // x input column (natural order)
-        const int kh = hidden_unit(kb, h, m);         // hidden input unit (accumulator order)
-        float w;
-        switch (seg) {
-            case 0: w = kx < kIn ? w0[unit * kIn + kx] : 0.0f; break;
-            case 1: w = w1[unit * 256 + kh]; break;
-            case 2: w = kx < kIn ? w2[unit * (256 + kIn) + 256 + kx] : 0.0f; break;
-            case 3: w = w2[unit * (256 + kIn) + kh]; break;
-            case 4: w = w3[unit * 256 + kh]; break;
-            default: w = w4[unit * 256 + kh]; break;
-        }
-        v[m] = w;
+// weight of segment `seg`, k-block kb, lane half h, element m for output unit
+__device__ __forceinline__ float seg_weight(const float* const* W, int seg, int kb, int h, int m, int unit) {
+    const int kx = 16 * kb + 8 * h + m;           // x input column (natural order)
+    const int kh = hidden_unit(kb, h, m);         // hidden input unit (accumulator order)
+    switch (seg) {
+        case 0: return kx < kIn ? W[0][unit * kIn + kx] : 0.0f;
+        case 1: return W[1][unit * 256 + kh];
+        case 2: return kx < kIn ? W[2][unit * (256 + kIn) + 256 + kx] : 0.0f;
+        case 3: return W[2][unit * (256 + kIn) + kh];
+        case 4: return W[3][unit * 256 + kh];
+        default: return W[4][unit * 256 + kh];
     }
-    uint4 hi, lo;
-    split8(v, hi, lo);
-    packed[(size_t)step * kStepVec + tile * 64 + lane] = hi;
-    packed[(size_t)step * kStepVec + 512 + tile * 64 + lane] = lo;
 }
 
-struct HeadArgsB {
+// packed[step 86][hi/lo][tile 8][lane 64] (8 f16 = 16 B each), rinv[layer][unit].
+// One wave per (layer, unit) row: the row's max |w| gives its scale, then the
+// lanes write the row's fragments of every step of the layer.
+struct PackArgs {
+    const float* W[5];
+    uint4* packed;
+    float* rinv;
+};
+__global__ void __launch_bounds__(256) k_pack_h16(PackArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int g = blockIdx.x * 4 + (threadIdx.x >> 6);       // (layer, unit)
+    if (g >= 5 * 256) return;
+    const int layer = g >> 8, unit = g & 255;
+    const int kin = kLogicalIn[layer];
+    const float* row = a.W[layer] + (size_t)unit * kin;
+    float m = 0.0f;
+    for (int k = lane; k < kin; k += 64) m = fmaxf(m, fabsf(row[k]));
+    const Scale2 sc = scale_of_max(wave_max64(m));
+    if (lane == 0) a.rinv[layer * 256 + unit] = sc.inv;
+    const int tile = unit >> 5, j = unit & 31;
+    for (int seg = 0; seg < 6; ++seg) {
+        if (kSegLayer[seg] != layer) continue;
+        for (int f = lane; f < 2 * kSegKb[seg]; f += 64) {
+            const int kb = f >> 1, h = f & 1;
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = seg_weight(a.W, seg, kb, h, e, unit);
+            uint4 hi, lo;
+            split8_f16(v, sc.s, hi, lo);
+            const size_t o = (size_t)(segBase(seg) + kb) * kStepVec + tile * 64 + j + 32 * h;
+            a.packed[o] = hi;
+            a.packed[o + 512] = lo;
+        }
+    }
+}
+
+struct HeadArgsH {
     const float* rows;
     uint32_t N;
     const uint4* packed;
+    const float* rinv;
     const float* b[5];
     const float* ln_w;
     const float* ln_b;
     float* out;
 };
-
-#define MFMA_BF16(A, B, C) __builtin_amdgcn_mfma_f32_32x32x16_bf16((A), (B), (C), 0, 0, 0)
-
-__device__ __forceinline__ floatx16 mfma3(uint4 ah, uint4 al, uint4 bh, uint4 bl, floatx16 c) {
-    const bf16x8 Ah = __builtin_bit_cast(bf16x8, ah), Al = __builtin_bit_cast(bf16x8, al);
-    const bf16x8 Bh = __builtin_bit_cast(bf16x8, bh), Bl = __builtin_bit_cast(bf16x8, bl);
-    c = MFMA_BF16(Al, Bh, c);
-    c = MFMA_BF16(Ah, Bl, c);
-    return MFMA_BF16(Ah, Bh, c);
-}
-
-typedef __attribute__((address_space(1))) const void* gptr_t;
-typedef __attribute__((address_space(3))) void* lptr_t;
 
 // Weight stream: step s's 16 KiB of fragments go global -> LDS by direct DMA
 // (global_load_lds_dwordx4, no VGPRs), into one of 3 buffers, two steps
@@ -347,10 +338,7 @@ struct HeadStepper {
         }
     }
 
-    // one k-block of the current layer for all 8 output tiles.  (Holding the
-    // next step's fragments in registers, read under this step's MFMAs with
-    // the skip layer's h-part moved first to make room, measured no faster:
-    // 0.581 vs 0.575 ms per view, with 21 VGPRs spilled.)
+    // one k-block of the current layer for all 8 output tiles
     __device__ __forceinline__ void run(floatx16 (&acc)[8], const uint4& bh, const uint4& bl) {
         const bool ahead = step + 2 < kSteps;
         if (ahead) issue(step + 2);
@@ -362,7 +350,7 @@ struct HeadStepper {
             fl[t] = cur[512 + t * 64];
         }
 #pragma unroll
-        for (int t = 0; t < 8; ++t) acc[t] = mfma3(fh[t], fl[t], bh, bl, acc[t]);
+        for (int t = 0; t < 8; ++t) acc[t] = mfma_f16x3(fh[t], fl[t], bh, bl, acc[t]);
         if (ahead) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // step + 1 landed
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -371,122 +359,71 @@ struct HeadStepper {
     }
 };
 
-// SAMNERF_HEAD_STAGE=1: the same stream staged through VGPRs by ordinary
-// loads (mask_head.hip's MaskStager): each thread loads its four 16-B pieces
-// of step s + 1 at the start of step s and writes them to the other half of a
-// 2-step LDS ring after step s's MFMAs, then the barrier.  500 VGPRs, no
-// spills, but slower here: 0.58 -> 0.82 ms per view (one step of lookahead
-// exposes the load latency before the store; the DMA runs two steps ahead
-// without registers).  The mask head, whose DMA form spilled, gains from it.
-#ifndef SAMNERF_HEAD_STAGE
-#define SAMNERF_HEAD_STAGE 0
-#endif
-struct HeadStager {
-    const uint4* __restrict__ packed;
-    uint4* Wb;            // LDS [2][kStepVec]
-    int tid, lane;
-    int step;
-    uint4 stg[4];
-
-    __device__ __forceinline__ void load(int s) {
-        const uint4* src = packed + (size_t)s * kStepVec + tid;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) stg[c] = src[c * 256];
-    }
-    __device__ __forceinline__ void store(int s) {
-        uint4* dst = Wb + (s & 1) * kStepVec + tid;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) dst[c * 256] = stg[c];
-    }
-    __device__ __forceinline__ void begin() {
-        load(0);
-        store(0);
-        __syncthreads();
-    }
-    __device__ __forceinline__ void run(floatx16 (&acc)[8], const uint4& bh, const uint4& bl) {
-        const bool ahead = step + 1 < kSteps;
-        if (ahead) load(step + 1);
-        const uint4* cur = Wb + (step & 1) * kStepVec + lane;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) acc[t] = mfma3(cur[t * 64], cur[512 + t * 64], bh, bl, acc[t]);
-        if (ahead) store(step + 1);
-        __syncthreads();
-        ++step;
-    }
-};
-
 __device__ __forceinline__ float leaky(float x, bool act) { return act && x < 0.0f ? x * 0.01f : x; }
 
-// bias (+ leaky_relu) on the accumulators, then the hi/lo split into the next
-// layer's B operands (k-block kb = 2t + s <- registers 8s..8s+7 of tile t)
-__device__ __forceinline__ void epilogue(const floatx16 (&acc)[8], const float* Bs, int h,
-                                         uint4 (&ah)[kHkb], uint4 (&al)[kHkb]) {
+// The accumulators of a layer back to fp32 values in place: unscale (row and
+// column inverse scales: exact), + bias in one rounding, leaky_relu when
+// `act`; returns this lane's max |value| (the ray's other units are on lane ^ 32).
+__device__ __forceinline__ float finish_layer(floatx16 (&acc)[8], const float* Bs, const float* Rs, float inv,
+                                              int h, bool act) {
+    float m = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {       // registers 4mm..4mm+3 = units 32t + 8mm + 4h + 0..3
+            const float4 bb = *reinterpret_cast<const float4*>(Bs + 32 * t + 8 * mm + 4 * h);
+            const float4 rr = *reinterpret_cast<const float4*>(Rs + 32 * t + 8 * mm + 4 * h);
+            const float b4[4] = {bb.x, bb.y, bb.z, bb.w}, r4[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float v = leaky(__builtin_fmaf(acc[t][4 * mm + e] * r4[e], inv, b4[e]), act);
+                acc[t][4 * mm + e] = v;
+                m = fmaxf(m, fabsf(v));
+            }
+        }
+    return m;
+}
+
+// the values (times s) as the next layer's B operands: k-block kb = 2t + c
+// <- registers 8c..8c+7 of tile t
+__device__ __forceinline__ void split_layer(const floatx16 (&acc)[8], float s, uint4 (&ah)[kHkb],
+                                            uint4 (&al)[kHkb]) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         float v[16];
 #pragma unroll
-        for (int mm = 0; mm < 4; ++mm) {      // registers 4mm..4mm+3 = units 32t + 8mm + 4h + 0..3
-            const float4 bb = *reinterpret_cast<const float4*>(Bs + 32 * t + 8 * mm + 4 * h);
-            v[4 * mm + 0] = leaky(acc[t][4 * mm + 0] + bb.x, true);
-            v[4 * mm + 1] = leaky(acc[t][4 * mm + 1] + bb.y, true);
-            v[4 * mm + 2] = leaky(acc[t][4 * mm + 2] + bb.z, true);
-            v[4 * mm + 3] = leaky(acc[t][4 * mm + 3] + bb.w, true);
-        }
-        split8(v, ah[2 * t], al[2 * t]);
-        split8(v + 8, ah[2 * t + 1], al[2 * t + 1]);
+        for (int q = 0; q < 16; ++q) v[q] = acc[t][q];
+        split8_f16(v, s, ah[2 * t], al[2 * t]);
+        split8_f16(v + 8, s, ah[2 * t + 1], al[2 * t + 1]);
     }
 }
-
-// One tile's epilogue (bias + leaky_relu, then the hi/lo split): the B
-// operands of k-blocks 2t and 2t + 1 of the next layer.
-__device__ __forceinline__ void epilogue_tile(const floatx16& acc, const float* Bs, int t, int h, uint4& h0,
-                                              uint4& l0, uint4& h1, uint4& l1) {
-    float v[16];
-#pragma unroll
-    for (int mm = 0; mm < 4; ++mm) {
-        const float4 bb = *reinterpret_cast<const float4*>(Bs + 32 * t + 8 * mm + 4 * h);
-        v[4 * mm + 0] = leaky(acc[4 * mm + 0] + bb.x, true);
-        v[4 * mm + 1] = leaky(acc[4 * mm + 1] + bb.y, true);
-        v[4 * mm + 2] = leaky(acc[4 * mm + 2] + bb.z, true);
-        v[4 * mm + 3] = leaky(acc[4 * mm + 3] + bb.w, true);
-    }
-    split8(v, h0, l0);
-    split8(v + 8, h1, l1);
-}
-
-// SAMNERF_HEAD_LAZY=1: two accumulator sets that alternate by layer, and each
-// layer's epilogue done tile by tile just before the next layer's k-blocks
-// that read it (k-blocks 2t, 2t + 1 read tile t), so the VALU epilogue runs
-// beside the previous step's MFMAs instead of between layers with the matrix
-// cores idle (the round-1 VERDICT's suggestion).  The B operands no longer sit
-// in 128 registers for a whole layer, which pays for the second set.
-#ifndef SAMNERF_HEAD_LAZY
-#define SAMNERF_HEAD_LAZY 0
-#endif
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-k_sam_head_bf3(HeadArgsB a) {
+k_sam_head_h16(HeadArgsH a) {
     // one LDS object (a second __shared__ object can de-pipeline the DMA
-    // waits): 3 x 16 KiB weight steps, then biases and LN weight/bias
-    constexpr int kRingSteps = SAMNERF_HEAD_STAGE ? 2 : 3;
-    __shared__ uint4 smem[kRingSteps * kStepVec + (7 * 256) / 4];
+    // waits): 3 x 16 KiB weight steps, then biases [5][256], LN weight / bias,
+    // and the weight rows' inverse scales [5][256]
+    __shared__ uint4 smem[3 * kStepVec + (12 * 256) / 4];
     uint4* Wb = smem;
-    float* Bs = reinterpret_cast<float*>(smem + kRingSteps * kStepVec);
+    float* Bs = reinterpret_cast<float*>(smem + 3 * kStepVec);
+    float* Rs = Bs + 7 * 256;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int j = lane & 31, h = lane >> 5;
     const uint32_t ray = blockIdx.x * kRaysV5 + wave * 32u + j;
     const bool live = ray < a.N;
 
-    for (int i = tid; i < 5 * 256; i += 256) Bs[i] = a.b[i >> 8][i & 255];
+    for (int i = tid; i < 5 * 256; i += 256) {
+        Bs[i] = a.b[i >> 8][i & 255];
+        Rs[i] = a.rinv[i];
+    }
     Bs[5 * 256 + tid] = a.ln_w[tid];
     Bs[6 * 256 + tid] = a.ln_b[tid];
 
     // x (head input row) as B operands: k-block kb, lane half h -> columns
-    // 16kb + 8h .. +7; loaded again for the skip layer rather than held in
-    // 88 VGPRs through layer 1
+    // 16kb + 8h .. +7; read again for the skip layer rather than held in 88
+    // VGPRs through layer 1
     const float* xr = a.rows + (size_t)(live ? ray : 0u) * kRowIn;
-    auto load_x = [&](int kb, uint4& xh, uint4& xl) {
-        float v[8];
+    auto x8 = [&](int kb, float (&v)[8]) {
         const int c0 = 16 * kb + 8 * h;
         if (c0 + 8 <= kRowIn) {
             const float4 p = *reinterpret_cast<const float4*>(xr + c0);
@@ -500,97 +437,79 @@ k_sam_head_bf3(HeadArgsB a) {
 #pragma unroll
         for (int m = 0; m < 8; ++m)
             if (!live || c0 + m >= kIn) v[m] = 0.0f;      // column 163 of a row is padding
-        split8(v, xh, xl);
+    };
+    float xmax = 0.0f;                                    // the ray's max |x| (both half-waves)
+#pragma unroll
+    for (int kb = 0; kb < kXkb; ++kb) {
+        float v[8];
+        x8(kb, v);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) xmax = fmaxf(xmax, fabsf(v[m]));
+    }
+    xmax = fmaxf(xmax, __shfl_xor(xmax, 32));
+    auto load_x = [&](float s, uint4 (&xh)[kXkb], uint4 (&xl)[kXkb]) {
+#pragma unroll
+        for (int kb = 0; kb < kXkb; ++kb) {
+            float v[8];
+            x8(kb, v);
+            split8_f16(v, s, xh[kb], xl[kb]);
+        }
     };
     uint4 xh[kXkb], xl[kXkb];
-#pragma unroll
-    for (int kb = 0; kb < kXkb; ++kb) load_x(kb, xh[kb], xl[kb]);
-#if SAMNERF_HEAD_STAGE
-    HeadStager st{a.packed, Wb, tid, lane, 0, {}};
-    st.begin();
-#else
+    Scale2 sc = scale_of_max(xmax);
+    load_x(sc.s, xh, xl);
     HeadStepper st{a.packed, Wb, wave, lane, 0};
     st.issue(0);
     st.issue(1);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");          // step 0 landed
     __syncthreads();
-#endif
-#if SAMNERF_HEAD_LAZY
-    floatx16 accA[8], accB[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) accA[t] = floatx16{};
-#pragma unroll
-    for (int kb = 0; kb < kXkb; ++kb) st.run(accA, xh[kb], xl[kb]);        // layer 0 -> A
-    // one hidden layer from `src` (its pre-activations) into `dst`
-    auto hidden = [&](floatx16 (&src)[8], floatx16 (&dst)[8], const float* bias) {
-        uint4 ch0, cl0, ch1, cl1;
-#pragma unroll
-        for (int kb = 0; kb < kHkb; ++kb) {
-            if ((kb & 1) == 0) epilogue_tile(src[kb >> 1], bias, kb >> 1, h, ch0, cl0, ch1, cl1);
-            if (kb & 1) st.run(dst, ch1, cl1);
-            else st.run(dst, ch0, cl0);
-        }
-    };
-#pragma unroll
-    for (int t = 0; t < 8; ++t) accB[t] = floatx16{};
-    hidden(accA, accB, Bs + 0 * 256);                                      // layer 1 -> B
-#pragma unroll
-    for (int kb = 0; kb < kXkb; ++kb) load_x(kb, xh[kb], xl[kb]);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) accA[t] = floatx16{};
-#pragma unroll
-    for (int kb = 0; kb < kXkb; ++kb) st.run(accA, xh[kb], xl[kb]);       // layer 2: x part -> A
-    hidden(accB, accA, Bs + 1 * 256);                                      //          h part
-#pragma unroll
-    for (int t = 0; t < 8; ++t) accB[t] = floatx16{};
-    hidden(accA, accB, Bs + 2 * 256);                                      // layer 3 -> B
-#pragma unroll
-    for (int t = 0; t < 8; ++t) accA[t] = floatx16{};
-    hidden(accB, accA, Bs + 3 * 256);                                      // layer 4 -> A
-    floatx16 (&acc)[8] = accA;
-#else
+
     floatx16 acc[8];
     uint4 ah[kHkb], al[kHkb];
     auto zero = [&]() {
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] = floatx16{};
     };
+    // the layer's values, then the next layer's B operands at the scale of
+    // their max (and of `extra`, another input of the same layer)
+    auto next = [&](int layer, float extra) {
+        float m = finish_layer(acc, Bs + layer * 256, Rs + layer * 256, sc.inv, h, true);
+        m = fmaxf(fmaxf(m, __shfl_xor(m, 32)), extra);
+        sc = scale_of_max(m);
+        split_layer(acc, sc.s, ah, al);
+    };
 
     zero();                                                   // layer 0: W0 . x
 #pragma unroll
     for (int kb = 0; kb < kXkb; ++kb) st.run(acc, xh[kb], xl[kb]);
-    epilogue(acc, Bs + 0 * 256, h, ah, al);
+    next(0, 0.0f);
     zero();                                                   // layer 1
 #pragma unroll
     for (int kb = 0; kb < kHkb; ++kb) st.run(acc, ah[kb], al[kb]);
-    epilogue(acc, Bs + 1 * 256, h, ah, al);
+    next(1, xmax);                                            // layer 2 reads cat(h, x): one scale
     zero();                                                   // layer 2: W2 . cat(h, x)
-#pragma unroll
-    for (int kb = 0; kb < kXkb; ++kb) load_x(kb, xh[kb], xl[kb]);
+    load_x(sc.s, xh, xl);
 #pragma unroll
     for (int kb = 0; kb < kXkb; ++kb) st.run(acc, xh[kb], xl[kb]);
 #pragma unroll
     for (int kb = 0; kb < kHkb; ++kb) st.run(acc, ah[kb], al[kb]);
-    epilogue(acc, Bs + 2 * 256, h, ah, al);
+    next(2, 0.0f);
     zero();                                                   // layer 3
 #pragma unroll
     for (int kb = 0; kb < kHkb; ++kb) st.run(acc, ah[kb], al[kb]);
-    epilogue(acc, Bs + 3 * 256, h, ah, al);
+    next(3, 0.0f);
     zero();                                                   // layer 4 (no activation)
 #pragma unroll
     for (int kb = 0; kb < kHkb; ++kb) st.run(acc, ah[kb], al[kb]);
-#endif
+    finish_layer(acc, Bs + 4 * 256, Rs + 4 * 256, sc.inv, h, false);
 
-    // + bias, LayerNorm(256, eps=1e-5) per ray: this lane holds 128 of the
-    // ray's units, the other half-wave (lane ^ 32) the rest; sums in double
+    // LayerNorm(256, eps=1e-5) per ray: this lane holds 128 of the ray's
+    // units, the other half-wave (lane ^ 32) the rest; sums in double
     double s = 0.0;
 #pragma unroll
     for (int t = 0; t < 8; ++t)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            acc[t][q] += Bs[4 * 256 + 32 * t + rho(q) + 4 * h];
-            s += (double)acc[t][q];
-        }
+        for (int q = 0; q < 16; ++q) s += (double)acc[t][q];
     s += __shfl_xor(s, 32);
     const double mean = s / 256.0;
     double var = 0.0;
@@ -626,27 +545,29 @@ k_sam_head_bf3(HeadArgsB a) {
 
 size_t sam_head_packed_floats() {
     const size_t f32 = (size_t)8 * kTotalGroups * 64 * 4;
-    const size_t bf3 = (size_t)kSteps * kStepVec * 4;        // uint4 fragments
-    return f32 > bf3 ? f32 : bf3;
+    const size_t h16 = (size_t)kPackedVec * 4 + 5 * 256;     // fragments + row inverse scales
+    return f32 > h16 ? f32 : h16;
 }
 
 int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, float* samvit,
                      float* packed, hipStream_t s) {
-    if (m->head_mode == 0) {                                     // bf16x3 (default)
-        uint4* pk = reinterpret_cast<uint4*>(packed);
-        const uint32_t nfrag = (uint32_t)kSteps * 8u * 64u;
-        k_pack_bf3<<<div_up(nfrag, 256), 256, 0, s>>>(m->sam_w[0], m->sam_w[1], m->sam_w[2],
-                                                      m->sam_w[3], m->sam_w[4], pk);
-        HeadArgsB a;
+    if (m->head_mode == 0) {                                     // f16x3 (default)
+        PackArgs p;
+        for (int i = 0; i < 5; ++i) p.W[i] = m->sam_w[i];
+        p.packed = reinterpret_cast<uint4*>(packed);
+        p.rinv = packed + (size_t)kPackedVec * 4;
+        k_pack_h16<<<5 * 256 / 4, 256, 0, s>>>(p);
+        HeadArgsH a;
         a.rows = rows;
         a.N = N;
-        a.packed = pk;
+        a.packed = p.packed;
+        a.rinv = p.rinv;
         for (int i = 0; i < 5; ++i) a.b[i] = m->sam_b[i];
         a.ln_w = m->ln_w;
         a.ln_b = m->ln_b;
         a.out = samvit;
-        k_sam_head_bf3<<<div_up(N, (uint32_t)kRaysV5), 256, 0, s>>>(a);
-        return check_launch("sam_head_bf3");
+        k_sam_head_h16<<<div_up(N, (uint32_t)kRaysV5), 256, 0, s>>>(a);
+        return check_launch("sam_head_h16");
     }
     const uint32_t nvec = 8u * kTotalGroups * 64u;
     k_pack<<<div_up(nvec, 256), 256, 0, s>>>(m->sam_w[0], m->sam_w[1], m->sam_w[2], m->sam_w[3],
@@ -664,3 +585,29 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
 }
 
 }  // namespace samnerf
+
+extern "C" {
+
+size_t samnerf_sam_head_workspace_size(void) { return samnerf::sam_head_packed_floats() * sizeof(float); }
+
+int samnerf_sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, float* samvit,
+                             void* workspace, size_t workspace_bytes, samnerf_stream_t stream) {
+    using namespace samnerf;
+    if (!m) return fail(SAMNERF_EINVAL, "sam_head_forward: null model");
+    if (!m->with_sam) return fail(SAMNERF_EINVAL, "sam_head_forward: model has no SAM head (with_sam = 0)");
+    for (int i = 0; i < 5; ++i)
+        if (!m->sam_w[i] || !m->sam_b[i]) return fail(SAMNERF_EINVAL, "sam_head_forward: null head weight");
+    if (!m->ln_w || !m->ln_b) return fail(SAMNERF_EINVAL, "sam_head_forward: null LayerNorm weight");
+    if (m->head_mode != 0 && m->head_mode != 1)
+        return fail(SAMNERF_EINVAL, "sam_head_forward: head_mode must be 0 or 1, got %d", m->head_mode);
+    if (N == 0) return SAMNERF_OK;
+    if (!rows || !samvit || !workspace) return fail(SAMNERF_EINVAL, "sam_head_forward: null pointer");
+    const size_t need = samnerf_sam_head_workspace_size();
+    if (workspace_bytes < need)
+        return fail(SAMNERF_EWORKSPACE, "sam_head_forward: workspace needs %zu bytes, got %zu", need,
+                    workspace_bytes);
+    return sam_head_forward(m, rows, N, samvit, static_cast<float*>(workspace),
+                            reinterpret_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

@@ -62,8 +62,9 @@ def perturbed_positions(N, num_steps, device):
 
 
 class FusedRenderer:
-    """head_mode: 0 = bf16x3 split precision for grid_mlp and the SAM head
-    (default), 1 = exact fp32.  t_thresh: 0 (default) = the reference's
+    """head_mode: 0 = f16x3 (each fp32 product of grid_mlp, the SAM head and
+    the mask head as three fp16 MFMA products on power-of-two scaled operands:
+    fp32-equivalent, csrc/f16x3.h; default), 1 = exact fp32 MFMA.  t_thresh: 0 (default) = the reference's
     semantics; > 0 = the flagged non-parity early-exit mode N1 (a wave stops
     marching once every ray's transmittance is below t_thresh; include/
     samnerf_hip.h), also from SAMNERF_T_THRESH."""
@@ -286,6 +287,22 @@ class FusedRenderer:
             out["samvit"] = samvit
         if keep_workspace:
             out["_workspace"] = (ws, need, m, int(m.view_width))
+        return out
+
+    @torch.no_grad()
+    def sam_head(self, rows):
+        """samvit_mlp (SkipConnMLP + LayerNorm, network.py:36-75, :120-123) on
+        head-input rows [N,164] (render(rows=...)'s layout) at this renderer's
+        head_mode -> samvit [N,256] (samnerf_sam_head_forward)."""
+        rows = rows.contiguous().float()
+        assert rows.dim() == 2 and rows.shape[1] == ROW, rows.shape
+        N = rows.shape[0]
+        m = self.model()
+        need = lib().samnerf_sam_head_workspace_size()
+        ws = torch.empty(need, dtype=torch.uint8, device=rows.device)
+        out = torch.empty(N, 256, device=rows.device)
+        check(lib().samnerf_sam_head_forward(ctypes.byref(m), _ptr(rows), N, _ptr(out), _ptr(ws), need,
+                                             _stream(rows)), "sam_head_forward")
         return out
 
     def sgrid_backward(self, grad_rows, workspace, grad_embeddings):

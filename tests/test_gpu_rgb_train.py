@@ -84,6 +84,54 @@ def test_fused_rgb_step_matches_cpu_twin(hip_lib, cuda):
     _compare_grads(gpu, cpu)
 
 
+def _float64_twin_errors(nets_fp32, cpu, ro, rd, gt, global_step=1):
+    """Relative gradient errors of each fp32 network against a float64 twin
+    of the step (tests/oracle_backend.float64_twin: the reference's op
+    sequence in float64 at the fp32 run's own sample positions), the fp32 CPU
+    twin (C oracle encoders) among them."""
+    import copy
+    from oracle_backend import float64_twin, oracle_encoders
+    from samnerf_amd.train import rgb_train_step
+    n64 = copy.deepcopy(cpu).double()
+    rec = []
+    with oracle_encoders(record=rec):
+        _, loss_c, _ = rgb_train_step(cpu, ro, rd, gt, global_step=global_step, perturb=False)
+        loss_c.backward()
+    with float64_twin(grid_inputs=rec):
+        _, loss64, _ = rgb_train_step(n64, ro.double(), rd.double(), gt.double(), global_step=global_step,
+                                      perturb=False)
+        loss64.backward()
+    errs = {}
+    for name, net in list(nets_fp32.items()) + [("cpu_fp32", cpu)]:
+        e = {}
+        for (k, a), (_, b) in zip(net.named_parameters(), n64.named_parameters()):
+            if b.grad is None:
+                continue
+            e[k] = ((a.grad.detach().cpu().double() - b.grad).norm() / b.grad.norm().clamp_min(1e-300)).item()
+        errs[name] = e
+    return errs, float(loss64)
+
+
+def test_fused_rgb_step_vs_float64_twin(hip_lib, cuda):
+    """Every gradient of the HIP training step, the density path's grid /
+    grid_mlp tensors included, is as close to the float64 twin of the step as
+    the fp32 CPU twin is (within 2x, or 1e-5 relative), at the reference's
+    table sizes' small stand-in (grid 2^12, proposal 2^10), perturb off."""
+    from samnerf_amd.train import rgb_train_step_fused
+    gpu, cpu = _rgb_nets(cuda)
+    ro, rd = _rays(16, 6)
+    gt = torch.rand(256, 3, generator=torch.Generator().manual_seed(2))
+    _, loss, _ = rgb_train_step_fused(gpu, ro.to(cuda), rd.to(cuda), gt.to(cuda), global_step=1, perturb=False)
+    errs, loss64 = _float64_twin_errors({"hip": gpu}, cpu, ro, rd, gt)
+    print("relative gradient error vs float64 twin (hip | cpu fp32):")
+    for k in errs["hip"]:
+        print(f"  {k:32s} {errs['hip'][k]:.2e} | {errs['cpu_fp32'][k]:.2e}")
+    assert abs(float(loss) - loss64) <= 2e-6 * abs(loss64)
+    bad = {k: (v, errs["cpu_fp32"][k]) for k, v in errs["hip"].items()
+           if v > max(2.0 * errs["cpu_fp32"][k], 1e-5)}
+    assert not bad, bad
+
+
 def test_fused_rgb_step_matches_torch_path_perturbed(hip_lib, cuda):
     """perturb=True (the reference's training sampling): the fused step and the
     torch path draw the same perturbed positions from the same seed and agree

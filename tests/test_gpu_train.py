@@ -58,7 +58,7 @@ def test_distillation_step_matches_cpu_twin_full_tables(hip_lib, cuda):
     loss (utils.py:1098-1106: bilinear resize + MSE vs an N(0,1) target).
     Loss to fp32 rounding; gradients of s_grid.embeddings and every
     samvit_mlp tensor within 2e-3 relative (norm): float atomics, GPU vs CPU
-    GEMM order, bf16x3 head forward (~1e-5)."""
+    GEMM order, f16x3 grid_mlp forward (fp32-equivalent)."""
     from oracle import renderer as orc
     from oracle_backend import oracle_encoders
     from samnerf_amd.fused import FusedRenderer

@@ -11,7 +11,7 @@ stop_if_fatal() {  # $1 = rc, $2 = step
 python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || { echo BUILD FAIL; tail -30 "$OUT/build.log"; exit 1; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"; stop_if_fatal $rc smoke
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider -rA --timeout 120 --timeout-method thread --durations=25 > "$OUT/pytest_gpu.log" 2>&1; rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error" "$OUT/pytest_gpu.log" | tail -15; stop_if_fatal $rc pytest
+timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -q ${PYTEST_K:+-k "$PYTEST_K"} -p no:cacheprovider -rA --timeout 120 --timeout-method thread --durations=25 > "$OUT/pytest_gpu.log" 2>&1; rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error" "$OUT/pytest_gpu.log" | tail -15; stop_if_fatal $rc pytest
 fi
 timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1; rc=$?; echo "bench rc=$rc"; tail -2 "$OUT/bench.log"; stop_if_fatal $rc bench
 # per-rank loads of an N-GPU strong-scaled 512x512 view: H = 512/N rows
