@@ -43,6 +43,10 @@ enum {
 /* Library identity / diagnostics (host only, no GPU needed). */
 const char* samnerf_version(void);
 const char* samnerf_last_error(void);
+/* 1 in the diagnostic build (libsamnerf_hip_diag.so: the kernels' A/B variant
+ * switches read from SAMNERF_* environment variables, for the bit-identity
+ * tests), 0 in the product library (one path per configuration). */
+int samnerf_diag_variants(void);
 
 /* ------------------------------------------------------------ gridencoder --
  * Replaces grid_encode_forward (gridencoder.h:12, gridencoder.cu:467-490).

@@ -19,6 +19,11 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "samnerf_amd")
 LIB = os.path.join(OUT_DIR, "libsamnerf_hip.so")
 OBJ_DIR = os.path.join(HERE, "build", "obj")
+# the diagnostic build: the same sources with the kernels' A/B variant switches
+# read from the environment (samnerf_common.h diag_env), for the bit-identity
+# tests of the alternative forms; never loaded by the product path
+DIAG_LIB = os.path.join(OUT_DIR, "libsamnerf_hip_diag.so")
+DIAG_OBJ_DIR = os.path.join(HERE, "build", "obj_diag")
 
 SOURCES = ["common.cpp", "grid_encoder.hip", "sh_freq_encoder.hip", "raymarch.hip",
            "sam_head.hip", "tile_codec.hip", "train_optim.hip", "sam_head_train.hip",
@@ -38,32 +43,42 @@ def _newer(src, obj):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src):
-    obj = os.path.join(OBJ_DIR, src + ".o")
+def _compile(src, diag=False):
+    obj = os.path.join(DIAG_OBJ_DIR if diag else OBJ_DIR, src + ".o")
     path = os.path.join(CSRC, src)
     if not _newer(path, obj):
         return obj
-    cmd = [HIPCC] + FLAGS + ["-c", path, "-o", obj]
+    flags = FLAGS + (["-DSAMNERF_DIAG_VARIANTS"] if diag else [])
+    cmd = [HIPCC] + flags + ["-c", path, "-o", obj]
     if src.endswith(".cpp"):
-        cmd = [HIPCC, "-x", "hip"] + FLAGS + ["-c", path, "-o", obj]
+        cmd = [HIPCC, "-x", "hip"] + flags + ["-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr}")
     return obj
 
 
-def build(jobs=None, verbose=True):
-    os.makedirs(OBJ_DIR, exist_ok=True)
-    jobs = jobs or min(len(SOURCES), os.cpu_count() or 4, 8)
-    with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(_compile, SOURCES))
-    if not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB] + objs
+def _link(objs, lib):
+    if not os.path.exists(lib) or any(os.path.getmtime(o) > os.path.getmtime(lib) for o in objs):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
+
+
+def build(jobs=None, verbose=True, diag=True):
+    """The product library, and (diag=True) the diagnostic build beside it."""
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    os.makedirs(DIAG_OBJ_DIR, exist_ok=True)
+    jobs = jobs or min(2 * len(SOURCES), os.cpu_count() or 4, 8)
+    work = [(src, False) for src in SOURCES] + ([(src, True) for src in SOURCES] if diag else [])
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda a: _compile(*a), work))
+    _link(objs[:len(SOURCES)], LIB)
+    if diag:
+        _link(objs[len(SOURCES):], DIAG_LIB)
     if verbose:
-        print(f"[samnerf] built {LIB}")
+        print(f"[samnerf] built {LIB}" + (f" and {os.path.basename(DIAG_LIB)}" if diag else ""))
     return LIB
 
 

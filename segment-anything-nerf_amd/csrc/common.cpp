@@ -61,7 +61,17 @@ LevelDesc make_level(uint32_t off, uint32_t size, uint32_t res, uint32_t gridtyp
 
 extern "C" {
 
-const char* samnerf_version(void) { return "samnerf_hip 0.1 (gfx950)"; }
+const char* samnerf_version(void) { return "samnerf_hip 0.3 (gfx950)"; }
+
+// 1 in the diagnostic build whose kernels read the A/B variant switches from
+// the environment (samnerf_common.h diag_env), 0 in the product library
+int samnerf_diag_variants(void) {
+#ifdef SAMNERF_DIAG_VARIANTS
+    return 1;
+#else
+    return 0;
+#endif
+}
 
 const char* samnerf_last_error(void) { return samnerf::g_err; }
 

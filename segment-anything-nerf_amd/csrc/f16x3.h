@@ -13,14 +13,14 @@
 // fp32 MFMA GEMM, 36x below the bf16 split it replaces).
 //
 // fp16's narrow exponent range (normal from 2^-14, max 65504) is handled by
-// exact power-of-two scaling: every weight ROW is scaled so its largest
-// |w| lies in [2^14, 2^15) (packing time, inverse kept per row), and every
+// exact power-of-two scaling: every weight tensor is scaled so its largest
+// |w| lies in [2^13, 2^14) (packing time, log2 of the scale kept), and every
 // activation COLUMN (one ray or sample) the same way at run time, from the max
 // over the column's K inputs.  Scaling by 2^e commutes with rounding, so the
 // scaled product is the unscaled one times 2^(e_row + e_col) exactly; the
 // consumer multiplies the accumulator by the two inverse scales.  With the
-// column maximum at 2^14, elements down to 2^-28 of it stay normal fp16 and the
-// absolute error floor is 2^-39 of the maximum.
+// column maximum at 2^13, elements down to 2^-27 of it stay normal fp16 and the
+// absolute error floor is 2^-38 of the maximum.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -34,9 +34,11 @@ typedef float f32x2v __attribute__((ext_vector_type(2)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // Power-of-two scale s and its inverse for a column (or row) whose largest
-// magnitude is `maxabs` (>= 0): maxabs * s in [2^14, 2^15).  The exponent is
+// magnitude is `maxabs` (>= 0): maxabs * s in [2^13, 2^14) -- one binade below
+// fp16's top, so values up to 4x the maximum a scale was chosen for still fit
+// (k_final's layer 1 takes its two k-blocks one at a time).  The exponent is
 // clamped so that both s and 1/s are normal floats (all-zero or tiny columns
-// get s = 2^126; inf / NaN columns s = 2^-114 and stay inf / NaN).
+// get s = 2^125; inf / NaN columns s = 2^-115 and stay inf / NaN).
 struct Scale2 {
     float s, inv;
 };
@@ -44,38 +46,59 @@ __host__ __device__ __forceinline__ Scale2 scale_of_max(float maxabs) {
     uint32_t e = __builtin_bit_cast(uint32_t, maxabs) >> 23;          // biased exponent (sign bit clear)
     e = e < 15u ? 15u : (e > 255u ? 255u : e);
     Scale2 r;
-    r.s = __builtin_bit_cast(float, (268u - e) << 23);             // 2^(141 - e)
-    r.inv = __builtin_bit_cast(float, (e - 14u) << 23);             // 2^(e - 141)
+    r.s = __builtin_bit_cast(float, (267u - e) << 23);             // 2^(140 - e)
+    r.inv = __builtin_bit_cast(float, (e - 13u) << 23);             // 2^(e - 140)
     return r;
 }
 
-// The same as an exponent k (s = 2^k, k in [-114, 126]) and 2^k as a float
+// The same as an exponent k (s = 2^k, k in [-115, 125]) and 2^k as a float
 // for any k (clamped to the normal range): scales tracked across layers.
 __device__ __forceinline__ int scale_exp_of_max(float maxabs) {
     uint32_t e = __builtin_bit_cast(uint32_t, maxabs) >> 23;
     e = e < 15u ? 15u : (e > 255u ? 255u : e);
-    return 141 - (int)e;
+    return 140 - (int)e;
 }
 __device__ __forceinline__ float exp2i(int k) {
     k = k < -126 ? -126 : (k > 127 ? 127 : k);
     return __builtin_bit_cast(float, (uint32_t)(k + 127) << 23);
 }
 
-// hi / lo halves of two (already scaled) values, packed as two f16 each
-__device__ __forceinline__ void split_pair_f16(float x, float y, uint32_t& hi, uint32_t& lo) {
-    const f16x2v h = __builtin_convertvector((f32x2v){x, y}, f16x2v);
-    const f32x2v hf = __builtin_convertvector(h, f32x2v);
-    const f16x2v l = __builtin_convertvector((f32x2v){x - hf.x, y - hf.y}, f16x2v);
-    hi = __builtin_bit_cast(uint32_t, h);
-    lo = __builtin_bit_cast(uint32_t, l);
+// hi / lo halves of x * s and y * s (s a power of two, so x * s is exact),
+// packed as two f16 each: hi = f16(x s), lo = f16(x s - hi), each one
+// v_fma_mix (fp32 fma of f32 / f16 sources rounded once to f16): 4
+// instructions per pair where multiply, convert, convert back, subtract and
+// convert took 6.  The same bits as that sequence (x s and x s - hi are exact
+// in fp32, so both round the same value once).
+__device__ __forceinline__ void split_pair_f16(float x, float y, float s, uint32_t& hi, uint32_t& lo) {
+    uint32_t h, l;
+    asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+        "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+        "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(h), "=&v"(l)
+        : "v"(x), "v"(y), "v"(s));
+    hi = h;
+    lo = l;
 }
 
 // 8 values (times the scale s) -> one B (or A) fragment pair
 __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
-    split_pair_f16(v[0] * s, v[1] * s, hi.x, lo.x);
-    split_pair_f16(v[2] * s, v[3] * s, hi.y, lo.y);
-    split_pair_f16(v[4] * s, v[5] * s, hi.z, lo.z);
-    split_pair_f16(v[6] * s, v[7] * s, hi.w, lo.w);
+    split_pair_f16(v[0], v[1], s, hi.x, lo.x);
+    split_pair_f16(v[2], v[3], s, hi.y, lo.y);
+    split_pair_f16(v[4], v[5], s, hi.z, lo.z);
+    split_pair_f16(v[6], v[7], s, hi.w, lo.w);
+}
+
+// running max |a|, |b| into m (one v_max3_f32 with |.| source modifiers)
+__device__ __forceinline__ float max_abs3(float m, float a, float b) {
+    float r;
+    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+// running max of relu(a), relu(b) on the float bits (m >= 0 as int; a
+// negative float is a negative int): one v_max3_i32
+__device__ __forceinline__ int max_relu3(int m, float a, float b) {
+    return max(m, max(__builtin_bit_cast(int, a), __builtin_bit_cast(int, b)));
 }
 
 // C += A.B in f16x3 (small terms first)

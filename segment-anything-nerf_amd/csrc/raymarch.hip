@@ -999,8 +999,9 @@ k_final(FinalArgs a) {
         // takes its two k-blocks one at a time (holding the first block's
         // features through the second gather costs ~50 VGPRs): the running
         // scale is the first block's, lowered -- and the accumulators rescaled
-        // by the same exact power of two -- when the second block's max is
-        // larger.
+        // by the same exact power of two -- when the second block's max needs
+        // a scale two or more binades lower (up to one binade it still fits
+        // fp16 at the first block's scale, f16x3.h).
         int k1 = 0, e_h1 = 0, e_h2 = 0;
 #pragma unroll
         for (int kbi = 0; kbi < 2; ++kbi) {
@@ -1026,12 +1027,13 @@ k_final(FinalArgs a) {
             } else {
                 float m = 0.0f;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(f[e]));
+                for (int e = 0; e < 8; e += 2) m = max_abs3(m, f[e], f[e + 1]);
                 m = fmaxf(m, __shfl_xor(m, 32));
                 const int kk = scale_exp_of_max(m);
                 if (kbi == 0) {
                     k1 = kk;
-                } else if (kk < k1) {                    // lanes of one column agree (both halves)
+                } else if (kk < k1 - 1) {                // (within 2x the first block's max: fits fp16
+                                                         // at its scale); lanes of a column agree
                     const float r = exp2i(kk - k1);
 #pragma unroll
                     for (int q = 0; q < 16; ++q) {
@@ -1058,10 +1060,10 @@ k_final(FinalArgs a) {
         }
         float s2 = 1.0f;
         if constexpr (!EXACT) {                          // max of relu(h1): the raw max, floored at 0
-            float m = 0.0f;
+            int mb = 0;                                  // max of relu(h1) on the float bits
 #pragma unroll
-            for (int i = 0; i < 16; ++i) m = fmaxf(m, fmaxf(h1a[i], h1b[i]));
-            m = fmaxf(m, __shfl_xor(m, 32));
+            for (int i = 0; i < 16; ++i) mb = max_relu3(mb, h1a[i], h1b[i]);
+            const float m = fmaxf(__builtin_bit_cast(float, mb), __shfl_xor(__builtin_bit_cast(float, mb), 32));
             const int k2 = scale_exp_of_max(m);
             s2 = exp2i(k2);
             e_h2 = e_h1 + k2 + ke1;
@@ -1099,10 +1101,10 @@ k_final(FinalArgs a) {
         float s3 = 1.0f;
         int e_o3 = 0;
         if constexpr (!EXACT) {
-            float m = 0.0f;
+            int mb = 0;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) m = fmaxf(m, fmaxf(h2a[i], h2b[i]));
-            m = fmaxf(m, __shfl_xor(m, 32));
+            for (int i = 0; i < 16; ++i) mb = max_relu3(mb, h2a[i], h2b[i]);
+            const float m = fmaxf(__builtin_bit_cast(float, mb), __shfl_xor(__builtin_bit_cast(float, mb), 32));
             const int k3 = scale_exp_of_max(m);
             s3 = exp2i(k3);
             e_o3 = e_h2 + k3 + ke2;
@@ -1836,7 +1838,7 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 // SAMNERF_LOOKUP = packed (default) | ref | box (k_sgrid only; the proposal
 // stages use packed).  Read per call (getenv is cheap next to a launch).
 int lookup_mode() {
-    const char* v = getenv("SAMNERF_LOOKUP");
+    const char* v = diag_env("SAMNERF_LOOKUP");
     if (!v || !*v) return kLookAuto;
     if (!strcmp(v, "ref")) return kLookRef;
     if (!strcmp(v, "box")) return kLookBox4;
@@ -1872,12 +1874,12 @@ constexpr uint32_t kBox4MinRays = 32768;
 // rows): on by default; SAMNERF_FINAL_CLASSES=0 takes the lane-varying form
 // everywhere (same bits: the A/B parity test).
 uint32_t final_classes() {
-    const char* v = getenv("SAMNERF_FINAL_CLASSES");
+    const char* v = diag_env("SAMNERF_FINAL_CLASSES");
     return (v && atoi(v) == 0) ? 0u : 1u;
 }
 
 bool final_prefetch(int seg) {
-    const char* v = getenv("SAMNERF_FINAL_PF");
+    const char* v = diag_env("SAMNERF_FINAL_PF");
     return v ? atoi(v) != 0 : false;
 }
 
@@ -2265,7 +2267,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     // SAMNERF_PROP_FUSED=1: one kernel per proposal stage, ds kept in LDS
     // (k_prop_fused; bit-identical, but measured 1.9x slower -- prop0 1.10 vs
     // 0.59 ms per view -- so the two-kernel form stays the default)
-    const char* pfv = getenv("SAMNERF_PROP_FUSED");
+    const char* pfv = diag_env("SAMNERF_PROP_FUSED");
     const bool pfused = !g_taps_on && look == kLookAuto && pfv && pfv[0] == '1';
     if (pfused) {
         k_prop_fused<128, 65, true><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(pa);
@@ -2363,7 +2365,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     mark_stage(2, s);
     // segments per ray: enough waves to fill the resident slots (2 per SIMD)
     // (SAMNERF_FINAL_S = 1 | 2 | 4 overrides, for measurement)
-    const char* fs = getenv("SAMNERF_FINAL_S");
+    const char* fs = diag_env("SAMNERF_FINAL_S");
     const int seg = fs ? atoi(fs) : (N >= 65536u ? 1 : N >= 32768u ? 2 : 4);
     const bool pf = final_prefetch(seg);
     if (m->sum_after_mlp && (m->t_thresh > 0.0f || sam_rows))
@@ -2476,12 +2478,12 @@ int samnerf_sgrid_backward(const samnerf_model* m, const float* grad_fsam, uint3
     // a wave's 8 neighbouring rays share corner rows at one sample index (the
     // butterfly) more often than consecutive samples of one ray do, and the
     // merge gives the butterfly up.  Kept selectable and tested.
-    const char* mode = getenv("SAMNERF_SGRID_BWD");
+    const char* mode = diag_env("SAMNERF_SGRID_BWD");
     const uint32_t max_cells = (mode && !strcmp(mode, "box")) ? kBwdBoxCells : 0u;
-    const char* rr = getenv("SAMNERF_SGRID_RUN_RES");
+    const char* rr = diag_env("SAMNERF_SGRID_RUN_RES");
     uint32_t run_res = rr ? (uint32_t)atoi(rr) : 0u;
     if (mode && !strcmp(mode, "run") && !rr) run_res = 0xFFFFFFFFu;
-    const char* sp = getenv("SAMNERF_SGRID_BWD_SPLIT");
+    const char* sp = diag_env("SAMNERF_SGRID_BWD_SPLIT");
     const uint32_t split = sp ? (uint32_t)std::max(1, std::min(32, atoi(sp))) : 1u;
     k_sgrid_backward<32><<<dim3(div_up((uint64_t)N * 8, 256), 16, split), 256, 0,
                            reinterpret_cast<hipStream_t>(stream)>>>(N, make_ray_tiles(N, m->view_width),

@@ -522,21 +522,29 @@ __global__ void __launch_bounds__(256) k_rt_final_bwd_ray_h(RtArgs a) {
         a.dout[q] = w * dfi[j];
     }
     if (c_dist != 0.0f) {
-        const float b0 = a.bins2[ks], b1 = a.bins2[ks + N], iv = b1 - b0, m = b0 + iv / 2.0f, wm = w * m;
-        const float Wi = half_incl_scan(w, k), WMi = half_incl_scan(wm, k);
-        const float Wt = __shfl(Wi, 31, 32), WMt = __shfl(WMi, 31, 32);
         // d/dw_k [2 sum_i sum_{j<i} w_i w_j (m_i - m_j) + 1/3 sum_i s_i w_i^2]
-        const float before = m * (Wi - w) - (WMi - wm);
-        const float after = (WMt - WMi) - m * (Wt - Wi);
-        g = __builtin_fmaf(c_dist, 2.0f * (before + after) + (2.0f / 3.0f) * iv * w, g);
+        // = 2 (m_k W_<k - WM_<k + WM_>k - m_k W_>k) + 2/3 s_k w_k: the partial
+        // sums in double (the torch form sums its cumsums in double on the
+        // CPU), and the differences of those nearly equal terms too
+        const float b0 = a.bins2[ks], b1 = a.bins2[ks + N], iv = b1 - b0, m = b0 + iv / 2.0f, wm = w * m;
+        const double wd = (double)w, wmd = (double)wm, md = (double)m;
+        const double Wi = half_incl_scan(wd, k), WMi = half_incl_scan(wmd, k);
+        const double Wt = __shfl(Wi, 31, 32), WMt = __shfl(WMi, 31, 32);
+        const double before = md * (Wi - wd) - (WMi - wmd);
+        const double after = (WMt - WMi) - md * (Wt - Wi);
+        g = __builtin_fmaf(c_dist, (float)(2.0 * (before + after)) + (2.0f / 3.0f) * iv * w, g);
     }
     const bool fin = isfinite(raw);                        // nan_to_num_ backward
     const float dw = fin ? g : 0.0f;
-    const float dr = fin ? dw * raw : 0.0f;
-    const float after_k = half_incl_suffix(dr, k) - dr;    // sum_{j>k} dw_j raw_j
+    // sum_{j>k} dw_j raw_j: the exclusive suffix sum in double (ATen sums the
+    // backward of the compositing cumsum in double on the CPU; in fp32, with
+    // the inclusive sum minus the own term, the cancellation below lost ~1e-2
+    // of the density gradients against a float64 twin)
+    const double drd = fin ? (double)(dw * raw) : 0.0;
+    const double after_k = half_incl_suffix(drd, k) - drd;
     float dx = 0.0f;
     if (!last) {
-        const float dds = dw * (e * Tk) - after_k;
+        const float dds = (float)((double)(dw * (e * Tk)) - after_k);
         const float x = a.out[s];
         dx = (dds * a.delta[s]) * expf(fminf(fmaxf(x, -15.0f), 15.0f));   // trunc_exp backward
     }
@@ -1057,7 +1065,7 @@ constexpr int kRayCh[10] = {32, 31, 32, 32, 3, 3, 32, 32, 4, 6};
 // the leading levels whose rows fit kRepRows (SAMNERF_RT_REP_ROWS overrides it: A/B timing)
 uint32_t rep_rows_cap() {
     static const uint32_t cap = [] {
-        const char* e = std::getenv("SAMNERF_RT_REP_ROWS");
+        const char* e = diag_env("SAMNERF_RT_REP_ROWS");
         return e ? (uint32_t)std::strtoul(e, nullptr, 10) : kRepRows;
     }();
     return cap;

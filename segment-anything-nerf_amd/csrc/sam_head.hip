@@ -208,9 +208,9 @@ __global__ void __launch_bounds__(256) k_sam_head(HeadArgs a) {
 
 // ===================================================================== f16x3
 // fp32-equivalent head (default, f16x3.h): each fp32 product as three fp16
-// MFMA products on power-of-two scaled operands -- weight rows scaled at
-// packing (k_pack_h16, inverse kept per row), each ray's activations at run
-// time from their max over the layer's inputs.  Error against float64 at the
+// MFMA products on power-of-two scaled operands -- each weight tensor scaled
+// at packing (k_head_wmax + k_pack_h16), each ray's activations at run time
+// from their max over the layer's inputs.  Error against float64 at the
 // level of an exact fp32 GEMM (tools/f16x3_error.py), at 3 v_mfma_f32_32x32x16_f16
 // per 16-deep k-block instead of 8 fp32 MFMAs of twice the cycles.
 //
@@ -238,7 +238,7 @@ constexpr int segBase(int seg) {
 constexpr int kSteps = segBase(6);            // 86
 constexpr int kStepVec = 2 * 8 * 64;          // uint4 per step: [hi/lo][tile][lane]
 constexpr int kRaysV5 = 128;                  // 4 waves x 32 rays
-constexpr int kPackedVec = kSteps * kStepVec; // uint4 of fragments; then rinv [5][256] floats
+constexpr int kPackedVec = kSteps * kStepVec; // uint4 of fragments; then kexp [5] ints
 
 __device__ __forceinline__ int rho(int q) { return (q & 3) + 8 * (q >> 2); }
 __device__ __forceinline__ int hidden_unit(int kb, int h, int m) {
@@ -259,47 +259,53 @@ __device__ __forceinline__ float seg_weight(const float* const* W, int seg, int 
     }
 }
 
-// packed[step 86][hi/lo][tile 8][lane 64] (8 f16 = 16 B each), rinv[layer][unit].
-// One wave per (layer, unit) row: the row's max |w| gives its scale, then the
-// lanes write the row's fragments of every step of the layer.
+// packed[step 86][hi/lo][tile 8][lane 64] (8 f16 = 16 B each), then kexp[5]:
+// each weight tensor scaled by the power of two that puts its max |w| in
+// [2^13, 2^14) (f16x3.h), kexp = log2 of that scale.  k_head_wmax finds the
+// five maxima (one workgroup per tensor), k_pack_h16 writes the fragments (one
+// thread per fragment).
 struct PackArgs {
     const float* W[5];
     uint4* packed;
-    float* rinv;
+    int* kexp;
 };
-__global__ void __launch_bounds__(256) k_pack_h16(PackArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int g = blockIdx.x * 4 + (threadIdx.x >> 6);       // (layer, unit)
-    if (g >= 5 * 256) return;
-    const int layer = g >> 8, unit = g & 255;
-    const int kin = kLogicalIn[layer];
-    const float* row = a.W[layer] + (size_t)unit * kin;
+__global__ void __launch_bounds__(1024) k_head_wmax(PackArgs a) {
+    __shared__ float wm[16];
+    const int layer = blockIdx.x, tid = threadIdx.x;
+    const int n = 256 * kLogicalIn[layer];
+    const float* W = a.W[layer];
     float m = 0.0f;
-    for (int k = lane; k < kin; k += 64) m = fmaxf(m, fabsf(row[k]));
-    const Scale2 sc = scale_of_max(wave_max64(m));
-    if (lane == 0) a.rinv[layer * 256 + unit] = sc.inv;
-    const int tile = unit >> 5, j = unit & 31;
-    for (int seg = 0; seg < 6; ++seg) {
-        if (kSegLayer[seg] != layer) continue;
-        for (int f = lane; f < 2 * kSegKb[seg]; f += 64) {
-            const int kb = f >> 1, h = f & 1;
-            float v[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = seg_weight(a.W, seg, kb, h, e, unit);
-            uint4 hi, lo;
-            split8_f16(v, sc.s, hi, lo);
-            const size_t o = (size_t)(segBase(seg) + kb) * kStepVec + tile * 64 + j + 32 * h;
-            a.packed[o] = hi;
-            a.packed[o + 512] = lo;
-        }
+    for (int i = tid; i < n; i += 1024) m = fmaxf(m, fabsf(W[i]));
+    m = wave_max64(m);
+    if ((tid & 63) == 0) wm[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 16; ++w) m = fmaxf(m, wm[w]);
+        a.kexp[layer] = scale_exp_of_max(m);
     }
+}
+__global__ void __launch_bounds__(256) k_pack_h16(PackArgs a) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;   // one (step, tile, lane)
+    if (t >= (uint32_t)kSteps * 8u * 64u) return;
+    const int lane = (int)(t & 63u), tile = (int)((t >> 6) & 7u), step = (int)(t >> 9);
+    int seg = 0;
+    while (seg < 5 && step >= segBase(seg + 1)) ++seg;
+    const int kb = step - segBase(seg);
+    const int j = lane & 31, h = lane >> 5, unit = tile * 32 + j;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = seg_weight(a.W, seg, kb, h, e, unit);
+    uint4 hi, lo;
+    split8_f16(v, exp2i(a.kexp[kSegLayer[seg]]), hi, lo);
+    a.packed[(size_t)step * kStepVec + tile * 64 + lane] = hi;
+    a.packed[(size_t)step * kStepVec + 512 + tile * 64 + lane] = lo;
 }
 
 struct HeadArgsH {
     const float* rows;
     uint32_t N;
     const uint4* packed;
-    const float* rinv;
+    const int* kexp;
     const float* b[5];
     const float* ln_w;
     const float* ln_b;
@@ -361,25 +367,23 @@ struct HeadStepper {
 
 __device__ __forceinline__ float leaky(float x, bool act) { return act && x < 0.0f ? x * 0.01f : x; }
 
-// The accumulators of a layer back to fp32 values in place: unscale (row and
-// column inverse scales: exact), + bias in one rounding, leaky_relu when
+// The accumulators of a layer back to fp32 values in place: times `inv` (the
+// inverse of the column's input scale and of the weight tensor's scale: a
+// power of two, so acc * inv is exact) + bias in one rounding, leaky_relu when
 // `act`; returns this lane's max |value| (the ray's other units are on lane ^ 32).
-__device__ __forceinline__ float finish_layer(floatx16 (&acc)[8], const float* Bs, const float* Rs, float inv,
-                                              int h, bool act) {
+__device__ __forceinline__ float finish_layer(floatx16 (&acc)[8], const float* Bs, float inv, int h, bool act) {
     float m = 0.0f;
 #pragma unroll
     for (int t = 0; t < 8; ++t)
 #pragma unroll
         for (int mm = 0; mm < 4; ++mm) {       // registers 4mm..4mm+3 = units 32t + 8mm + 4h + 0..3
             const float4 bb = *reinterpret_cast<const float4*>(Bs + 32 * t + 8 * mm + 4 * h);
-            const float4 rr = *reinterpret_cast<const float4*>(Rs + 32 * t + 8 * mm + 4 * h);
-            const float b4[4] = {bb.x, bb.y, bb.z, bb.w}, r4[4] = {rr.x, rr.y, rr.z, rr.w};
+            const float b4[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float v = leaky(__builtin_fmaf(acc[t][4 * mm + e] * r4[e], inv, b4[e]), act);
-                acc[t][4 * mm + e] = v;
-                m = fmaxf(m, fabsf(v));
-            }
+            for (int e = 0; e < 4; ++e)
+                acc[t][4 * mm + e] = leaky(__builtin_fmaf(acc[t][4 * mm + e], inv, b4[e]), act);
+#pragma unroll
+            for (int e = 0; e < 4; e += 2) m = max_abs3(m, acc[t][4 * mm + e], acc[t][4 * mm + e + 1]);
         }
     return m;
 }
@@ -402,20 +406,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 k_sam_head_h16(HeadArgsH a) {
     // one LDS object (a second __shared__ object can de-pipeline the DMA
     // waits): 3 x 16 KiB weight steps, then biases [5][256], LN weight / bias,
-    // and the weight rows' inverse scales [5][256]
-    __shared__ uint4 smem[3 * kStepVec + (12 * 256) / 4];
+    // the weight tensors' inverse scales [5]
+    __shared__ uint4 smem[3 * kStepVec + (7 * 256 + 8) / 4];
     uint4* Wb = smem;
     float* Bs = reinterpret_cast<float*>(smem + 3 * kStepVec);
-    float* Rs = Bs + 7 * 256;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int j = lane & 31, h = lane >> 5;
     const uint32_t ray = blockIdx.x * kRaysV5 + wave * 32u + j;
     const bool live = ray < a.N;
 
-    for (int i = tid; i < 5 * 256; i += 256) {
-        Bs[i] = a.b[i >> 8][i & 255];
-        Rs[i] = a.rinv[i];
-    }
+    for (int i = tid; i < 5 * 256; i += 256) Bs[i] = a.b[i >> 8][i & 255];
+    float* const Wi = Bs + 7 * 256;                       // 2^-kexp[l]
+    if (tid < 5) Wi[tid] = exp2i(-a.kexp[tid]);
     Bs[5 * 256 + tid] = a.ln_w[tid];
     Bs[6 * 256 + tid] = a.ln_b[tid];
 
@@ -473,7 +475,7 @@ k_sam_head_h16(HeadArgsH a) {
     // the layer's values, then the next layer's B operands at the scale of
     // their max (and of `extra`, another input of the same layer)
     auto next = [&](int layer, float extra) {
-        float m = finish_layer(acc, Bs + layer * 256, Rs + layer * 256, sc.inv, h, true);
+        float m = finish_layer(acc, Bs + layer * 256, sc.inv * Wi[layer], h, true);
         m = fmaxf(fmaxf(m, __shfl_xor(m, 32)), extra);
         sc = scale_of_max(m);
         split_layer(acc, sc.s, ah, al);
@@ -501,7 +503,7 @@ k_sam_head_h16(HeadArgsH a) {
     zero();                                                   // layer 4 (no activation)
 #pragma unroll
     for (int kb = 0; kb < kHkb; ++kb) st.run(acc, ah[kb], al[kb]);
-    finish_layer(acc, Bs + 4 * 256, Rs + 4 * 256, sc.inv, h, false);
+    finish_layer(acc, Bs + 4 * 256, sc.inv * Wi[4], h, false);
 
     // LayerNorm(256, eps=1e-5) per ray: this lane holds 128 of the ray's
     // units, the other half-wave (lane ^ 32) the rest; sums in double
@@ -545,7 +547,7 @@ k_sam_head_h16(HeadArgsH a) {
 
 size_t sam_head_packed_floats() {
     const size_t f32 = (size_t)8 * kTotalGroups * 64 * 4;
-    const size_t h16 = (size_t)kPackedVec * 4 + 5 * 256;     // fragments + row inverse scales
+    const size_t h16 = (size_t)kPackedVec * 4 + 8;           // fragments + the tensors' log2 scales
     return f32 > h16 ? f32 : h16;
 }
 
@@ -555,13 +557,14 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         PackArgs p;
         for (int i = 0; i < 5; ++i) p.W[i] = m->sam_w[i];
         p.packed = reinterpret_cast<uint4*>(packed);
-        p.rinv = packed + (size_t)kPackedVec * 4;
-        k_pack_h16<<<5 * 256 / 4, 256, 0, s>>>(p);
+        p.kexp = reinterpret_cast<int*>(packed + (size_t)kPackedVec * 4);
+        k_head_wmax<<<5, 1024, 0, s>>>(p);
+        k_pack_h16<<<div_up((uint32_t)kSteps * 8u * 64u, 256), 256, 0, s>>>(p);
         HeadArgsH a;
         a.rows = rows;
         a.N = N;
         a.packed = p.packed;
-        a.rinv = p.rinv;
+        a.kexp = p.kexp;
         for (int i = 0; i < 5; ++i) a.b[i] = m->sam_b[i];
         a.ln_w = m->ln_w;
         a.ln_b = m->ln_b;

@@ -9,12 +9,27 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "../../include/samnerf_hip.h"
 
 namespace samnerf {
 
 int fail(int code, const char* fmt, ...);
+
+// A/B variant switches of the kernels (the bit-identity tests' alternative
+// forms and the measured-slower variants): read from the environment only in
+// the diagnostic build (-DSAMNERF_DIAG_VARIANTS, libsamnerf_hip_diag.so, which
+// build.py makes beside the product library for the tests).  The product
+// library ignores the environment: one path per configuration.
+inline const char* diag_env(const char* name) {
+#ifdef SAMNERF_DIAG_VARIANTS
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
 int check_launch(const char* what);
 
 inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }

@@ -128,6 +128,11 @@ class NeRFRenderer(nn.Module):
         self.register_buffer("aabb_infer", box.clone())
         self.fused = True          # fused HIP pipeline for eligible calls
         self._fused = None
+        # fused path: GEMM precision (0 = f16x3, fp32-equivalent; 1 = exact fp32
+        # MFMA) and the flagged non-parity early exit N1 (0 = off, the
+        # reference's semantics); read by samnerf_amd.fused.FusedRenderer
+        self.head_mode = 0
+        self.t_thresh = 0.0
 
     def forward(self, x, d, **kwargs):
         raise NotImplementedError()

@@ -3,12 +3,13 @@
 The product path has no fallback: if the HIP library is missing or cannot be
 loaded, every op raises SamnerfUnavailable with the build command.
 """
+import contextlib
 import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SAMNERF_LIB: another build of the same library (A/B timing of two builds in
-# one GPU session, tools/gpu_ab.sh); the in-tree build otherwise.
+# one GPU session); the in-tree build otherwise.
 LIB_PATH = os.environ.get("SAMNERF_LIB") or os.path.join(_HERE, "libsamnerf_hip.so")
 
 _u32 = ctypes.c_uint32
@@ -42,6 +43,7 @@ class SamnerfModel(ctypes.Structure):
 
 
 _SIGS = {
+    "samnerf_diag_variants": ([], _int),
     "samnerf_version": ([], ctypes.c_char_p),
     "samnerf_last_error": ([], ctypes.c_char_p),
     "samnerf_grid_encode_forward": ([_vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _f32, _u32,
@@ -119,26 +121,52 @@ EXPORTED = tuple(_SIGS)
 _lib = None
 
 
+def _load(path, lenient=False):
+    if not os.path.exists(path):
+        raise SamnerfUnavailable(
+            f"{path} is not built; run `python segment-anything-nerf_amd/build.py` "
+            "(or __graft_entry__.build()).  There is no CPU fallback.")
+    try:
+        L = ctypes.CDLL(path)
+    except OSError as e:
+        raise SamnerfUnavailable(f"cannot load {path}: {e}") from e
+    for name, (args, res) in _SIGS.items():
+        if lenient and not hasattr(L, name):
+            continue                  # an older diagnostic build (tools/diag) lacks newer entry points
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    return L
+
+
 def lib():
     """Load the HIP library (once).  Raises SamnerfUnavailable if absent."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise SamnerfUnavailable(
-                f"{LIB_PATH} is not built; run `python segment-anything-nerf_amd/build.py` "
-                "(or __graft_entry__.build()).  There is no CPU fallback.")
-        try:
-            L = ctypes.CDLL(LIB_PATH)
-        except OSError as e:
-            raise SamnerfUnavailable(f"cannot load {LIB_PATH}: {e}") from e
-        for name, (args, res) in _SIGS.items():
-            if os.environ.get("SAMNERF_LIB") and not hasattr(L, name):
-                continue              # an older diagnostic build (tools/diag) lacks newer entry points
-            f = getattr(L, name)
-            f.argtypes = args
-            f.restype = res
-        _lib = L
+        _lib = _load(LIB_PATH, lenient=bool(os.environ.get("SAMNERF_LIB")))
     return _lib
+
+
+DIAG_LIB_PATH = os.path.join(_HERE, "libsamnerf_hip_diag.so")
+_diag = None
+
+
+@contextlib.contextmanager
+def diag_library():
+    """Tests only: route every call of this thread's renders through the
+    diagnostic build (libsamnerf_hip_diag.so), whose kernels read the A/B
+    variant switches (SAMNERF_LOOKUP, SAMNERF_FINAL_S, ...) from the
+    environment -- the product library has one path per configuration."""
+    global _lib, _diag
+    if _diag is None:
+        _diag = _load(DIAG_LIB_PATH)
+        assert _diag.samnerf_diag_variants() == 1
+    prev = lib()
+    _lib = _diag
+    try:
+        yield _diag
+    finally:
+        _lib = prev
 
 
 def check(rc, what):

@@ -67,19 +67,29 @@ class FusedRenderer:
     fp32-equivalent, csrc/f16x3.h; default), 1 = exact fp32 MFMA.  t_thresh: 0 (default) = the reference's
     semantics; > 0 = the flagged non-parity early-exit mode N1 (a wave stops
     marching once every ray's transmittance is below t_thresh; include/
-    samnerf_hip.h), also from SAMNERF_T_THRESH."""
+    samnerf_hip.h).  Unset, both follow the network's head_mode / t_thresh
+    attributes (NeRFRenderer, defaults 0)."""
 
     def __init__(self, net, head_mode=None, t_thresh=None):
-        import os
         self.net = net
         self._ws = None
         self._keep = []
         self._model = None
         self._model_key_cached = None
-        self.head_mode = int(os.environ.get("SAMNERF_HEAD_MODE", "0")) if head_mode is None else head_mode
-        self.t_thresh = float(os.environ.get("SAMNERF_T_THRESH", "0")) if t_thresh is None else float(t_thresh)
+        self._head_mode = head_mode
+        self._t_thresh = None if t_thresh is None else float(t_thresh)
         if not 0.0 <= self.t_thresh < 1.0:
             raise ValueError(f"t_thresh {self.t_thresh} outside [0, 1)")
+
+    # explicit arguments win; otherwise the network's attributes (NeRFRenderer.
+    # head_mode / t_thresh, defaults 0): no environment variable changes the path
+    @property
+    def head_mode(self):
+        return int(self._head_mode if self._head_mode is not None else getattr(self.net, "head_mode", 0))
+
+    @property
+    def t_thresh(self):
+        return float(self._t_thresh if self._t_thresh is not None else getattr(self.net, "t_thresh", 0.0))
 
     # --------------------------------------------------------------- model --
     def _grid(self, enc, name):
@@ -395,13 +405,12 @@ def render_sam_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None,
     """Differentiable SAM-feature render for the distillation step
     (nerf/utils.py:1098-1099): returns samvit [N,256] with autograd to
     s_grid.embeddings (HIP scatter) and samvit_mlp (HIP head forward +
-    backward, sam_head_train.hip; head="torch" or SAMNERF_TRAIN_HEAD=torch runs
+    backward, sam_head_train.hip; head="torch" runs
     the head as torch ops instead, for comparison)."""
-    import os
     net = renderer.net
     rows, image, depth, wsum = _FusedSamRows.apply(net.s_grid.embeddings, renderer, rays_o,
                                                     rays_d, cam_near_far, bg_color, view_width)
-    head = head or os.environ.get("SAMNERF_TRAIN_HEAD", "hip")
+    head = head or "hip"
     if head == "torch":
         samvit = net.samvit_mlp(rows[:, :163])
     else:

@@ -41,3 +41,13 @@ def cuda():
     import torch
     assert torch.cuda.is_available(), "GPU tests need an MI355X (run under gpurun)"
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def diag(hip_lib):
+    """The test runs on the diagnostic build (libsamnerf_hip_diag.so), whose
+    kernels take the A/B variant switches from SAMNERF_* environment
+    variables; the product library ignores them."""
+    from samnerf_amd._lib import diag_library
+    with diag_library() as L:
+        yield L

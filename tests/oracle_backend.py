@@ -195,3 +195,30 @@ def float64_twin(grid_inputs=None):
         _REPLAY[:] = []
         g.grid_encode, s.sh_encode, nw.trunc_exp = old[:3]
         torch.set_default_dtype(old[3])
+
+
+@contextlib.contextmanager
+def injected_bins(bins):
+    """The renderer's resampled bins (sample_pdf's outputs of the proposal
+    stages, in call order) replaced by the given tensors -- e.g. those the HIP
+    kernels computed (FusedRenderer.render(taps=True)) -- so that a CPU twin
+    evaluates the step at the HIP path's own sample positions.  The injected
+    bins must agree with what the twin computes to 1e-5 (a different pdf
+    walk would not be the same step)."""
+    import nerf.renderer as rr
+    old = rr.sample_pdf
+    queue = list(bins)
+
+    def fake(b, w, T, perturb=False):
+        mine = old(b, w, T, perturb)
+        inj = queue.pop(0).to(dtype=mine.dtype, device=mine.device).contiguous()
+        assert inj.shape == mine.shape, (inj.shape, mine.shape)
+        drift = (inj - mine).abs().max().item()
+        assert drift < 1e-5, f"injected bins differ from the twin's by {drift}"
+        return inj
+    rr.sample_pdf = fake
+    try:
+        yield
+        assert not queue, f"{len(queue)} injected bins not used"
+    finally:
+        rr.sample_pdf = old

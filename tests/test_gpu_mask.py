@@ -63,10 +63,10 @@ def test_fused_mask_head_matches_reference_golden(hip_lib, cuda, monkeypatch, na
     the sum_after_mlp fixture: the view MLP per sample) + k_mask_head
     (mask_head.hip) and matches the reference's own golden within 1e-3, in
     both precision modes."""
-    monkeypatch.setenv("SAMNERF_HEAD_MODE", str(head_mode))
     fx = np.load(os.path.join(GOLDEN, name + ".npz"))
     spec = spec_from_fixture(fx)
     net = make_net(spec, fixture_params(fx, spec), cuda)
+    net.head_mode = head_mode                        # the fused path's GEMM precision
     ro = torch.from_numpy(fx["rays_o"]).to(cuda)
     rd = torch.from_numpy(fx["rays_d"]).to(cuda)
     with torch.no_grad():
@@ -103,7 +103,7 @@ def test_fused_mask_head_matches_unfused_path(hip_lib, cuda, head_mode):
     assert torch.equal(got, tiled)
 
 
-def test_fused_sum_after_mlp_rgb_matches_unfused(hip_lib, cuda, monkeypatch):
+def test_fused_sum_after_mlp_rgb_matches_unfused(hip_lib, cuda, monkeypatch, diag):
     """--sum_after_mlp on an RGB model (image = sigmoid(sum_k w_k
     view_mlp(colour_k)), renderer.py:339-342) on the fused k_final<SA> against
     the unfused op sequence, all segment forms (S = 1 / 2 / 4 by ray count)."""

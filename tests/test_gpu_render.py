@@ -97,12 +97,12 @@ def test_fused_render_matches_reference_golden(hip_lib, cuda, monkeypatch, name,
     """Both precision modes against the reference's own outputs: head_mode 0
     (grid_mlp, SAM head on f16x3 MFMA) and 1 (every GEMM on
     exact fp32 MFMA)."""
-    monkeypatch.setenv("SAMNERF_HEAD_MODE", str(head_mode))
     fx = np.load(os.path.join(GOLDEN, name + ".npz"))
     spec = spec_from_fixture(fx)
     params = synth.make_params(spec, seed=int(fx["seed"]), emb_scale=float(fx["emb_scale"]),
                                ln_jitter=float(fx["ln_jitter"]))
     net = make_net(spec, params, cuda)
+    net.head_mode = head_mode                        # the fused path's GEMM precision
     ro = torch.from_numpy(fx["rays_o"]).to(cuda)
     rd = torch.from_numpy(fx["rays_d"]).to(cuda)
     H, W = int(fx["H"]), int(fx["W"])
@@ -274,7 +274,7 @@ def test_exact_fp32_mode_vs_oracle(hip_lib, cuda):
 
 
 @pytest.mark.parametrize("mode", ["ref", "box4"])
-def test_gather_variants_bit_identical(hip_lib, cuda, monkeypatch, mode):
+def test_gather_variants_bit_identical(hip_lib, cuda, monkeypatch, mode, diag):
     """The packed-FMA gathers (default), the per-corner scalar form (ref) and
     the LDS box gathers of k_sgrid_box4 (box4) read the same rows with the same
     weights in the same FMA order: every output bit must agree, including
@@ -356,7 +356,7 @@ def test_sam_feature_handoff_stays_on_device(hip_lib, cuda):
 
 @pytest.mark.parametrize("head_mode", [0, 1])
 @pytest.mark.parametrize("n", [70000, 40000, 9000])
-def test_final_prefetch_bit_identical(hip_lib, cuda, monkeypatch, n, head_mode):
+def test_final_prefetch_bit_identical(hip_lib, cuda, monkeypatch, n, head_mode, diag):
     """k_final with and without the cross-sample prefetch of its first
     k-block's gathers (SAMNERF_FINAL_PF), for each ray-segment form S = 1, 2,
     4 (chosen by N): identical bits."""
@@ -415,7 +415,7 @@ def test_fused_ragged_ray_counts(hip_lib, cuda, n):
 
 
 @pytest.mark.parametrize("n", [70000, 9000])
-def test_final_slot_classes_bit_identical(hip_lib, cuda, monkeypatch, n):
+def test_final_slot_classes_bit_identical(hip_lib, cuda, monkeypatch, n, diag):
     """k_final's wave-uniform slot paths -- one 16-B load per x-adjacent corner
     pair on dense levels (with the top-cell weight swap) and select-free
     hashed rows -- against the lane-varying form (SAMNERF_FINAL_CLASSES=0):
@@ -502,7 +502,7 @@ def test_ray_tiling_bit_identical(hip_lib, cuda, surface):
         assert torch.equal(outs[0][k][:H * W - 2 * W], outs[2][k]), k
 
 
-def test_fused_proposal_kernel_bit_identical(hip_lib, cuda, monkeypatch):
+def test_fused_proposal_kernel_bit_identical(hip_lib, cuda, monkeypatch, diag):
     """k_prop_fused (ds kept in LDS, one kernel per proposal stage; the
     SAMNERF_PROP_FUSED=1 variant, measured slower) against the default
     two-kernel form k_prop_sigma + k_prop_pdf: every output, head rows
@@ -536,7 +536,7 @@ def _twice_equal(render):
 @pytest.mark.parametrize("seg", ["1", "2", "4"])
 @pytest.mark.parametrize("pf", ["0", "1"])
 @pytest.mark.parametrize("head_mode", [0, 1])
-def test_final_forms_deterministic(hip_lib, cuda, monkeypatch, seg, pf, head_mode):
+def test_final_forms_deterministic(hip_lib, cuda, monkeypatch, seg, pf, head_mode, diag):
     """Every k_final form renders the same bits twice (a forward
     whose output varies run to run has a hazard): S = 1 / 2 / 4, with and
     without the cross-sample prefetch, both precisions, feature rows on."""

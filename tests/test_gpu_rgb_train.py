@@ -12,6 +12,8 @@ test_gpu_train.py's RGB test states them -- the density path's gradients are
 small sums of cancelling terms, so fp32 reassociation moves them ~1e-2
 relative (cosine > 0.9999 kept), every other tensor within 2e-3.
 """
+import contextlib
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -84,20 +86,24 @@ def test_fused_rgb_step_matches_cpu_twin(hip_lib, cuda):
     _compare_grads(gpu, cpu)
 
 
-def _float64_twin_errors(nets_fp32, cpu, ro, rd, gt, global_step=1):
+def _float64_twin_errors(nets_fp32, cpu, ro, rd, gt, global_step=1, bins=None):
     """Relative gradient errors of each fp32 network against a float64 twin
     of the step (tests/oracle_backend.float64_twin: the reference's op
     sequence in float64 at the fp32 run's own sample positions), the fp32 CPU
-    twin (C oracle encoders) among them."""
+    twin (C oracle encoders) among them.  bins: the proposal stages'
+    resampled bins to evaluate the step at (injected_bins), e.g. the HIP
+    path's -- the grid / grid_mlp gradients move ~1e-2 when the final sample
+    positions move by one ulp (fine levels: a cell is ~2^-12 of the range),
+    so the twins must sample where the kernels did."""
     import copy
-    from oracle_backend import float64_twin, oracle_encoders
+    from oracle_backend import float64_twin, injected_bins, oracle_encoders
     from samnerf_amd.train import rgb_train_step
     n64 = copy.deepcopy(cpu).double()
     rec = []
-    with oracle_encoders(record=rec):
+    with oracle_encoders(record=rec), injected_bins(bins or []) if bins else contextlib.nullcontext():
         _, loss_c, _ = rgb_train_step(cpu, ro, rd, gt, global_step=global_step, perturb=False)
         loss_c.backward()
-    with float64_twin(grid_inputs=rec):
+    with float64_twin(grid_inputs=rec), injected_bins(bins or []) if bins else contextlib.nullcontext():
         _, loss64, _ = rgb_train_step(n64, ro.double(), rd.double(), gt.double(), global_step=global_step,
                                       perturb=False)
         loss64.backward()
@@ -112,17 +118,28 @@ def _float64_twin_errors(nets_fp32, cpu, ro, rd, gt, global_step=1):
     return errs, float(loss64)
 
 
-def test_fused_rgb_step_vs_float64_twin(hip_lib, cuda):
+@pytest.mark.parametrize("lam", [(1.0, 0.02, 0.0), (1.0, 0.0, 0.0), (0.0, 0.0, 0.0), (1.0, 0.02, 1e-3)],
+                         ids=["default", "no_distort", "mse_only", "entropy"])
+def test_fused_rgb_step_vs_float64_twin(hip_lib, cuda, lam):
     """Every gradient of the HIP training step, the density path's grid /
     grid_mlp tensors included, is as close to the float64 twin of the step as
     the fp32 CPU twin is (within 2x, or 1e-5 relative), at the reference's
-    table sizes' small stand-in (grid 2^12, proposal 2^10), perturb off."""
+    table sizes' small stand-in (grid 2^12, proposal 2^10), perturb off; with
+    the default loss weights (lambda_proposal 1, lambda_distort 0.02), without
+    the distortion term, MSE alone, and with the entropy term."""
+    from samnerf_amd.fused import FusedRenderer
     from samnerf_amd.train import rgb_train_step_fused
     gpu, cpu = _rgb_nets(cuda)
+    for n in (gpu, cpu):
+        n.opt.lambda_proposal, n.opt.lambda_distort, n.opt.lambda_entropy = lam
     ro, rd = _rays(16, 6)
     gt = torch.rand(256, 3, generator=torch.Generator().manual_seed(2))
+    # the bins the HIP proposal kernels resample (the step runs the same
+    # kernels, proposal_forward): read through the render's parity taps
+    taps = FusedRenderer(gpu).render(ro.to(cuda), rd.to(cuda), taps=True)
+    bins = [taps["bins1"].cpu().contiguous(), taps["bins2"].cpu().contiguous()]
     _, loss, _ = rgb_train_step_fused(gpu, ro.to(cuda), rd.to(cuda), gt.to(cuda), global_step=1, perturb=False)
-    errs, loss64 = _float64_twin_errors({"hip": gpu}, cpu, ro, rd, gt)
+    errs, loss64 = _float64_twin_errors({"hip": gpu}, cpu, ro, rd, gt, bins=bins)
     print("relative gradient error vs float64 twin (hip | cpu fp32):")
     for k in errs["hip"]:
         print(f"  {k:32s} {errs['hip'][k]:.2e} | {errs['cpu_fp32'][k]:.2e}")

@@ -93,7 +93,7 @@ def test_distillation_step_matches_cpu_twin_full_tables(hip_lib, cuda):
     assert len(errs) == 13 and max(errs.values()) < 2e-3, errs
 
 
-def test_sgrid_backward_box_matches_per_corner(hip_lib, cuda, monkeypatch):
+def test_sgrid_backward_box_matches_per_corner(hip_lib, cuda, monkeypatch, diag):
     """The s_grid scatter's LDS-box aggregation (SAMNERF_SGRID_BWD=box; per
     wave and sample: corner sums in LDS, non-zero cells compacted, one atomic
     per distinct row) and the along-ray merge (SAMNERF_SGRID_BWD=run: a lane

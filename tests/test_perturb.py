@@ -69,12 +69,11 @@ def test_perturbed_positions_draw_like_the_reference():
 @pytest.mark.parametrize("head_mode", [0, 1])
 def test_fused_perturbed_matches_reference_golden(hip_lib, cuda, monkeypatch, head_mode):
     from samnerf_amd.fused import FusedRenderer
-    monkeypatch.setenv("SAMNERF_HEAD_MODE", str(head_mode))
     fx, spec, params, draws = _fixture()
     net = make_net(spec, params, cuda)
     ro = torch.from_numpy(fx["rays_o"]).to(cuda)
     rd = torch.from_numpy(fx["rays_d"]).to(cuda)
-    out = FusedRenderer(net).render(ro, rd, perturb=tuple(d.to(cuda) for d in draws))
+    out = FusedRenderer(net, head_mode=head_mode).render(ro, rd, perturb=tuple(d.to(cuda) for d in draws))
     errs = {k: (out[k].cpu() - torch.from_numpy(fx[k])).abs().max().item()
             for k in ("image", "depth", "weights_sum", "samvit")}
     print("perturbed golden", head_mode, errs)

@@ -13,7 +13,12 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
 timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -q ${PYTEST_K:+-k "$PYTEST_K"} -p no:cacheprovider -rA --timeout 120 --timeout-method thread --durations=25 > "$OUT/pytest_gpu.log" 2>&1; rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error" "$OUT/pytest_gpu.log" | tail -15; stop_if_fatal $rc pytest
 fi
+if [ "${RUN_TA:-0}" = "1" ]; then
+timeout -k 10 120 tools/bin/ta_rate > "$OUT/ta_rate.json" 2> "$OUT/ta_rate.err"; rc=$?; echo "ta_rate rc=$rc"; cat "$OUT/ta_rate.json"; stop_if_fatal $rc ta_rate
+fi
+if [ "${SKIP_BENCH:-0}" != "1" ]; then
 timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1; rc=$?; echo "bench rc=$rc"; tail -2 "$OUT/bench.log"; stop_if_fatal $rc bench
+fi
 # per-rank loads of an N-GPU strong-scaled 512x512 view: H = 512/N rows
 for h in ${SWEEP_H:-}; do
 timeout -k 10 200 python bench.py --H $h --cpu-rays 0 --steps 20 > "$OUT/bench_h$h.log" 2>&1; rc=$?; echo "bench H=$h rc=$rc"; tail -1 "$OUT/bench_h$h.log" | python -c "import json,sys; r=json.loads(sys.stdin.read()); print(r['value'], r['ms_per_step'], {k: round(v,3) for k,v in r['stage_ms'].items()})"; stop_if_fatal $rc bench_h$h

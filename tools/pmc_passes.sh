@@ -1,6 +1,6 @@
 #!/bin/bash
-# rocprofv3 PMC passes for the round-2 rooflines (one counter group per pass,
-# counters only, no tracing domains).  usage (GPU box): bash tools/pmc_r2.sh TAG [bench args]
+# rocprofv3 PMC passes for the rooflines (one counter group per pass,
+# counters only, no tracing domains).  usage (GPU box): bash tools/pmc_passes.sh TAG [bench args]
 set -o pipefail
 TAG=${1:-r2}; shift
 OUT="$GRAFT_REPO_ROOT/gpurun_out/pmc_$TAG"
