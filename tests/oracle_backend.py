@@ -222,3 +222,21 @@ def injected_bins(bins):
         assert not queue, f"{len(queue)} injected bins not used"
     finally:
         rr.sample_pdf = old
+
+
+@contextlib.contextmanager
+def recorded_bins(store):
+    """Keep the renderer's resampled bins (sample_pdf outputs, call order) in
+    `store` -- to inject them into another run (injected_bins)."""
+    import nerf.renderer as rr
+    old = rr.sample_pdf
+
+    def rec(*a, **k):
+        out = old(*a, **k)
+        store.append(out.detach().clone())
+        return out
+    rr.sample_pdf = rec
+    try:
+        yield store
+    finally:
+        rr.sample_pdf = old

@@ -1,16 +1,21 @@
 """The RGB training step on the HIP training kernels (samnerf_rgb_train_step,
 csrc/rgb_train.hip; SURVEY.md 8f-2, nerf/utils.py:897-937).
 
-Checked against two references of the same step:
+Checked against:
   * the CPU twin -- the reference's op sequence (run_torch) with autograd on
     the CPU and the C oracle's encoders (tests/oracle_backend.py), perturb off;
   * the torch path on the GPU (run_torch + autograd with the drop-in encoder
-    kernels) with perturb on, both drawing the perturbed positions from the
-    same generator state.
-Tolerances: the loss terms to fp32 rounding; gradients per tensor as
-test_gpu_train.py's RGB test states them -- the density path's gradients are
-small sums of cancelling terms, so fp32 reassociation moves them ~1e-2
-relative (cosine > 0.9999 kept), every other tensor within 2e-3.
+    kernels) with perturb on, both drawing the same perturbed positions;
+  * a float64 twin of the step (oracle_backend.float64_twin).
+Every comparison evaluates the reference at the HIP path's own resampled bins
+(oracle_backend.injected_bins, the bins read through the render's parity
+taps; they agree with the reference's own to ~1e-7): the proposal MLPs sum in
+another order than torch's GEMMs, the bins then differ by an ulp, and an ulp
+of a final sample position moves the grid / grid_mlp gradients by ~1e-2
+(fine levels resolve 2^-12 of the range) -- a real difference of the sampled
+function, not arithmetic error.  At the same bins: every gradient within
+GRAD_TOL of the reference (float atomics, reassociated sums), and within 2x
+of the fp32 CPU twin's own distance to the float64 twin.
 """
 import contextlib
 
@@ -45,22 +50,37 @@ def _rays(n_side, rot, cuda=None):
     return ro, rd
 
 
-def _compare_grads(net_a, net_b, strict=2e-3, loose=2e-2):
+GRAD_TOL = 3e-4          # relative, per tensor (the proposal loss's fp32 sums: ~1e-4 each side)
+
+
+def _compare_grads(net_a, net_b, tol=GRAD_TOL):
     worst = {}
     for (k, pa), (_, pb) in zip(net_a.named_parameters(), net_b.named_parameters()):
         if pb.grad is None:
             assert pa.grad is None, k
             continue
         a, b = pa.grad.detach().cpu(), pb.grad.detach().cpu()
-        err = float((a - b).norm() / b.norm().clamp_min(1e-12))
-        worst[k] = err
-        if k.startswith("grid.") or k.startswith("grid_mlp."):
-            cos = float(F.cosine_similarity(a.flatten(), b.flatten(), dim=0))
-            assert err < loose and cos > 0.9999, (k, err, cos)
-        else:
-            assert err < strict, (k, err)
+        worst[k] = float((a - b).norm() / b.norm().clamp_min(1e-12))
     print("relative gradient errors:", {k: f"{v:.1e}" for k, v in worst.items()})
+    bad = {k: v for k, v in worst.items() if v > tol}
+    assert not bad, bad
     return worst
+
+
+def _fused_bins(net, ro, rd, cnf=None, pert=None):
+    """The HIP proposal kernels' resampled bins for these rays ([N, 65],
+    [N, 33]; the training step runs the same kernels, proposal_forward), read
+    through the render's parity taps."""
+    from samnerf_amd.fused import FusedRenderer
+    out = FusedRenderer(net).render(ro, rd, cam_near_far=cnf, taps=True, perturb=pert or False)
+    return [out["bins1"].contiguous(), out["bins2"].contiguous()]
+
+
+def _draws(seed, n, device):
+    """perturb=True's draws (fused.perturbed_positions) from a seeded generator."""
+    from samnerf_amd.fused import perturbed_positions
+    torch.manual_seed(seed)
+    return perturbed_positions(n, [128, 64, 32], device)
 
 
 def test_fused_rgb_step_matches_cpu_twin(hip_lib, cuda):
@@ -69,12 +89,14 @@ def test_fused_rgb_step_matches_cpu_twin(hip_lib, cuda):
     the CPU with the oracle encoders."""
     from oracle_backend import oracle_encoders
     from samnerf_amd.train import rgb_train_step, rgb_train_step_fused
+    from oracle_backend import injected_bins
     gpu, cpu = _rgb_nets(cuda)
     ro, rd = _rays(16, 6)
     gt = torch.rand(256, 3, generator=torch.Generator().manual_seed(2))
+    bins = [b.cpu() for b in _fused_bins(gpu, ro.to(cuda), rd.to(cuda))]
     img, loss, out = rgb_train_step_fused(gpu, ro.to(cuda), rd.to(cuda), gt.to(cuda), global_step=1,
                                           perturb=False)
-    with oracle_encoders():
+    with oracle_encoders(), injected_bins(bins):
         img_c, loss_c, out_c = rgb_train_step(cpu, ro, rd, gt, global_step=1, perturb=False)
         loss_c.backward()
     assert (img.cpu() - img_c.detach()).abs().max().item() < 1e-5
@@ -158,11 +180,14 @@ def test_fused_rgb_step_matches_torch_path_perturbed(hip_lib, cuda):
     a, b = _rgb_nets(cuda, seed=21, log2=(19, 17), devices=("cuda", "cuda"))
     ro, rd = _rays(64, 3, cuda)
     gt = torch.rand(4096, 3, generator=torch.Generator().manual_seed(5)).to(cuda)
+    from oracle_backend import injected_bins
+    draws = _draws(11, 4096, cuda)
+    bins = _fused_bins(a, ro, rd, pert=draws)
+    img, loss, out = rgb_train_step_fused(a, ro, rd, gt, global_step=1, perturb=draws)
     torch.manual_seed(11)
-    img, loss, out = rgb_train_step_fused(a, ro, rd, gt, global_step=1)
-    torch.manual_seed(11)
-    img_t, loss_t, out_t = rgb_train_step(b, ro, rd, gt, global_step=1)
-    loss_t.backward()
+    with injected_bins(bins):
+        img_t, loss_t, out_t = rgb_train_step(b, ro, rd, gt, global_step=1)
+        loss_t.backward()
     assert (img - img_t.detach()).abs().max().item() < 1e-5
     assert abs(float(loss) - float(loss_t)) <= 1e-4 * abs(float(loss_t)) + 1e-7
     assert abs(float(out["proposal_loss"]) - float(out_t["proposal_loss"])) <= \
@@ -177,11 +202,14 @@ def test_fused_rgb_step_without_proposal_update(hip_lib, cuda):
     a, b = _rgb_nets(cuda, seed=4, devices=("cuda", "cuda"))
     ro, rd = _rays(16, 2, cuda)
     gt = torch.rand(256, 3, generator=torch.Generator().manual_seed(8)).to(cuda)
+    from oracle_backend import injected_bins
+    draws = _draws(3, 256, cuda)
+    bins = _fused_bins(a, ro, rd, pert=draws)
+    _, loss, _ = rgb_train_step_fused(a, ro, rd, gt, global_step=3001, perturb=draws)
     torch.manual_seed(3)
-    _, loss, _ = rgb_train_step_fused(a, ro, rd, gt, global_step=3001)
-    torch.manual_seed(3)
-    _, loss_t, _ = rgb_train_step(b, ro, rd, gt, global_step=3001)
-    loss_t.backward()
+    with injected_bins(bins):
+        _, loss_t, _ = rgb_train_step(b, ro, rd, gt, global_step=3001)
+        loss_t.backward()
     assert abs(float(loss) - float(loss_t)) <= 1e-4 * abs(float(loss_t)) + 1e-7
     assert all(p.grad is None for p in a.prop_encoders.parameters())
     assert all(p.grad is None for p in a.prop_mlp.parameters())
@@ -197,9 +225,12 @@ def test_fused_rgb_step_entropy_and_background(hip_lib, cuda):
         n.opt.lambda_entropy = 1e-3
     ro, rd = _rays(16, 5, cuda)
     gt = torch.rand(256, 4, generator=torch.Generator().manual_seed(1)).to(cuda)
+    from oracle_backend import injected_bins
+    bins = _fused_bins(a, ro, rd)
     _, loss, out = rgb_train_step_fused(a, ro, rd, gt, global_step=2, perturb=False)
-    _, loss_t, _ = rgb_train_step(b, ro, rd, gt, global_step=2, perturb=False)
-    loss_t.backward()
+    with injected_bins(bins):
+        _, loss_t, _ = rgb_train_step(b, ro, rd, gt, global_step=2, perturb=False)
+        loss_t.backward()
     assert float(out["entropy"]) > 0
     assert abs(float(loss) - float(loss_t)) <= 1e-4 * abs(float(loss_t)) + 1e-7
     _compare_grads(a, b)
@@ -235,11 +266,14 @@ def test_fused_rgb_step_ragged_batches(hip_lib, cuda, n_rays):
     g = torch.Generator().manual_seed(n_rays)
     gt = torch.rand(n_rays, 3, generator=g).to(cuda)
     cnf = torch.stack([torch.full((n_rays,), 0.3), 0.8 + 2 * torch.rand(n_rays, generator=g)], -1).to(cuda)
+    from oracle_backend import injected_bins
+    draws = _draws(n_rays, n_rays, cuda)
+    bins = _fused_bins(a, ro, rd, cnf=cnf, pert=draws)
+    img, loss, _ = rgb_train_step_fused(a, ro, rd, gt, global_step=1, cam_near_far=cnf, perturb=draws)
     torch.manual_seed(n_rays)
-    img, loss, _ = rgb_train_step_fused(a, ro, rd, gt, global_step=1, cam_near_far=cnf)
-    torch.manual_seed(n_rays)
-    img_t, loss_t, _ = rgb_train_step(b, ro, rd, gt, global_step=1, cam_near_far=cnf)
-    loss_t.backward()
+    with injected_bins(bins):
+        img_t, loss_t, _ = rgb_train_step(b, ro, rd, gt, global_step=1, cam_near_far=cnf)
+        loss_t.backward()
     assert (img - img_t.detach()).abs().max().item() < 1e-5
     assert abs(float(loss) - float(loss_t)) <= 1e-4 * abs(float(loss_t)) + 1e-7
     _compare_grads(a, b)
@@ -280,9 +314,12 @@ def test_train_mode_render_runs_the_training_kernels(hip_lib, cuda):
     gt = torch.rand(1024, 3, generator=torch.Generator().manual_seed(9)).to(cuda)
     torch.manual_seed(5)
     _, loss_a, _ = rgb_train_step_fused(a, ro, rd, gt, global_step=1)
+    from oracle_backend import injected_bins
+    bins = _fused_bins(a, ro, rd, pert=_draws(5, 1024, cuda))
     torch.manual_seed(5)
-    _, loss_b, _ = rgb_train_step(b, ro, rd, gt, global_step=1)
-    loss_b.backward()
+    with injected_bins(bins):
+        _, loss_b, _ = rgb_train_step(b, ro, rd, gt, global_step=1)
+        loss_b.backward()
     torch.manual_seed(5)
     img_c, loss_c, out_c = rgb_train_step(c, ro, rd, gt, global_step=1)
     assert "proposal_loss" in out_c and "distort_loss" in out_c and out_c["num_points"] == 1024 * 32
@@ -321,11 +358,13 @@ def test_autograd_rgb_step_with_depth_and_weights_sum_loss(hip_lib, cuda):
     a, b = _rgb_nets(cuda, seed=31, devices=("cuda", "cuda"))
     a.fused = True
     ro, rd = _rays(16, 4, cuda)
+    from oracle_backend import injected_bins
+    bins = _fused_bins(a, ro, rd)
     outs = []
     for n in (a, b):
-        torch.manual_seed(7)
-        o = n.render(ro, rd, staged=False, bg_color=1, perturb=False, update_proposal=True,
-                     return_feats=0)
+        with injected_bins(bins) if n is b else contextlib.nullcontext():
+            o = n.render(ro, rd, staged=False, bg_color=1, perturb=False, update_proposal=True,
+                         return_feats=0)
         loss = (o["image"].mean() + 0.3 * o["depth"].mean() + 2.0 * o["weights_sum"].mean()
                 + o["proposal_loss"])
         loss.backward()

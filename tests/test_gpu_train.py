@@ -33,12 +33,15 @@ def test_fused_sgrid_backward_matches_autograd(hip_lib, cuda):
     ro, rd = ops.get_rays(pose, intr, 32, 32, device=cuda)
     G = torch.randn(32 * 32, 256, device=cuda)
 
+    from oracle_backend import injected_bins
     out = render_sam_train(FusedRenderer(net), ro, rd)
     (out["samvit"] * G).sum().backward()
     g_fused = {k: p.grad.clone() for k, p in net.named_parameters() if p.requires_grad}
     net.zero_grad(set_to_none=True)
+    taps = FusedRenderer(net).render(ro, rd, taps=True)       # the fused path's resampled bins
 
-    ref = net.run_torch(ro, rd, return_feats=1)
+    with injected_bins([taps["bins1"].contiguous(), taps["bins2"].contiguous()]):
+        ref = net.run_torch(ro, rd, return_feats=1)
     (ref["samvit"] * G).sum().backward()
     g_ref = {k: p.grad.clone() for k, p in net.named_parameters() if p.requires_grad}
     assert torch.allclose(out["samvit"], ref["samvit"], atol=1e-3)
@@ -56,11 +59,12 @@ def test_distillation_step_matches_cpu_twin_full_tables(hip_lib, cuda):
     reference's op sequence on the CPU (the mirror's run_torch with the C
     oracle's encoder forward / backward: tests/oracle_backend.py), the same
     loss (utils.py:1098-1106: bilinear resize + MSE vs an N(0,1) target).
-    Loss to fp32 rounding; gradients of s_grid.embeddings and every
-    samvit_mlp tensor within 2e-3 relative (norm): float atomics, GPU vs CPU
-    GEMM order, f16x3 grid_mlp forward (fp32-equivalent)."""
+    Loss to fp32 rounding; at the same resampled bins, gradients of
+    s_grid.embeddings and every samvit_mlp tensor within 1e-4 relative (norm):
+    float atomics, GPU vs CPU GEMM order, f16x3 grid_mlp forward
+    (fp32-equivalent)."""
     from oracle import renderer as orc
-    from oracle_backend import oracle_encoders
+    from oracle_backend import injected_bins, oracle_encoders
     from samnerf_amd.fused import FusedRenderer
     from samnerf_amd.train import sam_train_step
     spec = synth.ModelSpec(with_sam=True)                      # 19 / 19 / 17, as network.py
@@ -75,7 +79,11 @@ def test_distillation_step_matches_cpu_twin_full_tables(hip_lib, cuda):
     gt = torch.randn(1, 256, 64, 64, generator=torch.Generator().manual_seed(1))
     _, lg = sam_train_step(FusedRenderer(nets["gpu"]), ro.to(cuda), rd.to(cuda), 64, 64, gt.to(cuda))
     lg.backward()
-    with oracle_encoders():
+    # the twin samples at the fused path's resampled bins (an ulp of a sample
+    # position moves the fine levels' gradients: tests/test_gpu_rgb_train.py)
+    taps = FusedRenderer(nets["gpu"]).render(ro.to(cuda), rd.to(cuda), taps=True)
+    bins = [taps["bins1"].cpu().contiguous(), taps["bins2"].cpu().contiguous()]
+    with oracle_encoders(), injected_bins(bins):
         out = nets["cpu"].run_torch(ro, rd, return_feats=1)
         pred = out["samvit"].reshape(1, 64, 64, 256).permute(0, 3, 1, 2).contiguous()
         pred = F.interpolate(pred, gt.shape[2:], mode="bilinear")
@@ -90,7 +98,7 @@ def test_distillation_step_matches_cpu_twin_full_tables(hip_lib, cuda):
         a, b = pg.grad.cpu(), pc.grad
         errs[k] = float((a - b).norm() / b.norm().clamp_min(1e-12))
     print("cfg5 gradient relative errors", errs)
-    assert len(errs) == 13 and max(errs.values()) < 2e-3, errs
+    assert len(errs) == 13 and max(errs.values()) < 1e-4, errs
 
 
 def test_sgrid_backward_box_matches_per_corner(hip_lib, cuda, monkeypatch, diag):
@@ -218,11 +226,11 @@ def test_rgb_train_step_gradients_match_cpu_twin(hip_lib, cuda):
     """one RGB training step (utils.py:897-937: MSE + proposal
     + distortion losses) on the GPU -- torch ops + HIP drop-in encoder
     forward/backward kernels -- against the same graph on the CPU with the C
-    oracle's encoders (tests/oracle_backend.py).  perturb=False so both see
-    the same samples; per-tensor relative gradient error < 2e-3 (float
-    atomics, reassociated sums, CPU vs GPU cumsum)."""
+    oracle's encoders (tests/oracle_backend.py).  perturb=False and the twin
+    at the GPU run's resampled bins, so both see the same samples; per-tensor
+    relative gradient error < 3e-4 (float atomics, reassociated sums)."""
     from oracle import renderer as orc
-    from oracle_backend import oracle_encoders
+    from oracle_backend import injected_bins, oracle_encoders, recorded_bins
     from samnerf_amd.train import rgb_train_step
     gpu, cpu = _rgb_pair(cuda)
     pose, intr = synth.gui_camera(16, 16, rot=synth.random_rotation(6))
@@ -236,10 +244,14 @@ def test_rgb_train_step_gradients_match_cpu_twin(hip_lib, cuda):
         seen["x"] = args[0].detach()
         out.register_hook(lambda g: seen.__setitem__("g", g.detach()))
     h = gpu.grid.register_forward_hook(grab)
-    _, lg, _ = rgb_train_step(gpu, ro.to(cuda), rd.to(cuda), gt.to(cuda), global_step=1, perturb=False)
+    bins = []
+    with recorded_bins(bins):
+        _, lg, _ = rgb_train_step(gpu, ro.to(cuda), rd.to(cuda), gt.to(cuda), global_step=1, perturb=False)
     lg.backward()
     h.remove()
-    with oracle_encoders():
+    # the twin samples at the GPU run's bins (an ulp of a final sample position
+    # moves the fine grid levels' gradients by ~1e-2: tests/test_gpu_rgb_train.py)
+    with oracle_encoders(), injected_bins([b.cpu() for b in bins]):
         _, lc, _ = rgb_train_step(cpu, ro, rd, gt, global_step=1, perturb=False)
         lc.backward()
         # (1) the kernel: oracle backward on the GPU's own (x, upstream grad)
@@ -251,24 +263,17 @@ def test_rgb_train_step_gradients_match_cpu_twin(hip_lib, cuda):
     assert k_err < 1e-4, float(k_err)
     # (2) end to end: forward loss to fp32 rounding
     assert abs(float(lg) - float(lc)) <= 1e-4 * abs(float(lc)) + 1e-7, (float(lg), float(lc))
-    # (3) end to end gradients.  The density path's parameter gradients are
-    # small sums of cancelling terms (sigma feeds the MSE, distortion and
-    # proposal losses; measured max |g| ~1e-6 for grid.embeddings against
-    # ~1e-3 for view_mlp), so fp32 reassociation (GPU vs CPU cumsum / sum /
-    # GEMM order) moves them by ~1e-2 relative while every other gradient
-    # agrees to <= 2e-4: per-tensor bound 2e-3, or 2e-2 with cosine > 0.9999
-    # for the grid / grid_mlp tensors behind the cancellation.
+    # (3) end to end gradients at the same samples: every tensor within 3e-4
+    # relative (float atomics, reassociated sums; the proposal loss's fp32
+    # sums ~1e-4)
+    errs = {}
     for (k, pg), (_, pc) in zip(gpu.named_parameters(), cpu.named_parameters()):
         if pc.grad is None:
             assert pg.grad is None or pg.grad.abs().sum() == 0, k
             continue
-        a = pg.grad.cpu()
-        err = (a - pc.grad).norm() / pc.grad.norm().clamp_min(1e-12)
-        if k.startswith("grid.") or k.startswith("grid_mlp."):
-            cos = F.cosine_similarity(a.flatten(), pc.grad.flatten(), dim=0)
-            assert err < 2e-2 and cos > 0.9999, (k, float(err), float(cos))
-        else:
-            assert err < 2e-3, (k, float(err))
+        errs[k] = float((pg.grad.cpu() - pc.grad).norm() / pc.grad.norm().clamp_min(1e-12))
+    print("relative gradient errors:", {k: f"{v:.1e}" for k, v in errs.items()})
+    assert all(v < 3e-4 for v in errs.values()), errs
 
 
 def test_rgb_training_reduces_loss(hip_lib, cuda):
