@@ -17,10 +17,11 @@ the lossy q16 transport is timed after it and reported beside it.
 
 Prints ONE JSON line (rank 0).  `value` = rays of the whole view x steps /
 (max over ranks of the timed region).  `roofline` prices the dominant kernel
-against the unit that binds it (the texture-address path of the gathers,
-DESIGN.md 5) from HIP events recorded on the launch stream inside the timed
-steps; `cpu_baseline` times the CPU oracle (torch-CPU restatement of the
-reference renderer + C restatement of its encoders) on the view's rays, and
+against the guide peak of the unit closest to saturation (L2 bandwidth on the
+algorithmic bytes, VALU issue or MFMA issue) from HIP events
+recorded on the launch stream, with the per-ray counter rates of the
+committed PMC passes (profiles/pmc_rates.json); `cpu_baseline` times the CPU
+oracle (torch-CPU restatement of the reference renderer + C restatement of its encoders) on the view's rays, and
 `parity_vs_ref` compares a parity-weight render of the same view with it.
 """
 import argparse
@@ -43,12 +44,15 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md: L2 ~34.5 TB/s aggregate
 CLOCK_GHZ = 2.4                # MI355X_MICROARCH.md: max clock
 N_CU, N_SIMD = 256, 1024
-# Texture-address path: a 64-lane gather instruction holds TA for ~16 cycles
-# whatever its width or coalescing (TA_BUSY and TCP_TOTAL_CACHE_ACCESSES per
-# VMEM instruction, profiles/r1s4_pmc_counters.txt), i.e. 4 lane
-# addresses per clock per CU.
-TA_LANES_PER_CLK = 4
-TA_PEAK_GADDR = N_CU * TA_LANES_PER_CLK * CLOCK_GHZ           # 2,457.6 G lane-addresses/s
+# Per-stage counter rates of one view (tools/pmc_rates.py over the rocprofv3
+# PMC passes of tools/pmc_passes.sh; recomputable from the PMC table committed
+# beside it): VALU-issue and MFMA-busy cycles per ray, HBM bytes per ray.
+PMC_RATES = os.path.join(REPO, "profiles", "pmc_rates.json")
+# The texture-address rate is not one number: tools/ta_rate.hip measured
+# 0.45 lane-addresses/clk/CU for random dword gathers (one 128-B line per lane)
+# and 14.6 for contiguous ones (profiles/r3_ta_rate.json), so the gather
+# stages are priced against the guide's L2 bandwidth and their VALU issue
+# rate instead, and `bound` names whichever is closer to its peak.
 
 # Algorithmic bytes per ray and stage (SURVEY.md 8d / BASELINE.md 3): fp32
 # embedding gathers (8 corners x C x 4 B per level per sample) + the stage's
@@ -62,14 +66,6 @@ ALG_BYTES_PER_RAY = {
     "sam_head": 164 * 4 + 256 * 4,
 }
 ALG_BYTES_RAY_TOTAL = 226_348
-# Gather lane-addresses per ray the kernels issue (the TA work), from their
-# gather code: dense levels load each x-adjacent corner pair with one 16-B
-# load (4 addresses instead of 8), hashed levels 8 per level.
-#   k_prop_sigma<128>: prop0 has 3 dense + 2 hashed levels -> 28 per sample
-#   k_prop_sigma<64>:  prop1 has 2 dense + 3 hashed levels -> 32 per sample
-#   k_final:           levels 0-3 dense in paired slots (16), level 4 dense but
-#                      sharing its slot with hashed level 5, 12 levels x 8 -> 112
-GATHER_ADDR_PER_RAY = {"prop0": 128 * 28, "prop1": 64 * 32, "final": 32 * 112}
 # SAM head (network.py:36-75): 163->256, 256->256, 419->256, 256->256, 256->256
 HEAD_FLOP_PER_RAY = 2 * 256 * (163 + 256 + 419 + 256 + 256)  # 691,200
 # MFMA issue of the head per 32 rays (one wave): 86 k-blocks of 16 (K padded
@@ -615,64 +611,74 @@ class ViewRunner:
         return dt, last, stage_avg, stage_src
 
 
-def rooflines(stage_avg, band_rays, head_mode, band_traffic):
-    """`roofline` of the dominant kernel and every stage against the unit its
-    counters say binds it: the gather kernels against the
-    texture-address rate, the SAM head against its MFMA issue rate.  frac <= 1
-    by construction: the counts are of work the kernels issue."""
-    def ta(st):
+def rooflines(stage_avg, band_rays, head_mode, rates):
+    """`roofline` of the dominant kernel and every stage, each against the
+    guide peak of the unit closest to saturation:
+      l2   -- algorithmic bytes (embedding gathers + ray I/O, ALG_BYTES_PER_RAY)
+              / live time vs the L2's 34.5 TB/s (the tables are L2/MALL-resident);
+      valu -- VALU-issue cycles of the stage's kernels (PMC SQ_ACTIVE_INST_VALU
+              x 4 per ray, profiles/pmc_rates.json) / (1024 SIMDs x 2.4 GHz x
+              live time);
+      mfma -- the SAM head's MFMA issue cycles from its structure (86 k-blocks
+              x 8 tiles x 3 v_mfma_f32_32x32x16_f16 per 32 rays) / (1024 x 2.4
+              GHz x live time), with the PMC MFMA-busy cycles beside it.
+    The nominal clock makes every busy fraction a lower bound (the chip runs
+    below 2.4 GHz under load)."""
+    st_rates = (rates or {}).get("stages", {})
+    cyc_avail = lambda ms: N_SIMD * CLOCK_GHZ * 1e9 * ms * 1e-3
+
+    def entry(st):
         ms = stage_avg.get(st, 0.0)
         if ms <= 0:
             return None
-        addr = GATHER_ADDR_PER_RAY[st] * band_rays
-        ach = addr / (ms * 1e-3) / 1e9
+        r = st_rates.get(st, {})
         alg = ALG_BYTES_PER_RAY[st] * band_rays
-        return {"bound": "ta", "unit": "Gaddr/s", "achieved": ach, "peak": TA_PEAK_GADDR,
-                "frac": ach / TA_PEAK_GADDR, "lane_addresses_per_ray": GATHER_ADDR_PER_RAY[st],
-                "l2_frac_of_alg_bytes": alg / (ms * 1e-3) / 1e9 / L2_PEAK_GBS}
+        cand = {"l2": {"unit": "GB/s", "achieved": alg / (ms * 1e-3) / 1e9, "peak": L2_PEAK_GBS,
+                       "alg_bytes_per_ray": ALG_BYTES_PER_RAY[st]}}
+        cand["l2"]["frac"] = cand["l2"]["achieved"] / L2_PEAK_GBS
+        if "valu_cycles_per_ray" in r:
+            c = r["valu_cycles_per_ray"] * band_rays
+            cand["valu"] = {"unit": "busy cycles / SIMD cycles", "frac": c / cyc_avail(ms),
+                            "valu_cycles_per_ray": r["valu_cycles_per_ray"]}
+        if st == "sam_head":
+            cyc = HEAD_MFMA_CYCLES_PER_32[head_mode] * band_rays / 32
+            cand["mfma"] = {"unit": "TFLOP/s", "frac": cyc / cyc_avail(ms),
+                            "achieved_fp32_equiv": HEAD_FLOP_PER_RAY * band_rays / (ms * 1e-3) / 1e12,
+                            "peak": F32_MFMA_PEAK_TFS if head_mode == 1 else BF16_MFMA_PEAK_TFS,
+                            "basis": "MFMA issue cycles of the head's structure (f16x3: 86 k-blocks x 8 "
+                                     "tiles x 3 v_mfma_f32_32x32x16_f16 per 32 rays) / (1024 SIMDs x "
+                                     "2.4 GHz x time)"}
+            if "mfma_busy_cycles_per_ray" in r:
+                cand["mfma"]["pmc_mfma_busy_frac"] = r["mfma_busy_cycles_per_ray"] * band_rays / cyc_avail(ms)
+        bound = max(cand, key=lambda k: cand[k]["frac"])
+        e = {"bound": bound}
+        e.update(cand[bound])
+        e["other_bounds"] = {k: v["frac"] for k, v in cand.items() if k != bound}
+        if "ta_busy_frac_in_pmc_run" in r:
+            e["ta_busy_frac_in_pmc_run"] = r["ta_busy_frac_in_pmc_run"]
+        return e
 
-    stages = {st: ta(st) for st in ("prop0", "prop1", "final")}
-    if stage_avg.get("sam_head", 0) > 0:
-        ms = stage_avg["sam_head"]
-        cyc = HEAD_MFMA_CYCLES_PER_32[head_mode] * band_rays / 32
-        frac = cyc / (N_SIMD * CLOCK_GHZ * 1e9 * ms * 1e-3)
-        stages["sam_head"] = {
-            "bound": "mfma", "unit": "TFLOP/s", "frac": frac,
-            "achieved_fp32_equiv": HEAD_FLOP_PER_RAY * band_rays / (ms * 1e-3) / 1e12,
-            "peak": F32_MFMA_PEAK_TFS if head_mode == 1 else BF16_MFMA_PEAK_TFS,
-            "basis": "MFMA issue cycles of the head's structure (f16x3: 86 k-blocks x 8 tiles x 3 "
-                     "v_mfma_f32_32x32x16_f16 per 32 rays) / (1024 SIMDs x 2.4 GHz x time)"}
-    if stage_avg.get("s_grid", 0) > 0:
-        ms = stage_avg["s_grid"]
-        alg = ALG_BYTES_PER_RAY["s_grid"] * band_rays
-        stages["s_grid"] = {
-            "bound": "valu", "frac": None,
-            "note": "de-duplicated LDS box gathers: VALU-bound (77% VALU busy, 24% TA, "
-                    "profiles/r1s4_pmc_counters.txt); the algorithmic gather rate below is not a "
-                    "roofline (rows are read once per wave, not per lane)",
-            "alg_gather_tbs": alg / (ms * 1e-3) / 1e12}
+    stages = {st: entry(st) for st in STAGES}
     stages = {k: v for k, v in stages.items() if v is not None}
-    cands = {k: stage_avg[k] for k in ("prop0", "prop1", "final") if stage_avg.get(k, 0) > 0}
+    cands = {k: stage_avg[k] for k in STAGES if stage_avg.get(k, 0) > 0}
     dom = max(cands, key=cands.get)
     roof = dict(stages[dom])
     roof.update({"kernel": dom, "avg_launch_ms": stage_avg[dom],
                  "alg_bytes_per_launch": ALG_BYTES_PER_RAY[dom] * band_rays})
-    t = band_traffic.get(dom) if band_traffic else None
+    hb = st_rates.get(dom, {}).get("hbm_bytes_per_ray")
+    t = hb * band_rays if hb else None
     roof["traffic"] = t
     roof["hbm_frac_counters"] = (t / (stage_avg[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS) if t else None
+    roof["pmc_source"] = os.path.relpath(PMC_RATES, REPO) if rates else None
     return roof, stages
 
 
-def pmc_traffic(band_rays, n_view):
-    """HBM bytes per launch of each stage from the committed rocprofv3 PMC
-    passes (profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE per the
-    guide's gfx950 correction), scaled to this band."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+def pmc_rates():
+    """profiles/pmc_rates.json (tools/pmc_rates.py), or None."""
     try:
-        d = json.load(open(path))
-        return {k: v["hbm_bytes"] * band_rays / n_view for k, v in d.items() if "hbm_bytes" in v}
+        return json.load(open(PMC_RATES))
     except Exception:
-        return {}
+        return None
 
 
 def main():
@@ -710,8 +716,7 @@ def main():
     runner = ViewRunner(args, renderer, world, dev, H, W, pose, intr, r0, r1, codec)
     dt, last, stage_avg, stage_src = runner.run(args.steps, args.warmup)
     value = n_total * args.steps / dt
-    roof, stage_roof = rooflines(stage_avg, band_rays, args.head_mode,
-                                 pmc_traffic(band_rays, H * W))
+    roof, stage_roof = rooflines(stage_avg, band_rays, args.head_mode, pmc_rates())
 
     side = {}
     if not args.no_alt and world > 1 and with_sam and args.chunks == 0:

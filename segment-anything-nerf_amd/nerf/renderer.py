@@ -48,7 +48,7 @@ def sample_pdf(bins, weights, T, perturb=False):
     pdf = weights / torch.sum(weights, -1, keepdim=True)
     cdf = torch.cumsum(pdf, -1).clamp(max=1)
     cdf = torch.cat([torch.zeros_like(cdf[..., :1]), cdf], -1)
-    u = torch.linspace(0.5 / T, 1 - 0.5 / T, steps=T, device=weights.device).expand(N, T)
+    u = torch.linspace(0.5 / T, 1 - 0.5 / T, steps=T).to(weights.device).expand(N, T)
     if perturb:
         u = u + (torch.rand_like(u) - 0.5) / T
     u = u.contiguous()

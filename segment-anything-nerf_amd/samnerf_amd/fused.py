@@ -55,7 +55,7 @@ def perturbed_positions(N, num_steps, device):
     bins = (bins + (torch.rand_like(bins) - 0.5) / T0).clamp(0, 1)
     out = [bins.contiguous()]
     for T in (int(num_steps[1]) + 1, int(num_steps[2]) + 1):
-        u = torch.linspace(0.5 / T, 1 - 0.5 / T, steps=T, device=device).expand(N, T)
+        u = torch.linspace(0.5 / T, 1 - 0.5 / T, steps=T).to(device).expand(N, T)   # on the CPU, then moved, as renderer.py:97
         u = u + (torch.rand_like(u) - 0.5) / T
         out.append(u.contiguous())
     return tuple(out)

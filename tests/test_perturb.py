@@ -66,6 +66,28 @@ def test_perturbed_positions_draw_like_the_reference():
 
 
 @pytest.mark.gpu
+def test_perturbed_positions_on_the_device_draw_like_the_reference(cuda):
+    """On the GPU: the helper's draws equal the reference's expressions run on
+    the device from the same seed -- the stage-0 bins from a device linspace
+    (renderer.py:264-271), sample_pdf's u from a CPU linspace moved to the
+    device (renderer.py:97), which can differ from a device linspace in the
+    last bit."""
+    from samnerf_amd.fused import perturbed_positions
+    N, steps = 4096, [128, 64, 32]
+    torch.cuda.manual_seed(11)
+    got = perturbed_positions(N, steps, cuda)
+    torch.cuda.manual_seed(11)
+    T0 = steps[0]
+    bins = torch.linspace(0, 1, T0 + 1, device=cuda).unsqueeze(0).expand(N, -1)
+    want = [(bins + (torch.rand_like(bins) - 0.5) / T0).clamp(0, 1)]
+    for T in (steps[1] + 1, steps[2] + 1):
+        u = torch.linspace(0.5 / T, 1 - 0.5 / T, steps=T).to(cuda).expand(N, T)
+        want.append(u + (torch.rand_like(u) - 0.5) / T)
+    for g, w in zip(got, want):
+        assert g.device.type == "cuda" and torch.equal(g, w)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("head_mode", [0, 1])
 def test_fused_perturbed_matches_reference_golden(hip_lib, cuda, monkeypatch, head_mode):
     from samnerf_amd.fused import FusedRenderer

@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Per-stage counter rates of one view from a tools/pmc_passes.sh output dir.
+
+usage: python tools/pmc_rates.py gpurun_out/pmc_<TAG> > profiles/pmc_rates.json
+
+For each stage of the view (the kernels bench.py's stage events bracket) it
+averages every counter over the stage's dispatches and sums the stage's
+kernels, per launch of the view (the profiled bench renders the headline
+512x512 view, 262,144 rays).  bench.py prices its live stage times with these
+(stage_roofline): VALU-issue cycles (SQ_ACTIVE_INST_VALU counts quad-cycles,
+MI355X_MICROARCH.md "s_memtime tick vs SQ PMC units"), MFMA-busy cycles, and
+HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (the guide's gfx950 correction).
+Every number is recomputable from the table tools/pmc_table.py prints for the
+same directory (profiles/<tag>_pmc_table.txt).
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+STAGE_KERNELS = {                     # substring of the kernel name -> stage
+    "k_get_rays": "prop0", "k_snf": "prop0", "k_prop_sigma<128": "prop0", "k_prop_pdf<128": "prop0",
+    "k_prop_sigma<64": "prop1", "k_prop_pdf<64": "prop1",
+    "k_final": "final",
+    "k_sgrid": "s_grid",
+    "k_head_wmax": "sam_head", "k_pack_h16": "sam_head", "k_sam_head": "sam_head",
+}
+RAYS = 262144
+
+
+def stage_of(name):
+    for k, st in STAGE_KERNELS.items():
+        if k in name:
+            return st
+    return None
+
+
+def main(root):
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            vals[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {}
+    for name, cs in vals.items():
+        st = stage_of(name)
+        if st is None:
+            continue
+        d = out.setdefault(st, {"kernels": [], "counters": collections.defaultdict(float)})
+        d["kernels"].append(name[:80])
+        for c, v in cs.items():
+            d["counters"][c] += sum(v) / len(v)          # per dispatch, summed over the stage's kernels
+    res = {"rays_per_view": RAYS, "source": root, "stages": {}}
+    for st, d in out.items():
+        c = d["counters"]
+        e = {"kernels": sorted(d["kernels"]), "counters_per_view": dict(c)}
+        if "SQ_ACTIVE_INST_VALU" in c:
+            e["valu_cycles_per_ray"] = 4.0 * c["SQ_ACTIVE_INST_VALU"] / RAYS
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+            e["mfma_busy_cycles_per_ray"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / RAYS
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            e["hbm_bytes_per_ray"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0 / RAYS
+        if "TA_BUSY_avr" in c and "GRBM_GUI_ACTIVE" in c:
+            e["ta_busy_frac_in_pmc_run"] = c["TA_BUSY_avr"] / (c["GRBM_GUI_ACTIVE"] / 8.0)
+        res["stages"][st] = e
+    json.dump(res, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
