@@ -262,6 +262,27 @@ int samnerf_sam_head_forward(const samnerf_model* model, const float* rows, uint
 int samnerf_mask_forward(const samnerf_model* model, uint32_t N, float* instance_mask_logits,
                          const void* workspace, size_t workspace_bytes, samnerf_stream_t stream);
 
+/* The --with_mask training step's instance head (nerf/utils.py:941-977 under
+ * renderer.py:392-395, :451-452; 'default' head, network.py:125-133), exact fp32
+ * on MFMA.  forward: instance_mask_logits [N, mask_out] from the final samples
+ * (positions, weights, geo_feat) that the samnerf_render_forward call with
+ * with_mask = 1 left in `render_ws`, saving the head's activations in
+ * `workspace` (samnerf_mask_train_workspace_size(N) bytes); backward: given
+ * d loss / d logits [N, mask_out], writes the gradients of mask_w[0..2]
+ * ([256,143] [256,256] [mask_out,256], overwritten) and scatters into
+ * grad_m_grid (the m_grid embedding gradient, accumulated into: the
+ * reference encoder's backward).  weights and geo_feat carry no gradient
+ * (.detach() in the reference), the sample positions none (no parameter).
+ * Replaces the reference's per-chunk torch ops and autograd of that branch. */
+size_t samnerf_mask_train_workspace_size(uint32_t N);
+int samnerf_mask_train_forward(const samnerf_model* model, uint32_t N, float* instance_mask_logits,
+                               const void* render_ws, size_t render_ws_bytes, void* workspace,
+                               size_t workspace_bytes, samnerf_stream_t stream);
+int samnerf_mask_train_backward(const samnerf_model* model, uint32_t N, const float* grad_logits,
+                                float* const* grad_mask_w, float* grad_m_grid, const void* render_ws,
+                                size_t render_ws_bytes, void* workspace, size_t workspace_bytes,
+                                samnerf_stream_t stream);
+
 /* Backward of the s_grid feature composite for the SAM-distillation step
  * (nerf/utils.py:1098-1106 training branch): given the per-ray gradient of
  * f_sam [N,128] (the first 128 columns of d(loss)/d(feature_rows)), scatter

@@ -27,7 +27,7 @@ DIAG_OBJ_DIR = os.path.join(HERE, "build", "obj_diag")
 
 SOURCES = ["common.cpp", "grid_encoder.hip", "sh_freq_encoder.hip", "raymarch.hip",
            "sam_head.hip", "tile_codec.hip", "train_optim.hip", "sam_head_train.hip",
-           "mask_head.hip", "rgb_train.hip"]
+           "mask_head.hip", "rgb_train.hip", "mask_head_train.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-munsafe-fp-atomics", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",

@@ -1,0 +1,459 @@
+// mask_head_train.hip -- the --with_mask training step's instance head
+// ('default' mask_mlp_type) with its backward, exact fp32 on matrix cores.
+//
+// Reference (nerf/utils.py:941-977 under nerf/renderer.py:392-395, :451-452,
+// heads at nerf/network.py:125-133): per final sample k of ray n
+//     x_k  = cat(m_grid(xyz_k) [16 levels x 8 channels], geo_feat_k.detach() [15])
+//     o_k  = W2 leaky(W1 leaky(W0 x_k))          (SkipConnMLP, bias=False)
+//     instance_mask_logits_n = sum_k weights_k.detach() * o_k
+// trained through softmax / clamp / NLL (utils.py:958-973): the gradient
+// reaches mask_mlp's three weights and m_grid's embeddings only (weights and
+// geo_feat are detached, the sample positions carry no gradient).  torch runs
+// this as ~350 kernels per step (m_grid forward / backward through the
+// encoder, [N, 32, 143] and [N, 32, 256] materialised twice, GEMMs, leaky
+// backward); here:
+//   k_mt_pack    the weights in 16x16x4 A-fragment order, forward and transposed;
+//   k_mt_fwd     16 rows (samples) per workgroup: the m_grid gathers + geo_feat
+//                into LDS, the three layers on v_mfma_f32_16x16x4_f32, x / h1 /
+//                h2 / o saved (unit-major, row-contiguous) for the backward;
+//   k_mt_logits  logits[n] = sum_k w_k o_k in sample order;
+//   k_mt_bwd     16 rows per workgroup: g_o = w_k dL/dlogits_n, dz2 = (W2^T g_o) *
+//                leaky'(h2), dz1 = (W1^T dz2) * leaky'(h1), dx = W0^T dz1, and
+//                the trilinear scatter of dx's m_grid part into the embedding
+//                gradient (one float atomic per corner and channel, the
+//                reference encoder's backward, gridencoder.cu:252-349);
+//   k_mt_dw      dW0 = dz1^T x, dW1 = dz2^T h1, dW2 = g_o^T h2 over all rows: one
+//                32x32 output tile x 1,024 rows per wave, float atomics.
+// Rows are sample-major (row = k * N + slot), the order in which the render
+// (k_final, GEO form) leaves positions, weights and geo_feat in its workspace.
+// Every product is an fp32 MFMA (exact fma chains), so the gradients match
+// torch's fp32 autograd up to summation order.
+#include <algorithm>
+
+#include "fp32_chain.h"
+#include "samnerf_common.h"
+
+using namespace samnerf;
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kRows = 16;                     // rows per workgroup (fwd / bwd)
+constexpr int kT = 32;                        // final samples per ray
+constexpr int kIn0 = 143;                     // 128 m_grid features + 15 geo_feat
+constexpr int kKp[3] = {144, 256, 256};       // padded fan-in per layer
+constexpr int kOp[3] = {256, 256, 32};        // padded fan-out per layer
+constexpr uint32_t kChunk = 1024;             // rows per dW work item
+
+__host__ __device__ constexpr int pack_base(int l) {     // floats before layer l (either pack)
+    int b = 0;
+    for (int i = 0; i < l; ++i) b += kKp[i] * kOp[i];
+    return b;
+}
+constexpr int kPackFloats = pack_base(3);
+
+struct MaskW {
+    const float* w[3];       // [256,143] [256,256] [K,256]
+    uint32_t K;
+};
+__host__ __device__ inline int logical_in(int l) { return l == 0 ? kIn0 : 256; }
+__host__ __device__ inline int logical_out(int l, uint32_t K) { return l == 2 ? (int)K : 256; }
+
+// wf[l][tile t < Op/16][step s < Kp/4][lane]: A of out = W x (16x16x4):
+//   A[i = lane & 15][k = lane >> 4] = W_l[16t + i][4s + k]
+// wb[l][tile t < Kp/16][step s < Op/4][lane]: A of dx = W^T g:
+//   A[i][k] = W_l[4s + k][16t + i]
+__global__ void __launch_bounds__(256) k_mt_pack(MaskW mw, float* __restrict__ wf, float* __restrict__ wb) {
+    const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+    if (e >= (uint32_t)kPackFloats) return;
+    int l = 0;
+    while (l < 2 && (int)e >= pack_base(l + 1)) ++l;
+    const uint32_t o = e - (uint32_t)pack_base(l);
+    const uint32_t lane = o & 63u, i = lane & 15u, k = lane >> 4, ts = o >> 6;
+    const float* W = mw.w[l];
+    const int li = logical_in(l), lo = logical_out(l, mw.K);
+    {
+        const uint32_t S = (uint32_t)kKp[l] / 4u, t = ts / S, s = ts % S;
+        const int r = (int)(16u * t + i), c = (int)(4u * s + k);
+        wf[e] = (r < lo && c < li) ? W[(size_t)r * li + c] : 0.0f;
+    }
+    {
+        const uint32_t S = (uint32_t)kOp[l] / 4u, t = ts / S, s = ts % S;
+        const int r = (int)(4u * s + k), c = (int)(16u * t + i);
+        wb[e] = (r < lo && c < li) ? W[(size_t)r * li + c] : 0.0f;
+    }
+}
+
+__device__ __forceinline__ float leaky(float x) { return x >= 0.0f ? x : x * 0.01f; }
+
+struct Saved {
+    float* x;      // [144][Rp]
+    float* h1;     // [256][Rp] (post leaky_relu)
+    float* h2;     // [256][Rp]
+    float* o;      // [32][Rp]  point mask logits
+    float* go;     // [32][Rp]  d loss / d o
+    float* g2;     // [256][Rp] d loss / d z2
+    float* g1;     // [256][Rp] d loss / d z1
+    uint32_t R, Rp;
+};
+
+struct SampleIn {
+    GridDesc<16> grid;       // m_grid (L16 C8)
+    const float* u;          // [32][3][N] grid-space positions (slot order)
+    const float* w;          // [32][N] final weights
+    const float* geo;        // [32][16][N] grid_mlp output rows (row 0 = sigma, unused)
+    uint32_t N;
+};
+
+struct FwdArgs {
+    SampleIn in;
+    const float* wf;
+    Saved sv;
+};
+
+// out[Op x 16] = W_l in[Kp x 16]: wave w owns output tiles w, w + 4, ..;
+// B operand = in[(4s + k) * 16 + j] from LDS.  Returns through `store`.
+template <int L, typename Store>
+__device__ __forceinline__ void fwd_layer(const float* __restrict__ wf, const float* in, int w, int lane,
+                                          Store store) {
+    constexpr int NT = kOp[L] / 16, MT = (NT + 3) / 4, S = kKp[L] / 4;
+    if (w >= NT) return;                                   // layer 2: waves 0, 1
+    const int j = lane & 15, k = lane >> 4;
+    f32x4 acc[MT];
+    const float* Ap[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        acc[m] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        Ap[m] = wf + pack_base(L) + (size_t)(w + 4 * m) * S * 64 + lane;
+    }
+    mfma_chain<MT, S, 4>(acc, Ap, in + k * kRows + j);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) store(16 * (w + 4 * m) + 4 * k + r, j, acc[m][r]);
+}
+
+// the m_grid features (16 levels x 8 channels) and geo_feat of the block's 16
+// rows into X[c * 16 + j]; thread (level tid >> 4, row tid & 15)
+__device__ __forceinline__ void gather_x(const SampleIn& in, const LevelDesc* sLv, uint32_t r0, uint32_t R,
+                                         float* X) {
+    const int tid = threadIdx.x, j = tid & 15, l = tid >> 4;
+    const uint32_t r = r0 + (uint32_t)j;
+    const bool live = r < R;
+    const uint32_t k = live ? r / in.N : 0u, s = live ? r % in.N : 0u;
+    const float* up = in.u + (size_t)k * 3u * in.N + s;
+    float f[8];
+    lookup_level3<8>(in.grid.emb, sLv[l], up[0], up[in.N], up[2u * in.N], f);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) X[(8 * l + c) * kRows + j] = live ? f[c] : 0.0f;
+    // geo_feat: thread (g = tid >> 4 = 0..15, row j); index 15 = padding
+    const float gv = (live && l < 15) ? in.geo[((size_t)k * 16u + (uint32_t)l + 1u) * in.N + s] : 0.0f;
+    X[(128 + l) * kRows + j] = gv;
+}
+
+__global__ void __launch_bounds__(256) k_mt_fwd(FwdArgs a) {
+    __shared__ float X[kKp[0] * kRows];
+    __shared__ float H1[256 * kRows];
+    __shared__ float H2[256 * kRows];
+    __shared__ LevelDesc sLv[16];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t r0 = blockIdx.x * kRows;
+    const Saved& sv = a.sv;
+    if (tid < 16) sLv[tid] = a.in.grid.lv[tid];
+    __syncthreads();
+    gather_x(a.in, sLv, r0, sv.R, X);
+    __syncthreads();
+    for (int idx = tid; idx < kKp[0] * kRows; idx += 256)
+        sv.x[(size_t)(idx / kRows) * sv.Rp + r0 + (idx % kRows)] = X[idx];
+    fwd_layer<0>(a.wf, X, w, lane, [&](int u, int j, float z) {
+        const float h = r0 + (uint32_t)j < sv.R ? leaky(z) : 0.0f;
+        H1[u * kRows + j] = h;
+        sv.h1[(size_t)u * sv.Rp + r0 + j] = h;
+    });
+    __syncthreads();
+    fwd_layer<1>(a.wf, H1, w, lane, [&](int u, int j, float z) {
+        const float h = r0 + (uint32_t)j < sv.R ? leaky(z) : 0.0f;
+        H2[u * kRows + j] = h;
+        sv.h2[(size_t)u * sv.Rp + r0 + j] = h;
+    });
+    __syncthreads();
+    fwd_layer<2>(a.wf, H2, w, lane, [&](int u, int j, float z) {
+        sv.o[(size_t)u * sv.Rp + r0 + j] = r0 + (uint32_t)j < sv.R ? z : 0.0f;
+    });
+}
+
+// logits[tiles(s)][u] = sum_k w[k][s] * o[u][k N + s], k in sample order
+__global__ void __launch_bounds__(256) k_mt_logits(const float* __restrict__ wk, const float* __restrict__ o,
+                                                   uint32_t N, uint32_t K, uint32_t Rp, RayTiles tiles,
+                                                   float* __restrict__ logits) {
+    const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+    if (e >= N * K) return;
+    const uint32_t s = e % N, u = e / N;
+    float acc = 0.0f;
+    for (int k = 0; k < kT; ++k) acc += wk[(size_t)k * N + s] * o[(size_t)u * Rp + (size_t)k * N + s];
+    logits[(size_t)tiles(s) * K + u] = acc;
+}
+
+struct BwdArgs {
+    SampleIn in;
+    const float* wb;
+    const float* glog;       // [N][K] d loss / d instance_mask_logits (ray order)
+    RayTiles tiles;
+    uint32_t K;
+    Saved sv;
+    float* gemb;             // m_grid embedding gradient (accumulated)
+};
+
+// dx[Kp x 16] = W_l^T g[Op x 16]: output tiles t = w, w + 4, .. of NT (tiles
+// past NT repeat the last and are dropped: the chain stays branch-free)
+template <int L, int NT, typename Store>
+__device__ __forceinline__ void bwd_layer(const float* __restrict__ wb, const float* g, int w, int lane,
+                                          Store store) {
+    constexpr int MT = (NT + 3) / 4, S = kOp[L] / 4;
+    const int j = lane & 15, k = lane >> 4;
+    f32x4 acc[MT];
+    const float* Ap[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        acc[m] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        const int t = min(w + 4 * m, NT - 1);
+        Ap[m] = wb + pack_base(L) + (size_t)t * S * 64 + lane;
+    }
+    mfma_chain<MT, S, 4>(acc, Ap, g + k * kRows + j);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int t = w + 4 * m;
+        if (t >= NT) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) store(16 * t + 4 * k + r, j, acc[m][r]);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_mt_bwd(BwdArgs a) {
+    __shared__ float P[256 * kRows];
+    __shared__ float Q[256 * kRows];
+    __shared__ LevelDesc sLv[16];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t r0 = blockIdx.x * kRows;
+    const Saved& sv = a.sv;
+    const uint32_t N = a.in.N;
+    if (tid < 16) sLv[tid] = a.in.grid.lv[tid];
+    // g_o[u][j] = w_row * dL/dlogits[ray][u] (u < K), into P (32 x 16)
+    for (int idx = tid; idx < 32 * kRows; idx += 256) {
+        const int u = idx / kRows, j = idx % kRows;
+        const uint32_t r = r0 + (uint32_t)j;
+        float g = 0.0f;
+        if (r < sv.R && (uint32_t)u < a.K) {
+            const uint32_t k = r / N, s = r % N;
+            g = a.in.w[(size_t)k * N + s] * a.glog[(size_t)a.tiles(s) * a.K + u];
+        }
+        P[idx] = g;
+        sv.go[(size_t)u * sv.Rp + r] = g;
+    }
+    __syncthreads();
+    // torch's leaky_relu backward: grad * (result > 0 ? 1 : slope)
+    bwd_layer<2, 16>(a.wb, P, w, lane, [&](int v, int j, float d) {
+        const uint32_t r = r0 + (uint32_t)j;
+        const float h = sv.h2[(size_t)v * sv.Rp + r];
+        const float gz = r < sv.R ? (h > 0.0f ? d : d * 0.01f) : 0.0f;
+        Q[v * kRows + j] = gz;
+        sv.g2[(size_t)v * sv.Rp + r] = gz;
+    });
+    __syncthreads();
+    bwd_layer<1, 16>(a.wb, Q, w, lane, [&](int v, int j, float d) {
+        const uint32_t r = r0 + (uint32_t)j;
+        const float h = sv.h1[(size_t)v * sv.Rp + r];
+        const float gz = r < sv.R ? (h > 0.0f ? d : d * 0.01f) : 0.0f;
+        P[v * kRows + j] = gz;
+        sv.g1[(size_t)v * sv.Rp + r] = gz;
+    });
+    __syncthreads();
+    // dx of the m_grid part (tiles 0..7 of 9; geo_feat is detached) into Q
+    bwd_layer<0, 8>(a.wb, P, w, lane, [&](int v, int j, float d) { Q[v * kRows + j] = d; });
+    __syncthreads();
+    // trilinear scatter: thread (level l, row j), 8 corners x 8 channels
+    const int j = tid & 15, l = tid >> 4;
+    const uint32_t r = r0 + (uint32_t)j;
+    if (r >= sv.R) return;
+    const uint32_t k = r / N, s = r % N;
+    const float* up = a.in.u + (size_t)k * 3u * N + s;
+    uint32_t off[8];
+    float cw[8];
+    corner_rows<8>(sLv[l], up[0], up[N], up[2u * N], off, cw);
+    float g[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) g[c] = Q[(8 * l + c) * kRows + j];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        float* row = a.gemb + off[c] / 4u;
+#pragma unroll
+        for (int ch = 0; ch < 8; ++ch) atomicAdd(row + ch, cw[c] * g[ch]);
+    }
+}
+
+struct DwArgs {
+    Saved sv;
+    uint32_t K;
+    float* gw[3];            // [256][143] [256][256] [K][256], zeroed, accumulated
+};
+
+constexpr int kDwTilesK[3] = {5, 8, 8};                  // 32-wide input tiles per layer
+constexpr int kDwTilesU[3] = {8, 8, 1};                  // 32-wide output tiles per layer
+__host__ __device__ constexpr int dw_items_before(int l) {
+    int b = 0;
+    for (int i = 0; i < l; ++i) b += kDwTilesU[i] * kDwTilesK[i];
+    return b;
+}
+constexpr int kDwTiles = dw_items_before(3);             // 112 output tiles of 32 x 32
+
+// dW_l[u][c] += sum over a chunk of rows of G_l[u][r] X_l[c][r] (G: dz1 / dz2
+// / g_o, X: x / h1 / h2); one wave per (output tile, chunk).  The rows of an
+// MFMA's k pair can be any two: lane half h of group m takes rows
+// c0 + 8m + 4h .. +3 over four MFMAs, one 16-B load per operand.
+__global__ void __launch_bounds__(256) k_mt_dw(DwArgs a) {
+    const uint32_t item = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t chunks = a.sv.Rp / kChunk;
+    if (item >= (uint32_t)kDwTiles * chunks) return;
+    const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+    const uint32_t tile = item % kDwTiles, chunk = item / kDwTiles;
+    int l = 0;
+    while (l < 2 && (int)tile >= dw_items_before(l + 1)) ++l;
+    const int lt = (int)tile - dw_items_before(l);
+    const int ut = lt / kDwTilesK[l], kt = lt % kDwTilesK[l];
+    const uint32_t c0 = chunk * kChunk;
+    const int u = 32 * ut + i, c = 32 * kt + i;              // A row (unit) / B column (input)
+    const Saved& sv = a.sv;
+    const float* G = l == 0 ? sv.g1 : l == 1 ? sv.g2 : sv.go;
+    const float* X = l == 0 ? sv.x : l == 1 ? sv.h1 : sv.h2;
+    const bool gok = u < kOp[l], xok = c < kKp[l];
+    const float* Ga = G + (size_t)(gok ? u : 0) * sv.Rp + c0 + 4 * h;
+    const float* Xb = X + (size_t)(xok ? c : 0) * sv.Rp + c0 + 4 * h;
+    f32x16 acc = {};
+    for (uint32_t m = 0; m < kChunk / 8u; ++m) {
+        float4 ga = *reinterpret_cast<const float4*>(Ga + 8 * m);
+        float4 xb = *reinterpret_cast<const float4*>(Xb + 8 * m);
+        if (!gok) ga = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (!xok) xb = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.x, xb.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.y, xb.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.z, xb.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.w, xb.w, acc, 0, 0, 0);
+    }
+    // acc register q of lane (col i, half h) = dW[32ut + (q & 3) + 8 (q >> 2) + 4h][32kt + i]
+    const int lo = logical_out(l, a.K), li = logical_in(l);
+    if (c >= li) return;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int row = 32 * ut + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (row < lo) atomicAdd(a.gw[l] + (size_t)row * li + c, acc[q]);
+    }
+}
+
+struct Layout {
+    float *wf, *wb;
+    Saved sv;
+    size_t bytes;
+};
+
+size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+Layout carve(uint32_t N, void* base) {
+    Layout L{};
+    const uint32_t R = N * (uint32_t)kT;
+    L.sv.R = R;
+    L.sv.Rp = (R + kChunk - 1u) / kChunk * kChunk;
+    char* p = static_cast<char*>(base);
+    size_t off = 0;
+    auto take = [&](size_t floats) {
+        float* q = base ? reinterpret_cast<float*>(p + off) : nullptr;
+        off += al256(floats * sizeof(float));
+        return q;
+    };
+    const size_t Rp = L.sv.Rp;
+    L.wf = take(kPackFloats);
+    L.wb = take(kPackFloats);
+    L.sv.x = take((size_t)kKp[0] * Rp);
+    L.sv.h1 = take((size_t)256 * Rp);
+    L.sv.h2 = take((size_t)256 * Rp);
+    L.sv.o = take((size_t)32 * Rp);
+    L.sv.go = take((size_t)32 * Rp);
+    L.sv.g2 = take((size_t)256 * Rp);
+    L.sv.g1 = take((size_t)256 * Rp);
+    L.bytes = off;
+    return L;
+}
+
+int mask_weights(const samnerf_model* m, MaskW& mw) {
+    if (!m || !m->with_mask || m->mask_kind != 0)
+        return fail(SAMNERF_EINVAL, "mask_train: the model has no 'default' mask head");
+    if (m->mask_out < 1 || m->mask_out > 32)
+        return fail(SAMNERF_EINVAL, "mask_train: mask_out %u outside 1..32", m->mask_out);
+    for (int i = 0; i < 3; ++i) {
+        if (!m->mask_w[i]) return fail(SAMNERF_EINVAL, "mask_train: null mask_mlp weight");
+        mw.w[i] = m->mask_w[i];
+    }
+    mw.K = m->mask_out;
+    return SAMNERF_OK;
+}
+
+}  // namespace
+
+namespace samnerf {
+
+size_t mask_train_workspace_bytes(uint32_t N) { return carve(N, nullptr).bytes; }
+
+// positions / weights / geo_feat of the render's final samples (sample-major,
+// slot order) and its ray order
+int mask_train_forward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
+                       const float* geo_f, uint32_t N, RayTiles tiles, float* logits, void* ws,
+                       size_t ws_bytes, hipStream_t s) {
+    MaskW mw;
+    int rc = mask_weights(m, mw);
+    if (rc) return rc;
+    const Layout L = carve(N, ws);
+    if (ws_bytes < L.bytes)
+        return fail(SAMNERF_EWORKSPACE, "mask_train_forward: workspace needs %zu bytes, got %zu", L.bytes,
+                    ws_bytes);
+    k_mt_pack<<<div_up(kPackFloats, 256), 256, 0, s>>>(mw, L.wf, L.wb);
+    FwdArgs a;
+    a.in = SampleIn{grid, u_f, w_f, geo_f, N};
+    a.wf = L.wf;
+    a.sv = L.sv;
+    k_mt_fwd<<<L.sv.Rp / kRows, 256, 0, s>>>(a);   // rows R .. Rp saved as zeros (k_mt_dw)
+    k_mt_logits<<<div_up((uint64_t)N * mw.K, 256), 256, 0, s>>>(w_f, L.sv.o, N, mw.K, L.sv.Rp, tiles, logits);
+    return check_launch("mask_train_forward");
+}
+
+int mask_train_backward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
+                        const float* geo_f, uint32_t N, RayTiles tiles, const float* grad_logits,
+                        float* const* grad_w, float* grad_m_grid, void* ws, size_t ws_bytes, hipStream_t s) {
+    MaskW mw;
+    int rc = mask_weights(m, mw);
+    if (rc) return rc;
+    const Layout L = carve(N, ws);
+    if (ws_bytes < L.bytes)
+        return fail(SAMNERF_EWORKSPACE, "mask_train_backward: workspace needs %zu bytes, got %zu", L.bytes,
+                    ws_bytes);
+    (void)hipMemsetAsync(grad_w[0], 0, sizeof(float) * 256 * kIn0, s);
+    (void)hipMemsetAsync(grad_w[1], 0, sizeof(float) * 256 * 256, s);
+    (void)hipMemsetAsync(grad_w[2], 0, sizeof(float) * mw.K * 256, s);
+    BwdArgs b;
+    b.in = SampleIn{grid, u_f, w_f, geo_f, N};
+    b.wb = L.wb;
+    b.glog = grad_logits;
+    b.tiles = tiles;
+    b.K = mw.K;
+    b.sv = L.sv;
+    b.gemb = grad_m_grid;
+    k_mt_bwd<<<L.sv.Rp / kRows, 256, 0, s>>>(b);
+    if ((rc = check_launch("mask_train_backward"))) return rc;
+    DwArgs d;
+    d.sv = L.sv;
+    d.K = mw.K;
+    for (int i = 0; i < 3; ++i) d.gw[i] = grad_w[i];
+    k_mt_dw<<<div_up((uint64_t)kDwTiles * (L.sv.Rp / kChunk), 4), 256, 0, s>>>(d);
+    return check_launch("mask_train_backward (dW)");
+}
+
+}  // namespace samnerf

@@ -52,6 +52,13 @@ int mask_head_forward(const samnerf_model* m, const GridDesc<16>& grid, const fl
                       const float* geo_f, uint32_t N, float* out, RayTiles tiles, float* packed,
                       hipStream_t s);
 size_t mask_head_packed_floats();
+size_t mask_train_workspace_bytes(uint32_t N);
+int mask_train_forward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
+                       const float* geo_f, uint32_t N, RayTiles tiles, float* logits, void* ws,
+                       size_t ws_bytes, hipStream_t s);
+int mask_train_backward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
+                        const float* geo_f, uint32_t N, RayTiles tiles, const float* grad_logits,
+                        float* const* grad_w, float* grad_m_grid, void* ws, size_t ws_bytes, hipStream_t s);
 }  // namespace samnerf
 
 namespace {
@@ -2449,6 +2456,55 @@ int samnerf_mask_forward(const samnerf_model* m, uint32_t N, float* logits, cons
     const RayTiles tiles = g_taps_on ? RayTiles{0u, 0u} : make_ray_tiles(N, m->view_width);
     return mask_head_forward(m, gm, w.u_f, w.w_f, w.geo_f, N, logits, tiles, w.mpacked,
                              reinterpret_cast<hipStream_t>(stream));
+}
+
+size_t samnerf_mask_train_workspace_size(uint32_t N) { return mask_train_workspace_bytes(N); }
+
+// the render workspace's final samples of a 'default' mask model, checked
+static int mask_train_inputs(const samnerf_model* m, uint32_t N, const void* render_ws, size_t render_bytes,
+                             Workspace& w, GridDesc<16>& gm, const char* what) {
+    if (!m) return fail(SAMNERF_EINVAL, "%s: null model", what);
+    if (!m->with_mask || m->mask_kind != 0)
+        return fail(SAMNERF_EINVAL, "%s: model has no 'default' mask head (with_mask = 1, mask_kind = 0)", what);
+    if (m->num_steps[2] != 32) return fail(SAMNERF_EINVAL, "%s: fused path is built for 32 final samples", what);
+    if (!render_ws) return fail(SAMNERF_EINVAL, "%s: null render workspace", what);
+    w = carve(m, N, const_cast<void*>(render_ws));
+    if (render_bytes < w.bytes)
+        return fail(SAMNERF_EWORKSPACE, "%s: render workspace needs %zu bytes, got %zu", what, w.bytes,
+                    render_bytes);
+    return make_grid_desc(m->m_grid, 8, 16, gm, "m_grid");
+}
+
+int samnerf_mask_train_forward(const samnerf_model* m, uint32_t N, float* logits, const void* render_ws,
+                               size_t render_bytes, void* workspace, size_t workspace_bytes,
+                               samnerf_stream_t stream) {
+    Workspace w;
+    GridDesc<16> gm;
+    int rc = mask_train_inputs(m, N, render_ws, render_bytes, w, gm, "mask_train_forward");
+    if (rc) return rc;
+    if (N == 0) return SAMNERF_OK;
+    if (!logits || !workspace) return fail(SAMNERF_EINVAL, "mask_train_forward: null pointer");
+    const RayTiles tiles = g_taps_on ? RayTiles{0u, 0u} : make_ray_tiles(N, m->view_width);
+    return mask_train_forward(m, gm, w.u_f, w.w_f, w.geo_f, N, tiles, logits, workspace, workspace_bytes,
+                              reinterpret_cast<hipStream_t>(stream));
+}
+
+int samnerf_mask_train_backward(const samnerf_model* m, uint32_t N, const float* grad_logits,
+                                float* const* grad_mask_w, float* grad_m_grid, const void* render_ws,
+                                size_t render_bytes, void* workspace, size_t workspace_bytes,
+                                samnerf_stream_t stream) {
+    Workspace w;
+    GridDesc<16> gm;
+    int rc = mask_train_inputs(m, N, render_ws, render_bytes, w, gm, "mask_train_backward");
+    if (rc) return rc;
+    if (N == 0) return SAMNERF_OK;
+    if (!grad_logits || !grad_mask_w || !grad_m_grid || !workspace)
+        return fail(SAMNERF_EINVAL, "mask_train_backward: null pointer");
+    for (int i = 0; i < 3; ++i)
+        if (!grad_mask_w[i]) return fail(SAMNERF_EINVAL, "mask_train_backward: null gradient");
+    const RayTiles tiles = g_taps_on ? RayTiles{0u, 0u} : make_ray_tiles(N, m->view_width);
+    return mask_train_backward(m, gm, w.u_f, w.w_f, w.geo_f, N, tiles, grad_logits, grad_mask_w, grad_m_grid,
+                               workspace, workspace_bytes, reinterpret_cast<hipStream_t>(stream));
 }
 
 int samnerf_sgrid_backward(const samnerf_model* m, const float* grad_fsam, uint32_t N,

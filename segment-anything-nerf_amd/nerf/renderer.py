@@ -205,8 +205,29 @@ class NeRFRenderer(nn.Module):
                 and o.background == "last_sample" and list(o.num_steps) == [128, 64, 32]
                 and (not torch.is_tensor(bg_color) or bg_color.numel() == 1))
 
+    def _fused_mask_train_ok(self, rays_o, bg_color, perturb, return_feats, return_mask):
+        """Train mode under grad with return_mask=1 for a 'default' mask head
+        (the --with_mask step, utils.py:946-948): the HIP mask-head training
+        kernels (samnerf_amd.fused.render_mask_train)."""
+        o = self.opt
+        if not (return_mask and not return_feats and getattr(o, "with_mask", False)):
+            return False
+        from samnerf_amd.fused import mask_kind
+        return (mask_kind(self) == 0 and o.mask_mlp_type == "default" and self.fused and rays_o.is_cuda
+                and self.training and torch.is_grad_enabled() and not perturb
+                and not (getattr(o, "sum_after_mlp", False) and o.with_sam)
+                and o.background == "last_sample"
+                and list(o.num_steps) == [128, 64, 32]
+                and (not o.with_sam or o.sam_use_view_direction)
+                and (not torch.is_tensor(bg_color) or bg_color.numel() == 1))
+
     def run(self, rays_o, rays_d, bg_color=None, perturb=False, cam_near_far=None,
             update_proposal=True, return_feats=0, return_mask=0, H=None, W=None, **kwargs):
+        if self._fused_mask_train_ok(rays_o, bg_color, perturb, return_feats, return_mask):
+            from samnerf_amd.fused import FusedRenderer, render_mask_train
+            if self._fused is None or self._fused.net is not self:
+                self._fused = FusedRenderer(self)
+            return render_mask_train(self._fused, rays_o, rays_d, cam_near_far, bg_color)
         if self._fused_train_ok(rays_o, bg_color, return_feats, return_mask):
             from samnerf_amd.fused import FusedRenderer, render_rgb_train
             if self._fused is None or self._fused.net is not self:

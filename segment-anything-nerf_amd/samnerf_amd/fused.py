@@ -194,7 +194,7 @@ class FusedRenderer:
     @torch.no_grad()
     def render(self, rays_o, rays_d, cam_near_far=None, bg_color=None, rows=None,
                keep_workspace=False, feats=True, taps=False, own_workspace=False, view_width=0,
-               mask=False, perturb=False):
+               mask=False, perturb=False, mask_logits=True):
         """rays_o, rays_d [N,3] (CUDA fp32) -> dict(image [N,3], depth [N],
         weights_sum [N], samvit [N,256] if with_sam and feats).  `rows`
         (optional [N,164] tensor) receives the head input cat(f_sam, f_image,
@@ -212,7 +212,9 @@ class FusedRenderer:
         tiles per wave, same outputs bit for bit, faster gathers.
         mask=True (a 'default' mask head, fused_mask_ok): also
         instance_mask_logits [N, n_inst + redundant_instance]
-        (samnerf_mask_forward on the render's workspace).
+        (samnerf_mask_forward on the render's workspace); with
+        mask_logits=False the samples' geo_feat are stored for a later
+        samnerf_mask_train_forward and no logits are computed.
         perturb: False (default), True (draw the perturbed sample positions
         with torch's generator, perturbed_positions -- the reference's
         perturb=True), or a (bins0, u1, u2) tuple of them [N, 129], [N, 65],
@@ -279,7 +281,7 @@ class FusedRenderer:
                 ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, _ptr(cnf), n_cnf, bg, _ptr(image),
                 _ptr(depth), _ptr(wsum), _ptr(samvit), _ptr(rows), _ptr(ws), need, _stream(rays_o)),
                 "render_forward")
-            if mask:
+            if mask and mask_logits:
                 logits = torch.empty(N, int(m.mask_out), device=dev)
                 check(lib().samnerf_mask_forward(ctypes.byref(m), N, _ptr(logits), _ptr(ws), need,
                                                  _stream(rays_o)), "mask_forward")
@@ -289,7 +291,7 @@ class FusedRenderer:
             for i in range(3):
                 m.perturb[i] = None
         out = {"image": image, "depth": depth, "weights_sum": wsum}
-        if mask:
+        if mask and mask_logits:
             out["instance_mask_logits"] = logits
         if tap is not None:
             out.update({k: v.t() for k, v in tap.items()})
@@ -416,6 +418,65 @@ def render_sam_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None,
     else:
         samvit = _SamHeadTrain.apply(rows, renderer, *_head_params(net))
     return {"samvit": samvit, "image": image, "depth": depth, "weights_sum": wsum}
+
+
+# ----------------------------------------------------------- mask training --
+class _FusedMaskTrain(torch.autograd.Function):
+    """instance_mask_logits of a 'default' mask head in the --with_mask training
+    step (nerf/utils.py:941-977 -> renderer.py:392-395, :451-452), forward and
+    backward on the HIP kernels (mask_head_train.hip, exact fp32 MFMA):
+    differentiable w.r.t. m_grid.embeddings and the three mask_mlp weights,
+    the tensors the reference's loss reaches (weights and geo_feat are
+    detached there).  image / depth / weights_sum come back without gradient."""
+
+    @staticmethod
+    def forward(ctx, renderer, rays_o, rays_d, cnf, bg, m_emb, w0, w1, w2):
+        N = rays_o.shape[0]
+        dev = rays_o.device
+        out = renderer.render(rays_o, rays_d, cnf, bg, keep_workspace=True, feats=False,
+                              own_workspace=True, mask=True, mask_logits=False)
+        ws, need, m, vw = out.pop("_workspace")
+        tneed = lib().samnerf_mask_train_workspace_size(N)
+        tws = torch.empty(max(tneed, 1), dtype=torch.uint8, device=dev)
+        logits = torch.empty(N, int(m.mask_out), device=dev)
+        m.with_mask, m.view_width = 1, vw
+        check(lib().samnerf_mask_train_forward(ctypes.byref(m), N, _ptr(logits), _ptr(ws), need, _ptr(tws),
+                                               tneed, _stream(rays_o)), "mask_train_forward")
+        ctx.state = (m, vw, ws, need, tws, tneed, list(renderer._keep))
+        ctx.shapes = (m_emb.shape, w0.shape, w1.shape, w2.shape)
+        ctx.mark_non_differentiable(out["image"], out["depth"], out["weights_sum"])
+        return logits, out["image"], out["depth"], out["weights_sum"]
+
+    @staticmethod
+    def backward(ctx, g_logits, g_img, g_depth, g_wsum):
+        m, vw, ws, need, tws, tneed, _ = ctx.state
+        g = g_logits.contiguous().float()          # bound: alive through the C call
+        dev = g.device
+        g_emb = torch.zeros(ctx.shapes[0], device=dev)
+        gw = [torch.empty(sh, device=dev) for sh in ctx.shapes[1:]]
+        arr = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in gw])
+        m.with_mask, m.view_width = 1, vw
+        check(lib().samnerf_mask_train_backward(ctypes.byref(m), g.shape[0], _ptr(g), arr, _ptr(g_emb),
+                                                _ptr(ws), need, _ptr(tws), tneed, _stream(g)),
+              "mask_train_backward")
+        return (None,) * 5 + (g_emb, *gw)
+
+
+def render_mask_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None):
+    """NeRFRenderer.run in train mode under grad with return_mask=1 for a
+    'default' mask head (the mask training step's render, utils.py:946-948):
+    image, depth, weights_sum (no gradient) and instance_mask_logits with
+    gradient to m_grid and mask_mlp (_FusedMaskTrain)."""
+    net = renderer.net
+    skip = net.mask_mlp[0]
+    rays_o = rays_o.contiguous().float()
+    rays_d = rays_d.contiguous().float()
+    bg = 1.0 if bg_color is None else float(bg_color)
+    cnf = None if cam_near_far is None else cam_near_far.contiguous().float()
+    logits, image, depth, wsum = _FusedMaskTrain.apply(
+        renderer, rays_o, rays_d, cnf, bg, net.m_grid.embeddings,
+        skip.net[0].weight, skip.net[1].weight, skip.net[2].weight)
+    return {"image": image, "depth": depth, "weights_sum": wsum, "instance_mask_logits": logits}
 
 
 # ------------------------------------------------------------ RGB training --
