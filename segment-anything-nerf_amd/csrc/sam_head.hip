@@ -318,37 +318,64 @@ struct HeadArgsH {
 // boundary waits only for the step about to be read (counted vmcnt, one step
 // stays in flight across the raw barrier), per cdna_hip_programming.md
 // "Pipelining across barriers".
+// vmcnt(N) for N = 0, 4, 8, 16 (the waits are counted by hand: the DMA is inline asm)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N == 0 || N == 4 || N == 8 || N == 16, "vmcnt literal");
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+}
+
+// The weight stream in "super-steps" of KPS k-blocks (KPS x 16 KiB): NBUF
+// LDS buffers, the DMA NBUF - 1 super-steps ahead, one barrier per
+// super-step (the k-blocks of a super-step may straddle a layer boundary: the
+// barrier only guards the weight buffers).  SPREAD: the DMA pieces are issued
+// between the MFMAs (one after every second tile) instead of before them.
+template <int NBUF, bool SPREAD, int KPS>
 struct HeadStepper {
+    static constexpr int kSuper = (kSteps + KPS - 1) / KPS;
+    static constexpr int kPieces = 4 * KPS;                  // 1-KiB pieces per wave and super-step
     const uint4* __restrict__ packed;
-    uint4* Wb;            // LDS [3][kStepVec]
+    uint4* Wb;            // LDS [NBUF][KPS][kStepVec]
     int wave, lane;
-    int step;
+    int step;             // k-block
 
     // The DMA is issued from inline asm so that the compiler does not see an
     // LDS write of unknown extent in flight (it would drain vmcnt(0) before
     // every ds_read); the waits are counted by hand in run().  No ordinary
     // vector-memory load is issued inside the step loop.
-    __device__ __forceinline__ void issue(int s) {
-        const uint4* src = packed + (size_t)s * kStepVec + wave * 256 + lane;
-        const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(Wb + (s % 3) * kStepVec + wave * 256);
+    __device__ __forceinline__ void piece(int S, int c) {
+        const size_t chunk = (size_t)wave * 256 * KPS + (size_t)c * 64;
+        const uint4* src = packed + (size_t)S * KPS * kStepVec + chunk + lane;
+        const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(Wb + (S % NBUF) * KPS * kStepVec + chunk);
+        const uint32_t d = __builtin_amdgcn_readfirstlane(dst);
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(src), "s"(d)
+            : "memory");
+    }
+    __device__ __forceinline__ void issue(int S) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t d = __builtin_amdgcn_readfirstlane(dst + c * 1024u);
-            uint32_t keep;
-            asm volatile(
-                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                : "=&s"(keep)
-                : "v"(src + c * 64), "s"(d)
-                : "memory");
-        }
+        for (int c = 0; c < kPieces; ++c) piece(S, c);
+    }
+    __device__ __forceinline__ void begin() {
+#pragma unroll
+        for (int q = 0; q < NBUF - 1; ++q) issue(q);
+        wait_vm<kPieces * (NBUF - 2)>();                      // super-step 0 landed
+        __syncthreads();
     }
 
     // one k-block of the current layer for all 8 output tiles
     __device__ __forceinline__ void run(floatx16 (&acc)[8], const uint4& bh, const uint4& bl) {
-        const bool ahead = step + 2 < kSteps;
-        if (ahead) issue(step + 2);
-        const uint4* cur = Wb + (step % 3) * kStepVec + lane;
+        const int S = step / KPS, sub = step % KPS;
+        const bool ahead = S + NBUF - 1 < kSuper;
+        if (!SPREAD && sub == 0 && ahead) issue(S + NBUF - 1);
+        const uint4* cur = Wb + ((S % NBUF) * KPS + sub) * kStepVec + lane;
         uint4 fh[8], fl[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -356,16 +383,28 @@ struct HeadStepper {
             fl[t] = cur[512 + t * 64];
         }
 #pragma unroll
-        for (int t = 0; t < 8; ++t) acc[t] = mfma_f16x3(fh[t], fl[t], bh, bl, acc[t]);
-        if (ahead) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // step + 1 landed
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        for (int t = 0; t < 8; ++t) {
+            acc[t] = mfma_f16x3(fh[t], fl[t], bh, bl, acc[t]);
+            if (SPREAD && (t & 1) && ahead) {
+                __builtin_amdgcn_sched_barrier(0);
+                piece(S + NBUF - 1, 4 * sub + (t >> 1));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (sub == KPS - 1 || step + 1 == kSteps) {
+            if (ahead) wait_vm<kPieces * (NBUF - 2)>();      // super-step S + 1 landed
+            else wait_vm<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
         ++step;
     }
 };
 
-__device__ __forceinline__ float leaky(float x, bool act) { return act && x < 0.0f ? x * 0.01f : x; }
+// leaky_relu(0.01) as max(x, 0.01 x): the same value for every x (x >= 0, -0.0
+// included, gives x; x < 0 gives 0.01 x), two VALU instead of three; x is an
+// arithmetic result (canonical), so fmaxf needs no canonicalising move
+__device__ __forceinline__ float leaky(float x, bool act) { return act ? fmaxf(x, x * 0.01f) : x; }
 
 // The accumulators of a layer back to fp32 values in place: times `inv` (the
 // inverse of the column's input scale and of the weight tensor's scale: a
@@ -402,14 +441,15 @@ __device__ __forceinline__ void split_layer(const floatx16 (&acc)[8], float s, u
     }
 }
 
+template <int NBUF, bool SPREAD, int KPS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_sam_head_h16(HeadArgsH a) {
     // one LDS object (a second __shared__ object can de-pipeline the DMA
     // waits): 3 x 16 KiB weight steps, then biases [5][256], LN weight / bias,
     // the weight tensors' inverse scales [5]
-    __shared__ uint4 smem[3 * kStepVec + (7 * 256 + 8) / 4];
+    __shared__ uint4 smem[NBUF * KPS * kStepVec + (7 * 256 + 8) / 4];
     uint4* Wb = smem;
-    float* Bs = reinterpret_cast<float*>(smem + 3 * kStepVec);
+    float* Bs = reinterpret_cast<float*>(smem + NBUF * KPS * kStepVec);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int j = lane & 31, h = lane >> 5;
     const uint32_t ray = blockIdx.x * kRaysV5 + wave * 32u + j;
@@ -460,11 +500,8 @@ k_sam_head_h16(HeadArgsH a) {
     uint4 xh[kXkb], xl[kXkb];
     Scale2 sc = scale_of_max(xmax);
     load_x(sc.s, xh, xl);
-    HeadStepper st{a.packed, Wb, wave, lane, 0};
-    st.issue(0);
-    st.issue(1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");          // step 0 landed
-    __syncthreads();
+    HeadStepper<NBUF, SPREAD, KPS> st{a.packed, Wb, wave, lane, 0};
+    st.begin();
 
     floatx16 acc[8];
     uint4 ah[kHkb], al[kHkb];
@@ -543,6 +580,294 @@ k_sam_head_h16(HeadArgsH a) {
         }
 }
 
+#ifdef SAMNERF_DIAG_VARIANTS
+// ============================================================ f16x3, paired
+// The same arithmetic as k_sam_head_h16 (every accumulator tile sees the same
+// f16x3 MFMA products in the same order, the same scales, the same finishing
+// and LayerNorm sums: bit-identical output) at 2 or 4 waves per SIMD instead
+// of 1: a 32-ray group's 8 output tiles are shared by WPG = 8 / TPW waves,
+// each holding TPW accumulator tiles, and the group's B operands (the layer
+// input, hi / lo fp16 fragments) live in LDS, written once per layer by the
+// waves that produced them and read by all of the group's waves each step.
+// The x rows (layer 0 and the skip input of layer 2) are read and split per
+// k-block, one k-block ahead.  While one wave waits on LDS, the barrier or
+// its DMA issue, the other waves of its SIMD issue MFMAs.
+//   LDS (one object, 160 KiB): 2 weight steps of 16 KiB (the step being read
+//   and the one in flight) + 4 groups x 32 KiB of B fragments; biases and
+//   LayerNorm parameters are read from global memory (L2) at layer ends.
+//   Layer boundary: finish the own tiles (bias, leaky_relu), exchange the
+//   per-ray max through the weight buffer that is idle between the layer's
+//   last step and the next step's DMA, split at the common scale, write the
+//   B fragments; two barriers.
+template <int TPW>
+struct PairCfg {
+    static constexpr int WPG = 8 / TPW;                  // waves per 32-ray group
+    static constexpr int NW = 4 * WPG;                   // waves per block (4 groups)
+    static constexpr int NT = 64 * NW;
+    static constexpr int PIECES = 16 / NW;               // 1-KiB DMA pieces per wave and step
+};
+constexpr int kBVec = kHkb * 2 * 64;                     // uint4 of one group's B fragments (32 KiB)
+constexpr int kPairSmemVec = 2 * kStepVec + 4 * kBVec;   // 10,240 uint4 = 160 KiB
+
+__device__ __forceinline__ void lds_dma16(const uint4* src, uint32_t lds_byte_addr) {
+    const uint32_t d = __builtin_amdgcn_readfirstlane(lds_byte_addr);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(d)
+        : "memory");
+}
+// every LDS access of this wave done, then the workgroup barrier
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <int TPW>
+__global__ void __launch_bounds__(PairCfg<TPW>::NT)
+__attribute__((amdgpu_waves_per_eu(PairCfg<TPW>::WPG, PairCfg<TPW>::WPG)))
+k_sam_head_h16p(HeadArgsH a) {
+    using C = PairCfg<TPW>;
+    __shared__ uint4 smem[kPairSmemVec];
+    uint4* const Wb = smem;                                   // [2][kStepVec] weight steps
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int grp = wave / C::WPG, part = wave % C::WPG;
+    const int t0 = part * TPW;                                // first own output tile
+    uint4* const Bg = smem + 2 * kStepVec + grp * kBVec;      // [kb][hi/lo][lane]
+    const int j = lane & 31, h = lane >> 5;
+    const uint32_t ray = blockIdx.x * kRaysV5 + grp * 32u + j;
+    const bool live = ray < a.N;
+    const float* xr = a.rows + (size_t)(live ? ray : 0u) * kRowIn;
+
+    // weight step s -> buffer s & 1; this wave moves PIECES KiB of it
+    auto issue = [&](int s) {
+        const uint4* src = a.packed + (size_t)s * kStepVec + wave * (64 * C::PIECES) + lane;
+        const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(Wb + (s & 1) * kStepVec + wave * (64 * C::PIECES));
+#pragma unroll
+        for (int c = 0; c < C::PIECES; ++c) lds_dma16(src + c * 64, dst + c * 1024u);
+    };
+    // raw x columns 16kb + 8h .. +7 of the row (masked where consumed, so the
+    // loads stay in flight across a step)
+    auto xload = [&](int kb, float4& p, float4& q) {
+        if (kb < kXkb - 1) {
+            p = *reinterpret_cast<const float4*>(xr + 16 * kb + 8 * h);
+            q = *reinterpret_cast<const float4*>(xr + 16 * kb + 8 * h + 4);
+        } else {                                              // columns 160..163 (h = 0) only
+            p = *reinterpret_cast<const float4*>(xr + 160);
+            q = p;
+        }
+    };
+    auto xvals = [&](int kb, const float4& p, const float4& q, float (&v)[8]) {
+        v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w;
+        v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
+        const int c0 = 16 * kb + 8 * h;
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            if (!live || c0 + m >= kIn) v[m] = 0.0f;          // column 163 of a row is padding
+    };
+
+    int s = 0;                                                // next weight step
+    issue(0);
+    float xmax = 0.0f;
+#pragma unroll
+    for (int kb = 0; kb < kXkb; ++kb) {
+        float4 p, q;
+        float v[8];
+        xload(kb, p, q);
+        xvals(kb, p, q, v);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) xmax = fmaxf(xmax, fabsf(v[m]));
+    }
+    xmax = fmaxf(xmax, __shfl_xor(xmax, 32));
+    float Wi[5];
+#pragma unroll
+    for (int l = 0; l < 5; ++l) Wi[l] = exp2i(-a.kexp[l]);
+    Scale2 sc = scale_of_max(xmax);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // step 0 landed
+    lds_barrier();
+
+    floatx16 acc[TPW];
+    auto zero = [&]() {
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) acc[t] = floatx16{};
+    };
+    // one k-block of the current layer for the own tiles; ends with step s + 1
+    // landed and visible, buffer s & 1 free
+    auto mma = [&](const uint4& bh, const uint4& bl) {
+        const uint4* cur = Wb + (s & 1) * kStepVec + lane;
+        uint4 fh[TPW], fl[TPW];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            fh[t] = cur[(t0 + t) * 64];
+            fl[t] = cur[512 + (t0 + t) * 64];
+        }
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) acc[t] = mfma_f16x3(fh[t], fl[t], bh, bl, acc[t]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        ++s;
+    };
+    // layer input x (layer 0, or the skip part of layer 2) at scale sc.s
+    auto x_segment = [&]() {
+        float4 p, q;
+        xload(0, p, q);
+#pragma unroll
+        for (int kb = 0; kb < kXkb; ++kb) {
+            float v[8];
+            xvals(kb, p, q, v);                               // waits for this k-block's loads only
+            uint4 bh, bl;
+            split8_f16(v, sc.s, bh, bl);
+            if (s + 1 < kSteps) issue(s + 1);
+            if (kb + 1 < kXkb) xload(kb + 1, p, q);
+            mma(bh, bl);
+        }
+    };
+    auto h_segment = [&]() {
+#pragma unroll
+        for (int kb = 0; kb < kHkb; ++kb) {
+            const uint4 bh = Bg[(2 * kb) * 64 + lane], bl = Bg[(2 * kb + 1) * 64 + lane];
+            if (s + 1 < kSteps) issue(s + 1);
+            mma(bh, bl);
+        }
+    };
+    // bias (+ leaky_relu) of the own tiles, the ray's max |value| over all 8
+    // tiles (with `extra`), the common scale, and the next layer's B fragments
+    auto next = [&](int layer, float extra) {
+        const float inv = sc.inv * Wi[layer];
+        const float* bias = a.b[layer];
+        float m = 0.0f;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t)
+#pragma unroll
+            for (int mm = 0; mm < 4; ++mm) {
+                const float4 bb = *reinterpret_cast<const float4*>(bias + 32 * (t0 + t) + 8 * mm + 4 * h);
+                const float b4[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    acc[t][4 * mm + e] = leaky(__builtin_fmaf(acc[t][4 * mm + e], inv, b4[e]), true);
+#pragma unroll
+                for (int e = 0; e < 4; e += 2) m = max_abs3(m, acc[t][4 * mm + e], acc[t][4 * mm + e + 1]);
+            }
+        m = fmaxf(m, __shfl_xor(m, 32));
+        float* X = reinterpret_cast<float*>(Wb + ((s + 1) & 1) * kStepVec);   // idle until step s + 1's DMA
+        if (h == 0) X[(grp * C::WPG + part) * 32 + j] = m;
+        lds_barrier();
+        float mm2 = 0.0f;
+#pragma unroll
+        for (int p = 0; p < C::WPG; ++p) mm2 = fmaxf(mm2, X[(grp * C::WPG + p) * 32 + j]);
+        sc = scale_of_max(fmaxf(mm2, extra));
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            float v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = acc[t][q];
+            uint4 hi, lo;
+            split8_f16(v, sc.s, hi, lo);
+            Bg[(2 * (2 * (t0 + t))) * 64 + lane] = hi;
+            Bg[(2 * (2 * (t0 + t)) + 1) * 64 + lane] = lo;
+            split8_f16(v + 8, sc.s, hi, lo);
+            Bg[(2 * (2 * (t0 + t) + 1)) * 64 + lane] = hi;
+            Bg[(2 * (2 * (t0 + t) + 1) + 1) * 64 + lane] = lo;
+        }
+        lds_barrier();
+    };
+
+    zero();                                                   // layer 0: W0 . x
+    x_segment();
+    next(0, 0.0f);
+    zero();                                                   // layer 1
+    h_segment();
+    next(1, xmax);                                            // layer 2 reads cat(h, x): one scale
+    zero();                                                   // layer 2: W2 . cat(h, x)
+    x_segment();
+    h_segment();
+    next(2, 0.0f);
+    zero();                                                   // layer 3
+    h_segment();
+    next(3, 0.0f);
+    zero();                                                   // layer 4 (no activation)
+    h_segment();
+
+    // layer 4 outputs (bias, no activation) into the group's B region as
+    // fp32, [tile][register quad][lane]; every wave of the group then forms
+    // the LayerNorm sums over all 8 tiles in k_sam_head_h16's order
+    float4* Y = reinterpret_cast<float4*>(Bg);
+    {
+        const float inv = sc.inv * Wi[4];
+        const float* bias = a.b[4];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t)
+#pragma unroll
+            for (int mm = 0; mm < 4; ++mm) {
+                const float4 bb = *reinterpret_cast<const float4*>(bias + 32 * (t0 + t) + 8 * mm + 4 * h);
+                float4 y;
+                y.x = __builtin_fmaf(acc[t][4 * mm + 0], inv, bb.x);
+                y.y = __builtin_fmaf(acc[t][4 * mm + 1], inv, bb.y);
+                y.z = __builtin_fmaf(acc[t][4 * mm + 2], inv, bb.z);
+                y.w = __builtin_fmaf(acc[t][4 * mm + 3], inv, bb.w);
+                Y[((t0 + t) * 4 + mm) * 64 + lane] = y;
+            }
+    }
+    lds_barrier();
+    // (one tile's values at a time: the empty asm keeps the compiler from
+    // holding all 128 of the lane's values in registers across the loops)
+    double sum = 0.0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+            const float4 y = Y[(t * 4 + mm) * 64 + lane];
+            sum += (double)y.x;
+            sum += (double)y.y;
+            sum += (double)y.z;
+            sum += (double)y.w;
+        }
+        asm volatile("" ::: "memory");
+    }
+    sum += __shfl_xor(sum, 32);
+    const double mean = sum / 256.0;
+    double var = 0.0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+            const float4 y = Y[(t * 4 + mm) * 64 + lane];
+            const float yy[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const double dlt = (double)yy[e] - mean;
+                var += dlt * dlt;
+            }
+        }
+        asm volatile("" ::: "memory");
+    }
+    var += __shfl_xor(var, 32);
+    const float rstd = (float)(1.0 / sqrt(var / 256.0 + 1e-5));
+    const float mf = (float)mean;
+    if (!live) return;
+    float* o = a.out + (size_t)ray * 256;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+            const int u = 32 * (t0 + t) + 8 * mm + 4 * h;
+            const float4 v = Y[((t0 + t) * 4 + mm) * 64 + lane];
+            const float4 lw = *reinterpret_cast<const float4*>(a.ln_w + u);
+            const float4 lb = *reinterpret_cast<const float4*>(a.ln_b + u);
+            float4 y;
+            y.x = ((v.x - mf) * rstd) * lw.x + lb.x;
+            y.y = ((v.y - mf) * rstd) * lw.y + lb.y;
+            y.z = ((v.z - mf) * rstd) * lw.z + lb.z;
+            y.w = ((v.w - mf) * rstd) * lw.w + lb.w;
+            *reinterpret_cast<float4*>(o + u) = y;
+        }
+}
+
+#endif  // SAMNERF_DIAG_VARIANTS
+
 }  // namespace
 
 size_t sam_head_packed_floats() {
@@ -569,7 +894,24 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         a.ln_w = m->ln_w;
         a.ln_b = m->ln_b;
         a.out = samvit;
-        k_sam_head_h16<<<div_up(N, (uint32_t)kRaysV5), 256, 0, s>>>(a);
+        const uint32_t blocks = div_up(N, (uint32_t)kRaysV5);
+#ifdef SAMNERF_DIAG_VARIANTS
+        // measured forms (tools/head_bench.py, profiles/r3_head_forms.txt), all
+        // bit-identical; 1 = the round-2 schedule (DMA before the MFMAs), 2 / 3
+        // = the paired 2 / 4-waves-per-SIMD forms (0.78 / 0.84 vs 0.72 ms),
+        // 5 / 7 / 8 = two k-blocks per barrier, 6 / 8 = four buffers
+        const char* v = diag_env("SAMNERF_HEAD_V");
+        const int form = v ? atoi(v) : 4;
+        if (form == 1) k_sam_head_h16<3, false, 1><<<blocks, 256, 0, s>>>(a);
+        else if (form == 2) k_sam_head_h16p<4><<<blocks, PairCfg<4>::NT, 0, s>>>(a);
+        else if (form == 3) k_sam_head_h16p<2><<<blocks, PairCfg<2>::NT, 0, s>>>(a);
+        else if (form == 5) k_sam_head_h16<3, false, 2><<<blocks, 256, 0, s>>>(a);
+        else if (form == 6) k_sam_head_h16<4, true, 1><<<blocks, 256, 0, s>>>(a);
+        else if (form == 7) k_sam_head_h16<3, true, 2><<<blocks, 256, 0, s>>>(a);
+        else if (form == 8) k_sam_head_h16<4, true, 2><<<blocks, 256, 0, s>>>(a);
+        else
+#endif
+        k_sam_head_h16<3, true, 1><<<blocks, 256, 0, s>>>(a);   // 3 buffers, DMA between the MFMAs
         return check_launch("sam_head_h16");
     }
     const uint32_t nvec = 8u * kTotalGroups * 64u;
