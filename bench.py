@@ -406,6 +406,51 @@ def rgb_train_steps(dev, steps, warmup, fused=True, h=64, w=128):
     return (time.perf_counter() - t0) * 1e3 / steps, float(loss.detach())
 
 
+def mask_train_steps(dev, steps, warmup, fused=True, n_rays=4096):
+    """One --with_mask training step (utils.py:941-977; main.py:255-262: only
+    m_grid and mask_mlp train): 4,096 rays at random pixels of a 512^2 view of
+    a 'default'-head mask model (n_inst 2) at the reference's table sizes,
+    render with return_mask=1, softmax / clamp / NLL of random labels,
+    backward, Adam(lr 1e-2, eps 1e-15).  fused: the HIP mask-training kernels
+    (mask_head_train.hip); else the torch path (run_torch + autograd with the
+    drop-in encoder kernels).  Returns (ms per step, final loss)."""
+    from nerf.network import NeRFNetwork, default_opt
+    from samnerf_amd import ops, synth
+    from samnerf_amd.optim import FusedAdam
+    from samnerf_amd.train import mask_train_step
+    spec = synth.ModelSpec(with_sam=False, with_mask=True, mask_type="default", sum_after_mlp=False)
+    params = synth.make_params(spec, seed=5, emb_scale=0.5)
+    net = NeRFNetwork(default_opt(with_sam=False, with_mask=True, mask_mlp_type="default", n_inst=2))
+    net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    net = net.to(dev).train()
+    net.fused = fused
+    for k, p in net.named_parameters():
+        p.requires_grad = k.startswith("m_grid") or k.startswith("mask_mlp")
+    opt = FusedAdam([p for p in net.parameters() if p.requires_grad], lr=1e-2, eps=1e-15)
+    pose, intr = synth.gui_camera(512, 512)
+    ro, rd = ops.get_rays(pose, intr, 512, 512, device=dev)
+    inds = torch.randint(0, 512 * 512, (n_rays,), generator=torch.Generator().manual_seed(6)).to(dev)
+    ro, rd = ro[inds].contiguous(), rd[inds].contiguous()
+    gt = torch.randint(0, 2, (n_rays,), generator=torch.Generator().manual_seed(7)).to(dev)
+
+    def step():
+        _, loss = mask_train_step(net, ro, rd, gt)
+        for p in net.parameters():
+            p.grad = None
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3 / steps, float(loss.detach())
+
+
 RGB_TRAIN_WHAT = {
     "dtype": "fp32 throughout (forward in the fused render's op order, grid_mlp / view_mlp exact fp32; "
              "hand-written backward; grid gradients by fp32 atomics)",
@@ -855,6 +900,21 @@ def main():
                              "steps": 20, "warmup": 5, "final_loss": lossr,
                              "torch_path_ms_per_step": msr_t, "speedup_vs_torch_path": msr_t / msr,
                              **RGB_TRAIN_WHAT}
+
+    if not args.no_alt and world == 1 and args.rank_share <= 1:
+        # the --with_mask training step on the HIP mask-training
+        # kernels, the torch path beside it
+        msm, lossm = mask_train_steps(dev, 20, 5, fused=True)
+        msm_t, _ = mask_train_steps(dev, 6, 2, fused=False)
+        side["mask_train"] = {
+            "ms_per_step": msm, "steps_per_s": 1e3 / msm, "rays_per_s": 4096 * 1e3 / msm, "steps": 20,
+            "warmup": 5, "final_loss": lossm, "torch_path_ms_per_step": msm_t,
+            "speedup_vs_torch_path": msm_t / msm,
+            "dtype": "fp32 (render forward in the fused op order; mask head forward + backward on exact "
+                     "fp32 MFMA, mask_head_train.hip; m_grid scatter and dW by fp32 atomics)",
+            "what": "--with_mask training step (utils.py:941-977): 4096 rays at random pixels of a 512x512 "
+                    "view, 'default' head (m_grid L16C8 2^19 + SkipConnMLP 143->256->256->2), softmax / "
+                    "clamp / NLL, backward, Adam over m_grid + mask_mlp"}
 
     if rank == 0:
         rec = {

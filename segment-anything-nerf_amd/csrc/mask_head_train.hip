@@ -272,23 +272,29 @@ __global__ void __launch_bounds__(256) k_mt_bwd(BwdArgs a) {
     // dx of the m_grid part (tiles 0..7 of 9; geo_feat is detached) into Q
     bwd_layer<0, 8>(a.wb, P, w, lane, [&](int v, int j, float d) { Q[v * kRows + j] = d; });
     __syncthreads();
-    // trilinear scatter: thread (level l, row j), 8 corners x 8 channels
-    const int j = tid & 15, l = tid >> 4;
-    const uint32_t r = r0 + (uint32_t)j;
-    if (r >= sv.R) return;
-    const uint32_t k = r / N, s = r % N;
-    const float* up = a.in.u + (size_t)k * 3u * N + s;
-    uint32_t off[8];
-    float cw[8];
-    corner_rows<8>(sLv[l], up[0], up[N], up[2u * N], off, cw);
-    float g[8];
+    // trilinear scatter: one (row, level) per wave-instruction, lane = (corner
+    // c, channel ch): each float atomic instruction adds to 8 corner rows of
+    // 32 contiguous bytes (a thread per (row, level) with 64 atomics of its
+    // own sent 64 lanes to 64 different rows: ~17x slower per byte,
+    // MI355X_MICROARCH.md "Global float atomics")
+    const int c = lane >> 3, ch = lane & 7;
+    for (int it = w; it < kRows * 16; it += 4) {              // 16 rows x 16 levels over 4 waves
+        const int j = it & 15, l = it >> 4;
+        const uint32_t r = r0 + (uint32_t)j;
+        if (r >= sv.R) continue;                              // wave-uniform
+        const uint32_t k = r / N, s = r % N;
+        const float* up = a.in.u + (size_t)k * 3u * N + s;
+        uint32_t off[8];
+        float cw[8];
+        corner_rows<8>(sLv[l], up[0], up[N], up[2u * N], off, cw);
+        uint32_t o = off[0];
+        float wc = cw[0];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) g[c] = Q[(8 * l + c) * kRows + j];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        float* row = a.gemb + off[c] / 4u;
-#pragma unroll
-        for (int ch = 0; ch < 8; ++ch) atomicAdd(row + ch, cw[c] * g[ch]);
+        for (int q = 1; q < 8; ++q) {
+            o = c == q ? off[q] : o;
+            wc = c == q ? cw[q] : wc;
+        }
+        atomicAdd(a.gemb + o / 4u + ch, wc * Q[(8 * l + ch) * kRows + j]);
     }
 }
 

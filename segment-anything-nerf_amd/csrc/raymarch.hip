@@ -521,6 +521,26 @@ struct FinalArgs {
     const float* aeff; // [K][240] E, blocks g 32 | h1 64 | h2 64 | o3 16 | v1 32 | v2 32 (k_mask_eff)
     float* mlog;       // [N][K] instance_mask_logits (ray order)
     uint32_t mask_out;
+    // N1 ray compaction (EXIT form): this pass marches samples [i0, i1) of
+    // the slots in list_in (n_in of them, a device count; null: every slot);
+    // a ray still open at i1 keeps its running sums in st_d / st_f and sets
+    // its bit in its wave's ballot mask (wave_mask, one 64-bit word per
+    // wave); k_n1_scan / k_n1_scatter then build the next pass's list in
+    // slot order (so a compacted wave's rays stay neighbours in the image).
+    // The others finish in this pass (outputs written, later samples
+    // zeroed).  Defaults: i0 0, i1 T, no lists.
+    int i0, i1;
+    const uint32_t* list_in;
+    const uint32_t* n_in;
+    uint64_t* wave_mask;   // [ceil(N / 32)] (non-null: a non-final pass)
+    struct {               // host side: the passes' buffers (workspace, t_thresh > 0)
+        uint32_t* list;    // [2][N] slot lists
+        uint32_t* cnt;     // [2] their lengths
+        uint64_t* mask;    // [ceil(N / 32)] ballot masks
+        uint32_t* base;    // [ceil(N / 32)] scan
+    } n1;
+    double* st_d;      // [3][N] optical depth, sum w, sum w t (slot order)
+    float* st_f;       // [16][N] sum w * grid_mlp rows
 };
 
 constexpr int kAeff = 240;          // columns of the adaptive heads' effective matrix
@@ -875,10 +895,14 @@ k_final(FinalArgs a) {
     const int seg = jj / R;                              // slot of this column
     const uint32_t chunk = xcd_chunk(blockIdx.x, (a.N + 4u * R - 1u) / (4u * R));
     const uint32_t ray0 = chunk * (4u * R) + wave * (uint32_t)R;
-    if (ray0 >= a.N) return;                             // wave-uniform
-    const uint32_t r = ray0 + (uint32_t)(jj % R);
-    const bool live = r < a.N;
-    const uint32_t rr = live ? r : a.N - 1;
+    // EXIT with a list: the wave's columns are list entries ray0 .. (slots)
+    const bool listed = EXIT && a.list_in != nullptr;
+    const uint32_t n_act = listed ? *a.n_in : a.N;
+    if (ray0 >= n_act) return;                           // wave-uniform
+    const uint32_t c_idx = ray0 + (uint32_t)(jj % R);
+    const bool live = c_idx < n_act;
+    const uint32_t rr = listed ? a.list_in[live ? c_idx : n_act - 1] : (live ? c_idx : a.N - 1);
+    const uint32_t r = listed ? rr : c_idx;              // this column's slot
     const bool sample_writer = live && hh == 0;          // u_out / w_out of this segment
     const bool writer = sample_writer && seg == 0;       // per-ray outputs
     const uint32_t N = a.N;
@@ -893,12 +917,20 @@ k_final(FinalArgs a) {
             d[c] = a.rays_d[(size_t)ray * 3 + c];
         }
     }
+    const int i_begin = EXIT ? a.i0 : 0, i_end = EXIT ? a.i1 : TS;
     const float sn = a.snf[rr], sf = a.snf[N + rr];
-    float rb_prev = real_bin(sn, sf, a.bins_in[(size_t)seg * N + rr]);
+    float rb_prev = real_bin(sn, sf, a.bins_in[(size_t)(i_begin * S + seg) * N + rr]);
     double cum = 0.0, wsum = 0.0, depth = 0.0;            // cum: optical depth before this step
     float fg[8];                                          // sum_k w_k * grid_mlp rows (acc layout)
 #pragma unroll
     for (int q = 0; q < 8; ++q) fg[q] = 0.0f;
+    if (EXIT && i_begin > 0) {                            // N1 compaction: a later pass
+        cum = a.st_d[rr];
+        wsum = a.st_d[N + rr];
+        depth = a.st_d[2 * (size_t)N + rr];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) fg[q] = a.st_f[(size_t)(q + 8 * hh) * N + rr];
+    }
     float sh[16];                                         // SH(4) of the normalised direction
     auto sh_of_ray = [&]() {
         float dx = d[0], dy = d[1], dz = d[2];
@@ -952,7 +984,7 @@ k_final(FinalArgs a) {
     // saves a division), recomputed from the bins otherwise
     auto position = [&](int i, float& rbp, float& rbn, float& ux, float& uy, float& uz) {
         const int k = i * S + seg;
-        if (S > 1 || i == 0) rbp = real_bin(sn, sf, a.bins_in[(size_t)k * N + rr]);
+        if (S > 1 || i == i_begin) rbp = real_bin(sn, sf, a.bins_in[(size_t)k * N + rr]);
         rbn = real_bin(sn, sf, a.bins_in[(size_t)(k + 1) * N + rr]);
         const float t = (rbn + rbp) / 2.0f;
         float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
@@ -975,8 +1007,8 @@ k_final(FinalArgs a) {
         gather_issue_c2<4>(emb, dl, p_ux, p_uy, p_uz, pre, pf_kinds(kPre));
     }
 
-    int exit_at = TS;                                     // EXIT: first dropped step
-    for (int i = 0; i < TS; ++i) {
+    int exit_at = i_end;                                  // EXIT: first step not marched
+    for (int i = i_begin; i < i_end; ++i) {
         const int k = i * S + seg;
         float rb_next, ux, uy, uz;
         if constexpr (PF) {
@@ -1217,7 +1249,7 @@ k_final(FinalArgs a) {
         // positions as the grid centre (in range for any gather).  Nothing of
         // the sample is held past its MFMAs for this (holding the position
         // spilled 16 more VGPRs at 3 waves per SIMD).
-        if (EXIT && i + 1 < TS) {
+        if (EXIT && i + 1 < i_end) {
             const bool open = live && !(cum > (double)a.exit_depth);
             if (__builtin_amdgcn_ballot_w64(open) == 0) {
                 exit_at = i + 1;
@@ -1225,7 +1257,23 @@ k_final(FinalArgs a) {
             }
         }
     }
-    if (EXIT && sample_writer) {
+    // N1 compaction: rays still open at the end of a non-final pass go on
+    bool cont = false;
+    if constexpr (EXIT) {
+        cont = a.wave_mask != nullptr && live && !(cum > (double)a.exit_depth);
+        if (cont) {                                      // running sums for the next pass
+            if (hh == 0) {
+                a.st_d[rr] = cum;
+                a.st_d[N + rr] = wsum;
+                a.st_d[2 * (size_t)N + rr] = depth;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a.st_f[(size_t)(q + 8 * hh) * N + rr] = fg[q];
+        }
+        const uint64_t m = __builtin_amdgcn_ballot_w64(cont && hh == 0);   // lanes 0..31 = the rays
+        if (a.wave_mask && lane == 0) a.wave_mask[ray0 / 32u] = m;
+    }
+    if (EXIT && sample_writer && !cont) {
         for (int i2 = exit_at; i2 < TS; ++i2) {
             const int k2 = i2 * S + seg;
             a.w_out[(size_t)k2 * N + r] = 0.0f;
@@ -1265,6 +1313,7 @@ k_final(FinalArgs a) {
         }
     }
 
+    if (EXIT && __builtin_amdgcn_ballot_w64(live && !cont) == 0) return;   // nothing finishes here
     // view MLP on the accumulated colour features: rows 1..15 of fg are
     // f_image[0..14] (geo), f_image[15..30] = sh * sum(w) (colour = cat(geo, sh)
     // with sh constant along the ray, renderer.py:338; a rounding-level
@@ -1312,7 +1361,7 @@ k_final(FinalArgs a) {
             if (live && hh == 0) a.mlog[(size_t)a.tiles(r) * K + c] = sacc;
         }
     }
-    if (!live || seg != 0) return;
+    if (!live || seg != 0 || cont) return;
     const uint32_t ray = a.tiles(r);                     // per-ray outputs in ray order
     float* row = a.rows ? a.rows + (size_t)ray * kRow : nullptr;
     if (row) {                                 // geo units owned by this half-wave
@@ -1836,6 +1885,12 @@ struct Workspace {
     float* mpacked;    // mask head weight stream (with_mask, kind 0)
     float* aeff;       // [K][240] adaptive heads' effective matrix (with_mask, kinds 1-2)
     float* mlog;       // [N][K] adaptive heads' logits (with_mask, kinds 1-2)
+    uint32_t* n1_list; // [2][N] N1 compaction: the passes' slot lists (t_thresh > 0)
+    uint32_t* n1_cnt;  // [2] their lengths
+    uint64_t* n1_mask; // [ceil(N / 32)] the waves' ballot masks of open rays
+    uint32_t* n1_base; // [ceil(N / 32)] their exclusive scan
+    double* n1_std;    // [3][N] running optical depth / sum w / sum w t of open rays
+    float* n1_stf;     // [16][N] running sum w * grid_mlp rows
     size_t bytes;
 };
 
@@ -1968,6 +2023,63 @@ __global__ void __launch_bounds__(256) k_mask_eff(EffArgs a) {
 
 // k_final by ray-segment form S and prefetch; EXACT = the exact-fp32
 // grid_mlp of head_mode 1.  The non-prefetching forms by segment count:
+// N1 compaction between k_final passes: exclusive scan of the waves' open
+// counts (popcount of their ballot masks; one workgroup, the waves of the
+// pass in order), then each wave's open slots are written at its base in
+// lane order: the next list keeps slot order (the image's tile order).
+__global__ void __launch_bounds__(1024) k_n1_scan(const uint64_t* __restrict__ mask, const uint32_t* n_in,
+                                                  uint32_t n_all, uint32_t* __restrict__ base,
+                                                  uint32_t* __restrict__ n_out) {
+    __shared__ uint32_t part[1024];
+    const uint32_t n = n_in ? *n_in : n_all;
+    const uint32_t nw = (n + 31u) / 32u, tid = threadIdx.x;
+    const uint32_t per = (nw + 1023u) / 1024u, b0 = tid * per, b1 = min(b0 + per, nw);
+    uint32_t sum = 0;
+    for (uint32_t i = b0; i < b1; ++i) sum += (uint32_t)__popcll(mask[i]);
+    part[tid] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024u; off <<= 1) {          // inclusive scan (Hillis-Steele)
+        const uint32_t v = tid >= off ? part[tid - off] : 0u;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[tid] - sum;                           // exclusive
+    for (uint32_t i = b0; i < b1; ++i) {
+        base[i] = run;
+        run += (uint32_t)__popcll(mask[i]);
+    }
+    if (tid == 1023u) *n_out = part[1023];
+}
+
+__global__ void __launch_bounds__(256) k_n1_scatter(const uint64_t* __restrict__ mask,
+                                                    const uint32_t* __restrict__ base,
+                                                    const uint32_t* __restrict__ list_in,
+                                                    const uint32_t* n_in, uint32_t n_all,
+                                                    uint32_t* __restrict__ list_out) {
+    const uint32_t n = n_in ? *n_in : n_all;
+    const uint32_t c = blockIdx.x * 256u + threadIdx.x;       // list entry (32 per wave of k_final)
+    if (c >= n) return;
+    const uint32_t w = c / 32u, l = c % 32u;
+    const uint64_t m = mask[w];
+    if (!((m >> l) & 1ull)) return;
+    list_out[base[w] + (uint32_t)__popcll(m & ((1ull << l) - 1ull))] = list_in ? list_in[c] : c;
+}
+
+// N1: sample chunks of the compacted march (k_final passes; the diagnostic
+// build's SAMNERF_N1_CHUNKS).  1 = the wave-level exit alone, the product
+// form: on the opaque-sphere 512^2 view the compacted passes measured slower
+// -- k_final 0.97 ms in one pass, 1.37 ms in 2 passes (0.61 + 0.77), 1.53 ms
+// in 4 (0.32 + 0.35 + 0.54 + 0.31), profiles/r3_n1_compaction.txt: a
+// compacted wave's rays come from several 8 x 4 pixel tiles, its gathers
+// touch more distinct rows, and each pass re-reads the state and refills
+// the weights, while the wave exit keeps every wave's rays neighbours.
+inline int n1_chunks() {
+    const char* v = diag_env("SAMNERF_N1_CHUNKS");
+    const int c = v ? atoi(v) : 1;
+    return (c == 1 || c == 2 || c == 4 || c == 8) ? c : 1;
+}
+
 template <bool EXACT, bool EXIT, bool GEO, bool SA>
 void launch_final_np(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa) {
     if (seg == 1) k_final<32, 1, false, EXACT, EXIT, GEO, SA><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
@@ -1994,7 +2106,23 @@ void launch_final(int seg, bool pf, uint32_t N, hipStream_t s, const FinalArgs& 
         return;
     }
     if (fa.exit_depth < INFINITY) {                      // N1 (no prefetch form)
-        launch_final_np<EXACT, true, false, false>(seg, N, s, fa);
+        const int chunks = seg == 1 && fa.n1.list ? n1_chunks() : 1;
+        const int cs = 32 / chunks;
+        uint32_t* list[2] = {fa.n1.list, fa.n1.list + N};
+        for (int p = 0; p < chunks; ++p) {              // ray compaction between sample chunks
+            FinalArgs f = fa;
+            f.i0 = p * cs;
+            f.i1 = (p + 1) * cs;
+            f.list_in = p ? list[(p - 1) & 1] : nullptr;
+            f.n_in = p ? fa.n1.cnt + ((p - 1) & 1) : nullptr;
+            f.wave_mask = p + 1 < chunks ? fa.n1.mask : nullptr;
+            launch_final_np<EXACT, true, false, false>(chunks > 1 ? 1 : seg, N, s, f);
+            if (p + 1 < chunks) {
+                k_n1_scan<<<1, 1024, 0, s>>>(fa.n1.mask, f.n_in, N, fa.n1.base, fa.n1.cnt + (p & 1));
+                k_n1_scatter<<<div_up(N, 256), 256, 0, s>>>(fa.n1.mask, fa.n1.base, f.list_in, f.n_in, N,
+                                                            list[p & 1]);
+            }
+        }
         return;
     }
     if (seg == 1) {
@@ -2034,6 +2162,13 @@ Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
     w.mpacked = take(mdef ? mask_head_packed_floats() : 0);
     w.aeff = take(madapt ? (size_t)32 * kAeff : 0);
     w.mlog = take(madapt ? (size_t)m->mask_out * n : 0);
+    const bool n1 = m->t_thresh > 0.0f;
+    w.n1_list = reinterpret_cast<uint32_t*>(take(n1 ? 2 * n : 0));
+    w.n1_cnt = reinterpret_cast<uint32_t*>(take(n1 ? 2 : 0));
+    w.n1_mask = reinterpret_cast<uint64_t*>(take(n1 ? 2 * ((n + 31) / 32) : 0));
+    w.n1_base = reinterpret_cast<uint32_t*>(take(n1 ? (n + 31) / 32 : 0));
+    w.n1_std = reinterpret_cast<double*>(take(n1 ? 6 * n : 0));
+    w.n1_stf = take(n1 ? 16 * n : 0);
     w.bytes = off;
     return w;
 }
@@ -2339,6 +2474,16 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     if (!(m->t_thresh >= 0.0f && m->t_thresh < 1.0f))
         return fail(SAMNERF_EINVAL, "render_forward: t_thresh %g outside [0, 1)", (double)m->t_thresh);
     fa.exit_depth = m->t_thresh > 0.0f ? -logf(m->t_thresh) : INFINITY;
+    fa.i0 = 0;
+    fa.i1 = 32;                                          // reset below for S > 1 (EXIT only reads it)
+    if (m->t_thresh > 0.0f) {                            // N1: ray compaction buffers (k_final passes)
+        fa.n1.list = w.n1_list;
+        fa.n1.cnt = w.n1_cnt;
+        fa.n1.mask = w.n1_mask;
+        fa.n1.base = w.n1_base;
+        fa.st_d = w.n1_std;
+        fa.st_f = w.n1_stf;
+    }
     int ad = 0;
     if (m->with_mask) {
         if (m->t_thresh > 0.0f)
@@ -2373,7 +2518,10 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     // segments per ray: enough waves to fill the resident slots (2 per SIMD)
     // (SAMNERF_FINAL_S = 1 | 2 | 4 overrides, for measurement)
     const char* fs = diag_env("SAMNERF_FINAL_S");
-    const int seg = fs ? atoi(fs) : (N >= 65536u ? 1 : N >= 32768u ? 2 : 4);
+    // N1's compaction passes (diagnostic build) need whole rays: one segment
+    const bool n1_passes = m->t_thresh > 0.0f && n1_chunks() > 1;
+    const int seg = fs ? atoi(fs) : (n1_passes || N >= 65536u ? 1 : N >= 32768u ? 2 : 4);
+    fa.i1 = 32 / seg;
     const bool pf = final_prefetch(seg);
     if (m->sum_after_mlp && (m->t_thresh > 0.0f || sam_rows))
         return fail(SAMNERF_EINVAL, "render_forward: sum_after_mlp renders RGB (+ mask) only: no SAM "

@@ -77,3 +77,56 @@ def test_early_exit_error_bounded_by_threshold(hip_lib, scene, t):
     # the mode is opt-in: a renderer without it reproduces the default bits
     again = _render(net, ro, rd, 0.0)
     assert all(torch.equal(again[k], full[k]) for k in full)
+
+
+def _full_one_segment(net, ro, rd, monkeypatch):
+    """The default mode at N1's one segment per ray (small views split their
+    rays into 2 or 4 segments by default: another summation order)."""
+    from samnerf_amd import _lib
+    monkeypatch.setenv("SAMNERF_FINAL_S", "1")
+    with _lib.diag_library():
+        out = _render(net, ro, rd, 0.0)
+    monkeypatch.delenv("SAMNERF_FINAL_S")
+    return out
+
+
+def test_compaction_exact_when_no_ray_closes(hip_lib, cuda, monkeypatch, diag):
+    """N1's ray compaction (k_final passes over 8-sample chunks; the rays still
+    open at a chunk's end -- wave ballot, scan, scatter -- form the next
+    pass's list, their running sums carried in the workspace): on a
+    parity-weight scene no ray's transmittance falls below 1e-4 before its
+    last sample, so every ray goes through all four passes and the render
+    must equal the default mode's bits.  (The passes are the diagnostic
+    build's SAMNERF_N1_CHUNKS; the product's N1 is the wave-level exit,
+    measured faster, profiles/r3_n1_compaction.txt.)"""
+    spec = synth.ModelSpec(with_sam=True, grid_log2=14, s_grid_log2=14, prop_log2=12)
+    net = make_net(spec, synth.make_params(spec, seed=4, emb_scale=0.5), cuda)
+    pose, intr = synth.gui_camera(64, 64, rot=synth.random_rotation(2))
+    from oracle import renderer as orc
+    ro, rd = orc.get_rays(pose, intr, 64, 64)
+    ro, rd = ro.to(cuda), rd.to(cuda)
+    from samnerf_amd import _lib
+    full = _full_one_segment(net, ro, rd, monkeypatch)
+    monkeypatch.setenv("SAMNERF_N1_CHUNKS", "4")
+    with _lib.diag_library():
+        out = _render(net, ro, rd, 1e-4)
+    for k in ("image", "depth", "weights_sum", "samvit"):
+        assert torch.equal(out[k], full[k]), k
+
+
+@pytest.mark.parametrize("chunks", ["2", "4", "8"])
+def test_compaction_error_bounded_by_threshold(hip_lib, scene, monkeypatch, diag, chunks):
+    """The diagnostic build's compaction passes (2 / 4 / 8 sample chunks) on
+    the opaque-sphere scene: the same bound as the wave-level exit -- each
+    ray loses at most t of its weight -- and rays do close."""
+    from samnerf_amd import _lib
+    net, ro, rd, ref = scene
+    t = 1e-3
+    full = _full_one_segment(net, ro, rd, monkeypatch)
+    monkeypatch.setenv("SAMNERF_N1_CHUNKS", chunks)
+    with _lib.diag_library():
+        out = _render(net, ro, rd, t)
+    drop = full["weights_sum"] - out["weights_sum"]
+    assert (drop > 0).float().mean().item() > 0.1
+    assert drop.max().item() <= t * 1.001 + 1e-6
+    assert max_abs(out["image"], ref["image"]) <= t + 1e-3
