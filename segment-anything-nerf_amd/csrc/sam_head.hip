@@ -447,9 +447,10 @@ k_sam_head_h16(HeadArgsH a) {
     // one LDS object (a second __shared__ object can de-pipeline the DMA
     // waits): 3 x 16 KiB weight steps, then biases [5][256], LN weight / bias,
     // the weight tensors' inverse scales [5]
-    __shared__ uint4 smem[NBUF * KPS * kStepVec + (7 * 256 + 8) / 4];
+    constexpr int kBufVec = NBUF * KPS * kStepVec;
+    __shared__ uint4 smem[kBufVec + (7 * 256 + 8) / 4];
     uint4* Wb = smem;
-    float* Bs = reinterpret_cast<float*>(smem + NBUF * KPS * kStepVec);
+    float* Bs = reinterpret_cast<float*>(smem + kBufVec);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int j = lane & 31, h = lane >> 5;
     const uint32_t ray = blockIdx.x * kRaysV5 + wave * 32u + j;
@@ -500,7 +501,12 @@ k_sam_head_h16(HeadArgsH a) {
     uint4 xh[kXkb], xl[kXkb];
     Scale2 sc = scale_of_max(xmax);
     load_x(sc.s, xh, xl);
-    HeadStepper<NBUF, SPREAD, KPS> st{a.packed, Wb, wave, lane, 0};
+    HeadStepper<NBUF, SPREAD, KPS> st{};
+    st.packed = a.packed;
+    st.Wb = Wb;
+    st.wave = wave;
+    st.lane = lane;
+    st.step = 0;
     st.begin();
 
     floatx16 acc[8];
