@@ -660,7 +660,8 @@ def rooflines(stage_avg, band_rays, head_mode, rates):
     """`roofline` of the dominant kernel and every stage, each against the
     guide peak of the unit closest to saturation:
       l2   -- algorithmic bytes (embedding gathers + ray I/O, ALG_BYTES_PER_RAY)
-              / live time vs the L2's 34.5 TB/s (the tables are L2/MALL-resident);
+              / live time vs the L2's 34.5 TB/s (the tables are L2/MALL-resident;
+              not for s_grid, whose box gathers read a row once per wave);
       valu -- VALU-issue cycles of the stage's kernels (PMC SQ_ACTIVE_INST_VALU
               x 4 per ray, profiles/pmc_rates.json) / (1024 SIMDs x 2.4 GHz x
               live time);
@@ -678,9 +679,11 @@ def rooflines(stage_avg, band_rays, head_mode, rates):
             return None
         r = st_rates.get(st, {})
         alg = ALG_BYTES_PER_RAY[st] * band_rays
-        cand = {"l2": {"unit": "GB/s", "achieved": alg / (ms * 1e-3) / 1e9, "peak": L2_PEAK_GBS,
-                       "alg_bytes_per_ray": ALG_BYTES_PER_RAY[st]}}
-        cand["l2"]["frac"] = cand["l2"]["achieved"] / L2_PEAK_GBS
+        cand = {}
+        if st != "s_grid":
+            cand["l2"] = {"unit": "GB/s", "achieved": alg / (ms * 1e-3) / 1e9, "peak": L2_PEAK_GBS,
+                          "alg_bytes_per_ray": ALG_BYTES_PER_RAY[st]}
+            cand["l2"]["frac"] = cand["l2"]["achieved"] / L2_PEAK_GBS
         if "valu_cycles_per_ray" in r:
             c = r["valu_cycles_per_ray"] * band_rays
             cand["valu"] = {"unit": "busy cycles / SIMD cycles", "frac": c / cyc_avail(ms),
@@ -695,8 +698,15 @@ def rooflines(stage_avg, band_rays, head_mode, rates):
                                      "2.4 GHz x time)"}
             if "mfma_busy_cycles_per_ray" in r:
                 cand["mfma"]["pmc_mfma_busy_frac"] = r["mfma_busy_cycles_per_ray"] * band_rays / cyc_avail(ms)
+        if not cand:
+            return None
         bound = max(cand, key=lambda k: cand[k]["frac"])
         e = {"bound": bound}
+        if st == "s_grid":
+            # the box form reads each distinct corner row once per wave, so the
+            # algorithmic gather bytes (every lane's 8 corners) are no traffic
+            # bound: reported, not priced
+            e["alg_gather_tbs"] = alg / (ms * 1e-3) / 1e12
         e.update(cand[bound])
         e["other_bounds"] = {k: v["frac"] for k, v in cand.items() if k != bound}
         if "ta_busy_frac_in_pmc_run" in r:

@@ -373,11 +373,12 @@ size_t samnerf_rgb_train_workspace_size(const samnerf_model* model, uint32_t N);
  * the render's own losses (proposal_loss when with_proposal, distort_loss), the
  * Trainer's criterion left to the caller:
  *   forward: weights [N,32] (or NULL) = the final samples' weights, results['weights']
- *     of renderer.py:350 (not differentiable); losses [2] (device) = (proposal_loss,
+ *     of renderer.py:350; losses [2] (device) = (proposal_loss,
  *     distort_loss), unweighted; keeps
  *     what the backward reads in `workspace` (same model, rays, N, perturb arrays);
- *   backward: grad_image [N,3], grad_weights_sum [N] / grad_depth [N] (NULL = 0),
- *     grad_losses [2] (device; NULL = 0, required with with_proposal) -> the
+ *   backward: grad_image [N,3], grad_weights_sum [N] / grad_depth [N] / grad_weights
+ *     [N,32] (NULL = 0), grad_losses [2] (device; NULL = 0, required with
+ *     with_proposal) -> the
  *     gradients, OVERWRITTEN as in samnerf_rgb_train_step. */
 int samnerf_rgb_train_forward(const samnerf_model* model, const float* rays_o, const float* rays_d,
                               uint32_t N, const float* cam_near_far, uint32_t n_cnf, float bg_color,
@@ -387,8 +388,9 @@ int samnerf_rgb_train_forward(const samnerf_model* model, const float* rays_o, c
 int samnerf_rgb_train_backward(const samnerf_model* model, const float* rays_o, const float* rays_d,
                                uint32_t N, float bg_color, int with_proposal, const float* grad_image,
                                const float* grad_weights_sum, const float* grad_depth,
-                               const float* grad_losses, const samnerf_rgb_grads* grads, void* workspace,
-                               size_t workspace_bytes, samnerf_stream_t stream);
+                               const float* grad_weights, const float* grad_losses,
+                               const samnerf_rgb_grads* grads, void* workspace, size_t workspace_bytes,
+                               samnerf_stream_t stream);
 int samnerf_rgb_train_step(const samnerf_model* model, const float* rays_o, const float* rays_d,
                            uint32_t N, const float* cam_near_far, uint32_t n_cnf, const float* gt_rgb,
                            const samnerf_rgb_train_opts* opts, float* image, float* depth,

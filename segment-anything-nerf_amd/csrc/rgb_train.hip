@@ -97,6 +97,7 @@ struct RtArgs {
     const float* g_img;       // [N][3] d loss / d image
     const float* g_ws;        // [N] d loss / d weights_sum, or null
     const float* g_depth;     // [N] d loss / d depth, or null
+    const float* g_w;         // [N][32] d loss / d weights (results['weights']), or null
     const float* g_loss;      // [2] d loss / d (proposal_loss, distort_loss) (device), or null
     float inv_n;              // 1 / N
     // per final sample s = 32 r + k (ray-major): [channel][S], S = 32 N
@@ -534,6 +535,7 @@ __global__ void __launch_bounds__(256) k_rt_final_bwd_ray_h(RtArgs a) {
         const double after = (WMt - WMi) - md * (Wt - Wi);
         g = __builtin_fmaf(c_dist, (float)(2.0 * (before + after)) + (2.0f / 3.0f) * iv * w, g);
     }
+    if (a.g_w) g = g + a.g_w[(size_t)r * kT + k];          // a loss on results['weights'] itself
     const bool fin = isfinite(raw);                        // nan_to_num_ backward
     const float dw = fin ? g : 0.0f;
     // sum_{j>k} dw_j raw_j: the exclusive suffix sum in double (ATen sums the
@@ -1331,9 +1333,9 @@ int samnerf_rgb_train_forward(const samnerf_model* m, const float* rays_o, const
 
 int samnerf_rgb_train_backward(const samnerf_model* m, const float* rays_o, const float* rays_d, uint32_t N,
                                float bg_color, int with_proposal, const float* grad_image,
-                               const float* grad_weights_sum, const float* grad_depth, const float* grad_losses,
-                               const samnerf_rgb_grads* grads, void* workspace, size_t workspace_bytes,
-                               samnerf_stream_t stream) {
+                               const float* grad_weights_sum, const float* grad_depth, const float* grad_weights,
+                               const float* grad_losses, const samnerf_rgb_grads* grads, void* workspace,
+                               size_t workspace_bytes, samnerf_stream_t stream) {
     if (!m) return fail(SAMNERF_EINVAL, "rgb_train_backward: null model");
     if (N == 0) return SAMNERF_OK;
     if (!rays_o || !rays_d || !grad_image) return fail(SAMNERF_EINVAL, "rgb_train_backward: null pointer");
@@ -1353,6 +1355,7 @@ int samnerf_rgb_train_backward(const samnerf_model* m, const float* rays_o, cons
     c.a.g_img = grad_image;
     c.a.g_ws = grad_weights_sum;
     c.a.g_depth = grad_depth;
+    c.a.g_w = grad_weights;
     c.a.g_loss = grad_losses;
     if ((rc = rt_backward(m, N, with_proposal != 0, grads, c, w, s))) return rc;
     return check_launch("rgb_train_backward");
@@ -1396,6 +1399,7 @@ int samnerf_rgb_train_step(const samnerf_model* m, const float* rays_o, const fl
     c.a.g_img = g_img;
     c.a.g_ws = g_ws;
     c.a.g_depth = nullptr;
+    c.a.g_w = nullptr;
     c.a.g_loss = g_loss;
     if ((rc = rt_backward(m, N, with_prop, grads, c, w, s))) return rc;
     return check_launch("rgb_train_step");

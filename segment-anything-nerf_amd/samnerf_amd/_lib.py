@@ -82,7 +82,7 @@ _SIGS = {
     "samnerf_rgb_train_forward": ([ctypes.POINTER(SamnerfModel), _vp, _vp, _u32, _vp, _u32, _f32, _int,
                                    _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp], _int),
     "samnerf_rgb_train_backward": ([ctypes.POINTER(SamnerfModel), _vp, _vp, _u32, _f32, _int, _vp, _vp,
-                                    _vp, _vp, ctypes.c_void_p, _vp, _sz, _vp], _int),
+                                    _vp, _vp, _vp, ctypes.c_void_p, _vp, _sz, _vp], _int),
     "samnerf_sam_head_workspace_size": ([], _sz),
     "samnerf_sam_head_forward": ([ctypes.POINTER(SamnerfModel), _vp, _u32, _vp, _vp, _sz, _vp], _int),
     "samnerf_head_train_workspace_size": ([_u32], _sz),

@@ -527,21 +527,26 @@ class _FusedRGBTrain(torch.autograd.Function):
                 m.perturb[i] = None
         ctx.state = (renderer, m, rays_o, rays_d, bg, pert, with_prop, ws, need, list(renderer._keep))
         ctx.shapes = [p.shape for p in params]
-        ctx.mark_non_differentiable(weights)
+        # outputs the loss does not use arrive as None (no zero tensors to
+        # read): only results['weights'] usually is
+        ctx.set_materialize_grads(False)
         return image, depth, wsum, losses[0], losses[1], weights
 
     @staticmethod
-    def backward(ctx, g_img, g_depth, g_wsum, g_prop, g_dist, _g_weights):
+    def backward(ctx, g_img, g_depth, g_wsum, g_prop, g_dist, g_weights):
         renderer, m, rays_o, rays_d, bg, pert, with_prop, ws, need, _ = ctx.state
         dev = rays_o.device
         N = rays_o.shape[0]
         # every converted gradient is bound to a local so that it stays alive
         # until the C call returns (a temporary's block could otherwise be
         # handed to the next conversion by the caching allocator)
-        g_img = g_img.contiguous().float()
-        g_ws = g_wsum.contiguous().float()
-        g_dp = g_depth.contiguous().float()
-        g_loss = torch.stack([g_prop.reshape(()), g_dist.reshape(())]).float().contiguous()
+        def conv(t):
+            return None if t is None else t.contiguous().float()
+        g_img = conv(g_img) if g_img is not None else torch.zeros(N, 3, device=dev)
+        g_ws, g_dp, g_w = conv(g_wsum), conv(g_depth), conv(g_weights)   # None: no gradient (NULL)
+        zero = torch.zeros((), device=dev)
+        g_loss = torch.stack([(zero if g_prop is None else g_prop).reshape(()),
+                              (zero if g_dist is None else g_dist).reshape(())]).float().contiguous()
         grads = [torch.empty(sh, device=dev) for sh in ctx.shapes]
         g = SamnerfRgbGrads()
         g.grid = grads[0].data_ptr()
@@ -558,7 +563,7 @@ class _FusedRGBTrain(torch.autograd.Function):
                 m.perturb[i] = None if pert is None else _param(pert[i], f"perturb[{i}]")
             check(lib().samnerf_rgb_train_backward(
                 ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, float(bg), int(with_prop), _ptr(g_img),
-                _ptr(g_ws), _ptr(g_dp), _ptr(g_loss),
+                _ptr(g_ws), _ptr(g_dp), _ptr(g_w), _ptr(g_loss),
                 ctypes.byref(g), _ptr(ws), need, _stream(g_img)), "rgb_train_backward")
         finally:
             for i in range(3):

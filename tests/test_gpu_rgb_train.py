@@ -371,3 +371,29 @@ def test_autograd_rgb_step_with_depth_and_weights_sum_loss(hip_lib, cuda):
         outs.append(float(loss))
     assert abs(outs[0] - outs[1]) <= 1e-5 * abs(outs[1])
     _compare_grads(a, b)
+
+
+def test_fused_render_weights_are_differentiable(hip_lib, cuda):
+    """results['weights'] carries gradient on the fused training path as in the
+    reference (renderer.py:350): a loss on the per-sample weights (plus depth
+    and image, no proposal / distortion terms) against the torch path's
+    autograd at the same bins."""
+    from oracle_backend import injected_bins
+    a, b = _rgb_nets(cuda, seed=14, devices=("cuda", "cuda"))
+    ro, rd = _rays(16, 4, cuda)
+    bins = _fused_bins(a, ro, rd)
+    ramp = torch.linspace(0.0, 1.0, 32, device=cuda)
+
+    def loss_of(net):
+        out = net.render(ro, rd, staged=False, perturb=False, bg_color=1.0)
+        w = out["weights"]
+        assert w.requires_grad
+        return (w * ramp).sum() / w.shape[0] + 1e-3 * out["depth"].mean() + out["image"].mean()
+
+    la = loss_of(a)
+    la.backward()
+    with injected_bins(bins):
+        lb = loss_of(b)
+        lb.backward()
+    assert abs(float(la) - float(lb)) <= 1e-5 * abs(float(lb)) + 1e-7
+    _compare_grads(a, b)
