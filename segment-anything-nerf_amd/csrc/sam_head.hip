@@ -318,11 +318,12 @@ struct HeadArgsH {
 // boundary waits only for the step about to be read (counted vmcnt, one step
 // stays in flight across the raw barrier), per cdna_hip_programming.md
 // "Pipelining across barriers".
-// vmcnt(N) for N = 0, 4, 8, 16 (the waits are counted by hand: the DMA is inline asm)
+// vmcnt(N) for N = 0, 2, 4, 8, 16 (the waits are counted by hand: the DMA is inline asm)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-    static_assert(N == 0 || N == 4 || N == 8 || N == 16, "vmcnt literal");
+    static_assert(N == 0 || N == 2 || N == 4 || N == 8 || N == 16, "vmcnt literal");
     if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");

@@ -537,6 +537,9 @@ class _FusedRGBTrain(torch.autograd.Function):
         renderer, m, rays_o, rays_d, bg, pert, with_prop, ws, need, _ = ctx.state
         dev = rays_o.device
         N = rays_o.shape[0]
+        # a loss without proposal_loss leaves the proposal networks' .grad None,
+        # as autograd does (the final weights use detached bins)
+        with_prop = with_prop and g_prop is not None
         # every converted gradient is bound to a local so that it stays alive
         # until the C call returns (a temporary's block could otherwise be
         # handed to the next conversion by the caching allocator)
@@ -568,6 +571,8 @@ class _FusedRGBTrain(torch.autograd.Function):
         finally:
             for i in range(3):
                 m.perturb[i] = None
+        if not with_prop:
+            grads = grads[:7] + [None] * (len(grads) - 7)
         return (None,) * 7 + tuple(grads)
 
 

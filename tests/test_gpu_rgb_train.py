@@ -323,7 +323,7 @@ def test_train_mode_render_runs_the_training_kernels(hip_lib, cuda):
     torch.manual_seed(5)
     img_c, loss_c, out_c = rgb_train_step(c, ro, rd, gt, global_step=1)
     assert "proposal_loss" in out_c and "distort_loss" in out_c and out_c["num_points"] == 1024 * 32
-    assert out_c["weights"].shape == (1024, 32) and not out_c["weights"].requires_grad
+    assert out_c["weights"].shape == (1024, 32) and out_c["weights"].requires_grad   # as renderer.py:350
     torch.testing.assert_close(out_c["weights"].sum(-1), out_c["weights_sum"].detach(), rtol=1e-5, atol=1e-6)
     assert img_c.requires_grad and loss_c.requires_grad
     loss_c.backward()
