@@ -334,8 +334,12 @@ __device__ __forceinline__ void wait_vm() {
 // super-step (the k-blocks of a super-step may straddle a layer boundary: the
 // barrier only guards the weight buffers).  SPREAD: the DMA pieces are issued
 // between the MFMAs (one after every second tile) instead of before them.
-template <int NBUF, bool SPREAD, int KPS>
+template <int NBUF, bool SPREAD, int KPS_>
 struct HeadStepper {
+    // KPS_ 0: the diagnostic no-DMA form (one k-block per barrier, the weight
+    // stream skipped: wrong results, for timing what the DMA costs)
+    static constexpr int KPS = KPS_ ? KPS_ : 1;
+    static constexpr bool kNoDma = KPS_ == 0;
     static constexpr int kSuper = (kSteps + KPS - 1) / KPS;
     static constexpr int kPieces = 4 * KPS;                  // 1-KiB pieces per wave and super-step
     const uint4* __restrict__ packed;
@@ -348,6 +352,7 @@ struct HeadStepper {
     // every ds_read); the waits are counted by hand in run().  No ordinary
     // vector-memory load is issued inside the step loop.
     __device__ __forceinline__ void piece(int S, int c) {
+        if constexpr (kNoDma) return;
         const size_t chunk = (size_t)wave * 256 * KPS + (size_t)c * 64;
         const uint4* src = packed + (size_t)S * KPS * kStepVec + chunk + lane;
         const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(Wb + (S % NBUF) * KPS * kStepVec + chunk);
@@ -448,7 +453,7 @@ k_sam_head_h16(HeadArgsH a) {
     // one LDS object (a second __shared__ object can de-pipeline the DMA
     // waits): 3 x 16 KiB weight steps, then biases [5][256], LN weight / bias,
     // the weight tensors' inverse scales [5]
-    constexpr int kBufVec = NBUF * KPS * kStepVec;
+    constexpr int kBufVec = NBUF * (KPS ? KPS : 1) * kStepVec;
     __shared__ uint4 smem[kBufVec + (7 * 256 + 8) / 4];
     uint4* Wb = smem;
     float* Bs = reinterpret_cast<float*>(smem + kBufVec);
@@ -916,6 +921,7 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         else if (form == 6) k_sam_head_h16<4, true, 1><<<blocks, 256, 0, s>>>(a);
         else if (form == 7) k_sam_head_h16<3, true, 2><<<blocks, 256, 0, s>>>(a);
         else if (form == 8) k_sam_head_h16<4, true, 2><<<blocks, 256, 0, s>>>(a);
+        else if (form == 11) k_sam_head_h16<3, true, 0><<<blocks, 256, 0, s>>>(a);   // no DMA (timing only)
         else
 #endif
         k_sam_head_h16<3, true, 1><<<blocks, 256, 0, s>>>(a);   // 3 buffers, DMA between the MFMAs
