@@ -310,6 +310,7 @@ struct HeadArgsH {
     const float* ln_w;
     const float* ln_b;
     float* out;
+    unsigned long long* stamps;   // diagnostic form 13 only: [block][wave][16] s_memtime marks
 };
 
 // Weight stream: step s's 16 KiB of fragments go global -> LDS by direct DMA
@@ -318,15 +319,35 @@ struct HeadArgsH {
 // boundary waits only for the step about to be read (counted vmcnt, one step
 // stays in flight across the raw barrier), per cdna_hip_programming.md
 // "Pipelining across barriers".
-// vmcnt(N) for N = 0, 2, 4, 8, 16 (the waits are counted by hand: the DMA is inline asm)
+// vmcnt(N) for N = 0, 2, 4, 8, 16 (the waits are counted by hand: the DMA is inline asm);
+// wait_vmn: any N that folds to a constant (0..63)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-    static_assert(N == 0 || N == 2 || N == 4 || N == 8 || N == 16, "vmcnt literal");
+    static_assert(N == 0 || N == 2 || N == 4 || N == 5 || N == 6 || N == 8 || N == 16, "vmcnt literal");
     if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+}
+
+// 16 B per lane, global -> LDS at lds_byte_addr + 16 lane (direct DMA, no
+// VGPRs; counted in vmcnt, waited by hand)
+__device__ __forceinline__ void lds_dma16(const void* src, uint32_t lds_byte_addr) {
+    const uint32_t d = __builtin_amdgcn_readfirstlane(lds_byte_addr);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(d)
+        : "memory");
+}
+
+__device__ __forceinline__ void wait_vmn(int n) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory");
 }
 
 // The weight stream in "super-steps" of KPS k-blocks (KPS x 16 KiB): NBUF
@@ -450,9 +471,23 @@ __device__ __forceinline__ void split_layer(const floatx16 (&acc)[8], float s, u
 // LAZY (diagnostic form 12, measured 3 % slower): a layer's values stay fp32
 // through the next layer and each k-block's B operands are split right before
 // its step, inside the MFMA shadow, instead of at the layer boundary
-template <int NBUF, bool SPREAD, int KPS, bool LAZY = false>
+// STAMP (diagnostic form 13): s_memtime at the phase boundaries of every wave
+// (kernel start, stream primed, each layer's steps, each layer boundary, the
+// LayerNorm), written by lane 0 at the end: where the cycles of a wave go
+template <int NBUF, bool SPREAD, int KPS, bool LAZY = false, bool STAMP = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_sam_head_h16(HeadArgsH a) {
+    unsigned long long ts[16];
+    auto mark = [&](int i) {
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            ts[i] = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    mark(0);
+    unsigned long long rt0 = 0;
+    if constexpr (STAMP) rt0 = __builtin_amdgcn_s_memrealtime();
     // one LDS object (a second __shared__ object can de-pipeline the DMA
     // waits): 3 x 16 KiB weight steps, then biases [5][256], LN weight / bias,
     // the weight tensors' inverse scales [5]
@@ -517,6 +552,7 @@ k_sam_head_h16(HeadArgsH a) {
     st.lane = lane;
     st.step = 0;
     st.begin();
+    mark(1);
 
     floatx16 acc[8];
     uint4 ah[LAZY ? 1 : kHkb], al[LAZY ? 1 : kHkb];
@@ -558,22 +594,32 @@ k_sam_head_h16(HeadArgsH a) {
     zero();                                                   // layer 0: W0 . x
 #pragma unroll
     for (int kb = 0; kb < kXkb; ++kb) st.run(acc, xh[kb], xl[kb]);
+    mark(2);
     next(0, 0.0f);
+    mark(3);
     zero();                                                   // layer 1
     h_segment();
+    mark(4);
     next(1, xmax);                                            // layer 2 reads cat(h, x): one scale
     zero();                                                   // layer 2: W2 . cat(h, x)
     load_x(sc.s, xh, xl);
+    mark(5);
 #pragma unroll
     for (int kb = 0; kb < kXkb; ++kb) st.run(acc, xh[kb], xl[kb]);
     h_segment();
+    mark(6);
     next(2, 0.0f);
+    mark(7);
     zero();                                                   // layer 3
     h_segment();
+    mark(8);
     next(3, 0.0f);
+    mark(9);
     zero();                                                   // layer 4 (no activation)
     h_segment();
+    mark(10);
     finish_layer(acc, Bs + 4 * 256, sc.inv * Wi[4], h, false);
+    mark(11);
 
     // LayerNorm(256, eps=1e-5) per ray: this lane holds 128 of the ray's
     // units, the other half-wave (lane ^ 32) the rest; sums in double
@@ -595,6 +641,15 @@ k_sam_head_h16(HeadArgsH a) {
     var += __shfl_xor(var, 32);
     const float rstd = (float)(1.0 / sqrt(var / 256.0 + 1e-5));
     const float mf = (float)mean;
+    mark(12);
+    if constexpr (STAMP) {
+        // where the wave ran: HW_ID (wave, SIMD, CU, SH, SE bits) in ts[15], XCC_ID in ts[14]
+        ts[15] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        ts[14] = (unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+        ts[13] = __builtin_amdgcn_s_memrealtime() - rt0;     // 100 MHz ticks over marks 0 .. 12
+        if (lane == 0)
+            for (int i = 0; i < 16; ++i) a.stamps[((size_t)blockIdx.x * 4 + wave) * 16 + i] = ts[i];
+    }
     if (!live) return;
     float* o = a.out + (size_t)ray * 256;
     const float* lw = Bs + 5 * 256;
@@ -612,6 +667,280 @@ k_sam_head_h16(HeadArgsH a) {
             *reinterpret_cast<float4*>(o + u) = y;
         }
 }
+
+#ifdef SAMNERF_DIAG_VARIANTS
+// ======================================================= f16x3, persistent
+// Diagnostic form (measured, not faster): one workgroup per CU over its
+// tiles cuts the cycles per tile 9 % (142 k vs 156 k per wave, gap between
+// blocks included), but the shader clock over the kernel falls from 1.89 to
+// 1.77 GHz (s_memtime / s_memrealtime, tools/head_stamps.py): the head runs at
+// the power limit, so the time stays (0.687 vs 0.678 ms, bit-identical).
+// k_sam_head_h16's arithmetic (the same MFMA products in
+// the same order, the same scales, finishing and LayerNorm: bit-identical
+// output) in a persistent workgroup per CU that walks its 128-ray tiles
+// (tile = blockIdx.x + i * gridDim.x).  Per tile, k_sam_head_h16 spent ~20 k
+// of its ~145 k cycles per wave in the prologue (the rows' HBM latency, the
+// weight stream priming) and ~12 k between blocks (tools/head_stamps.py); here
+//   * the weight ring runs on across tiles: the last two steps of tile i
+//     stream steps 0 and 1 of tile i + 1 (the weights are the same for every
+//     tile), ring buffer = global step mod 3 (`rot` = the tile's first buffer);
+//   * the next tile's rows (one contiguous 82 KiB: 128 rows of 164 floats) go
+//     global -> LDS by DMA during steps kXFirst .. kXFirst + 20, one 1 KiB
+//     piece per wave and step after the step's weight pieces, into the x
+//     region that the current tile last reads at layer 2's skip input
+//     (step 11's barrier long passed); layer 0 and the skip input read x
+//     from LDS (conflict-free: row stride 656 B = 41 slots);
+//   * the output stores of tile i drain under tile i + 1's first step.
+// LDS: 48 KiB ring + 84 KiB x + 7 KiB biases / LayerNorm / scales.
+constexpr int kTileBytes = kRaysV5 * kRowIn * 4;    // 83,968 B = 82 KiB
+constexpr int kXPieces = 21;                        // per wave: 84 pieces per tile, 82 carry rows
+constexpr int kXVec = 4 * kXPieces * 64;            // uint4 of the x region
+constexpr int kXFirst = 40;                         // x pieces in steps 40 .. 60 (layer 2's h part, layer 3)
+static_assert(4 * kXPieces * 1024 >= kTileBytes, "x region holds a tile");
+static_assert(kXFirst > kXkb + kHkb + kXkb && kXFirst + kXPieces + 3 < kSteps, "x stream window");
+
+template <int NBUF>
+struct HeadStreamQ {
+    const uint4* packed;
+    uint4* Wb;                 // LDS ring [NBUF][kStepVec]
+    const char* rows;          // head-input rows (global)
+    const char* rows_end;      // their last 16 B
+    uint32_t xs;               // LDS byte address of the x region
+    uint32_t next_tile;        // whose rows the x pieces carry
+    int wave, lane;
+    int rot;                   // ring buffer of the tile's step 0 (uniform)
+    int step;                  // in-tile step (constant per call site: every loop is unrolled)
+
+    __device__ __forceinline__ int buf(int s) const {
+        const int b = rot + s % NBUF;
+        return b >= NBUF ? b - NBUF : b;
+    }
+    // piece c (0..3) of in-tile step s (s >= kSteps: the next tile's step s - kSteps)
+    __device__ __forceinline__ void wpiece(int s, int c) {
+        const uint4* base = packed + (size_t)(s % kSteps) * kStepVec + (size_t)wave * 256 + (size_t)c * 64;
+        lds_dma16(base + lane, (uint32_t)reinterpret_cast<uintptr_t>(Wb + buf(s) * kStepVec + wave * 256 + c * 64));
+    }
+    __device__ __forceinline__ void xpiece(int q) {
+        const uint32_t p = (uint32_t)(wave * kXPieces + q);
+        const char* base = rows + (size_t)next_tile * kTileBytes + (size_t)p * 1024u;
+        const char* src = base + (size_t)lane * 16u;
+        src = src > rows_end ? rows_end : src;            // pieces past the rows reload the last 16 B
+        lds_dma16(src, xs + p * 1024u);
+    }
+    static __device__ __forceinline__ constexpr bool xstep(int s) { return s >= kXFirst && s < kXFirst + kXPieces; }
+
+    // one k-block of the current layer for all 8 output tiles
+    __device__ __forceinline__ void run(floatx16 (&acc)[8], const uint4& bh, const uint4& bl) {
+        const int s = step;
+        const uint4* cur = Wb + buf(s) * kStepVec + lane;
+        uint4 fh[8], fl[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            fh[t] = cur[t * 64];
+            fl[t] = cur[512 + t * 64];
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            acc[t] = mfma_f16x3(fh[t], fl[t], bh, bl, acc[t]);
+            if (t & 1) {
+                __builtin_amdgcn_sched_barrier(0);
+                wpiece(s + NBUF - 1, t >> 1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (xstep(s)) {
+            __builtin_amdgcn_sched_barrier(0);
+            xpiece(s - kXFirst);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // step s + 1 landed: younger than its pieces (issued in step s + 2 - NBUF)
+        // are that step's x piece and the pieces of the steps after it
+        int n = 4 * (NBUF - 2);
+#pragma unroll
+        for (int k = s + 2 - NBUF; k <= s; ++k) n += xstep(k) ? 1 : 0;
+        wait_vmn(n);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        ++step;
+    }
+};
+
+template <int NBUF, bool STAMP = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_sam_head_h16q(HeadArgsH a, uint32_t ntiles) {
+    unsigned long long t0 = 0, rt0 = 0;                   // STAMP: the wave's clock over its life
+    if constexpr (STAMP) {
+        t0 = __builtin_amdgcn_s_memtime();
+        rt0 = __builtin_amdgcn_s_memrealtime();
+    }
+    __shared__ uint4 smem[NBUF * kStepVec + kXVec + (7 * 256 + 8) / 4];
+    uint4* const Wb = smem;
+    float* const Xs = reinterpret_cast<float*>(smem + NBUF * kStepVec);
+    float* const Bs = reinterpret_cast<float*>(smem + NBUF * kStepVec + kXVec);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int j = lane & 31, h = lane >> 5;
+
+    for (int i = tid; i < 5 * 256; i += 256) Bs[i] = a.b[i >> 8][i & 255];
+    float* const Wi = Bs + 7 * 256;                       // 2^-kexp[l]
+    if (tid < 5) Wi[tid] = exp2i(-a.kexp[tid]);
+    Bs[5 * 256 + tid] = a.ln_w[tid];
+    Bs[6 * 256 + tid] = a.ln_b[tid];
+
+    HeadStreamQ<NBUF> st;
+    st.packed = a.packed;
+    st.Wb = Wb;
+    st.rows = reinterpret_cast<const char*>(a.rows);
+    st.rows_end = st.rows + (size_t)a.N * kRowIn * 4 - 16;
+    st.xs = (uint32_t)reinterpret_cast<uintptr_t>(Xs);
+    st.next_tile = blockIdx.x;
+    st.wave = __builtin_amdgcn_readfirstlane(wave);
+    st.lane = lane;
+    st.rot = 0;
+    st.step = 0;
+    // the first tile's rows, then weight steps 0 and 1; rows and step 0 landed
+#pragma unroll
+    for (int q = 0; q < kXPieces; ++q) st.xpiece(q);
+#pragma unroll
+    for (int q = 0; q + 1 < NBUF; ++q)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) st.wpiece(q, c);
+    wait_vmn(4 * (NBUF - 2));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const float* xr = Xs + (wave * 32 + j) * kRowIn;      // this lane's row of the tile
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        st.next_tile = tile + gridDim.x;
+        st.step = 0;
+        // the stream's bases made opaque per tile: otherwise the compiler hoists
+        // the 344 piece addresses of a tile out of the tile loop (spilled)
+        asm volatile("" : "+s"(st.packed), "+s"(st.rows));
+        const uint32_t ray = tile * kRaysV5 + wave * 32u + j;
+        const bool live = ray < a.N;
+        auto x8 = [&](int kb, float (&v)[8]) {
+            const int c0 = 16 * kb + 8 * h;
+            if (c0 + 8 <= kRowIn) {
+                const float4 p = *reinterpret_cast<const float4*>(xr + c0);
+                const float4 q = *reinterpret_cast<const float4*>(xr + c0 + 4);
+                v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w;
+                v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
+            } else {
+#pragma unroll
+                for (int m = 0; m < 8; ++m) v[m] = c0 + m < kRowIn ? xr[c0 + m] : 0.0f;
+            }
+#pragma unroll
+            for (int m = 0; m < 8; ++m)
+                if (!live || c0 + m >= kIn) v[m] = 0.0f;  // column 163 of a row is padding
+        };
+        float xmax = 0.0f;
+#pragma unroll
+        for (int kb = 0; kb < kXkb; ++kb) {
+            float v[8];
+            x8(kb, v);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) xmax = fmaxf(xmax, fabsf(v[m]));
+        }
+        xmax = fmaxf(xmax, __shfl_xor(xmax, 32));
+        auto load_x = [&](float sc_s, uint4 (&xh)[kXkb], uint4 (&xl)[kXkb]) {
+#pragma unroll
+            for (int kb = 0; kb < kXkb; ++kb) {
+                float v[8];
+                x8(kb, v);
+                split8_f16(v, sc_s, xh[kb], xl[kb]);
+            }
+        };
+        uint4 xh[kXkb], xl[kXkb];
+        Scale2 sc = scale_of_max(xmax);
+        load_x(sc.s, xh, xl);
+
+        floatx16 acc[8];
+        uint4 ah[kHkb], al[kHkb];
+        auto zero = [&]() {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc[t] = floatx16{};
+        };
+        auto next = [&](int layer, float extra) {
+            float m = finish_layer(acc, Bs + layer * 256, sc.inv * Wi[layer], h, true);
+            m = fmaxf(fmaxf(m, __shfl_xor(m, 32)), extra);
+            sc = scale_of_max(m);
+            split_layer(acc, sc.s, ah, al);
+        };
+        auto h_segment = [&]() {
+#pragma unroll
+            for (int kb = 0; kb < kHkb; ++kb) st.run(acc, ah[kb], al[kb]);
+        };
+
+        zero();                                               // layer 0: W0 . x
+#pragma unroll
+        for (int kb = 0; kb < kXkb; ++kb) st.run(acc, xh[kb], xl[kb]);
+        next(0, 0.0f);
+        zero();                                               // layer 1
+        h_segment();
+        next(1, xmax);                                        // layer 2 reads cat(h, x): one scale
+        zero();                                               // layer 2: W2 . cat(h, x)
+        load_x(sc.s, xh, xl);
+#pragma unroll
+        for (int kb = 0; kb < kXkb; ++kb) st.run(acc, xh[kb], xl[kb]);
+        h_segment();
+        next(2, 0.0f);
+        zero();                                               // layer 3
+        h_segment();
+        next(3, 0.0f);
+        zero();                                               // layer 4 (no activation)
+        h_segment();
+        finish_layer(acc, Bs + 4 * 256, sc.inv * Wi[4], h, false);
+
+        // LayerNorm(256, eps=1e-5), as k_sam_head_h16
+        double s = 0.0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) s += (double)acc[t][q];
+        s += __shfl_xor(s, 32);
+        const double mean = s / 256.0;
+        double var = 0.0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const double dlt = (double)acc[t][q] - mean;
+                var += dlt * dlt;
+            }
+        var += __shfl_xor(var, 32);
+        const float rstd = (float)(1.0 / sqrt(var / 256.0 + 1e-5));
+        const float mf = (float)mean;
+        if (live) {
+            float* o = a.out + (size_t)ray * 256;
+            const float* lw = Bs + 5 * 256;
+            const float* lb = Bs + 6 * 256;
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+#pragma unroll
+                for (int mm = 0; mm < 4; ++mm) {
+                    const int u = 32 * t + 8 * mm + 4 * h;
+                    float4 y;
+                    y.x = ((acc[t][4 * mm + 0] - mf) * rstd) * lw[u + 0] + lb[u + 0];
+                    y.y = ((acc[t][4 * mm + 1] - mf) * rstd) * lw[u + 1] + lb[u + 1];
+                    y.z = ((acc[t][4 * mm + 2] - mf) * rstd) * lw[u + 2] + lb[u + 2];
+                    y.w = ((acc[t][4 * mm + 3] - mf) * rstd) * lw[u + 3] + lb[u + 3];
+                    *reinterpret_cast<float4*>(o + u) = y;
+                }
+        }
+        st.rot = (st.rot + kSteps) % NBUF;
+    }
+    wait_vmn(0);
+    if constexpr (STAMP) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            unsigned long long* o = a.stamps + ((size_t)blockIdx.x * 4 + wave) * 16;
+            for (int i = 0; i < 16; ++i) o[i] = 0;
+            o[12] = t1 - t0;
+            o[13] = rt1 - rt0;
+        }
+    }                                             // the DMA past the last tile drained
+}
+
+#endif  // SAMNERF_DIAG_VARIANTS
 
 #ifdef SAMNERF_DIAG_VARIANTS
 // ============================================================ f16x3, paired
@@ -642,16 +971,6 @@ struct PairCfg {
 constexpr int kBVec = kHkb * 2 * 64;                     // uint4 of one group's B fragments (32 KiB)
 constexpr int kPairSmemVec = 2 * kStepVec + 4 * kBVec;   // 10,240 uint4 = 160 KiB
 
-__device__ __forceinline__ void lds_dma16(const uint4* src, uint32_t lds_byte_addr) {
-    const uint32_t d = __builtin_amdgcn_readfirstlane(lds_byte_addr);
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(src), "s"(d)
-        : "memory");
-}
 // every LDS access of this wave done, then the workgroup barrier
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -903,6 +1222,21 @@ k_sam_head_h16p(HeadArgsH a) {
 
 }  // namespace
 
+#ifdef SAMNERF_DIAG_VARIANTS
+// compute units of the current device (the persistent head's grid)
+static int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+#endif
+
 size_t sam_head_packed_floats() {
     const size_t f32 = (size_t)8 * kTotalGroups * 64 * 4;
     const size_t h16 = (size_t)kPackedVec * 4 + 8;           // fragments + the tensors' log2 scales
@@ -927,22 +1261,35 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         a.ln_w = m->ln_w;
         a.ln_b = m->ln_b;
         a.out = samvit;
+        a.stamps = nullptr;
         const uint32_t blocks = div_up(N, (uint32_t)kRaysV5);
 #ifdef SAMNERF_DIAG_VARIANTS
         // measured forms (tools/head_bench.py, profiles/r3_head_forms.txt), all
         // bit-identical; 1 = the round-2 schedule (DMA before the MFMAs), 2 / 3
         // = the paired 2 / 4-waves-per-SIMD forms (0.78 / 0.84 vs 0.72 ms),
-        // 5 / 7 / 8 = two k-blocks per barrier, 6 / 8 = four buffers
+        // 5 / 7 / 8 = two k-blocks per barrier, 6 / 8 = four buffers, 11 = no
+        // weight DMA (timing only), 12 = lazy split, 13 = phase stamps,
+        // 20 / 22 = persistent with 3 / 4 buffers, 21 = 22 with clock stamps
         const char* v = diag_env("SAMNERF_HEAD_V");
         const int form = v ? atoi(v) : 4;
-        if (form == 1) k_sam_head_h16<3, false, 1><<<blocks, 256, 0, s>>>(a);
+        const uint32_t grid = blocks < (uint32_t)device_cus() ? blocks : (uint32_t)device_cus();
+        if (form == 20) k_sam_head_h16q<3><<<grid, 256, 0, s>>>(a, blocks);
+        else if (form == 22) k_sam_head_h16q<4><<<grid, 256, 0, s>>>(a, blocks);
+        else if (form == 21 || form == 13) {                   // stamps (tools/head_stamps.py)
+            const char* p = diag_env("SAMNERF_HEAD_STAMPS");
+            a.stamps = reinterpret_cast<unsigned long long*>(p ? strtoull(p, nullptr, 16) : 0ull);
+            if (!a.stamps) return fail(SAMNERF_EINVAL, "sam_head form %d needs SAMNERF_HEAD_STAMPS", form);
+            if (form == 21) k_sam_head_h16q<4, true><<<grid, 256, 0, s>>>(a, blocks);
+            else k_sam_head_h16<3, true, 1, false, true><<<blocks, 256, 0, s>>>(a);
+        }
+        else if (form == 1) k_sam_head_h16<3, false, 1><<<blocks, 256, 0, s>>>(a);
         else if (form == 2) k_sam_head_h16p<4><<<blocks, PairCfg<4>::NT, 0, s>>>(a);
         else if (form == 3) k_sam_head_h16p<2><<<blocks, PairCfg<2>::NT, 0, s>>>(a);
         else if (form == 5) k_sam_head_h16<3, false, 2><<<blocks, 256, 0, s>>>(a);
         else if (form == 6) k_sam_head_h16<4, true, 1><<<blocks, 256, 0, s>>>(a);
         else if (form == 7) k_sam_head_h16<3, true, 2><<<blocks, 256, 0, s>>>(a);
         else if (form == 8) k_sam_head_h16<4, true, 2><<<blocks, 256, 0, s>>>(a);
-        else if (form == 11) k_sam_head_h16<3, true, 0><<<blocks, 256, 0, s>>>(a);   // no DMA (timing only)
+        else if (form == 11) k_sam_head_h16<3, true, 0><<<blocks, 256, 0, s>>>(a);
         else if (form == 12) k_sam_head_h16<3, true, 1, true><<<blocks, 256, 0, s>>>(a);
         else
 #endif

@@ -162,7 +162,8 @@ def near_far(rays_o, rays_d, aabb, min_near):
     box = (ctypes.c_float * 6)(*[float(v) for v in aabb])
     n = torch.empty(N, 1, device=rays_o.device)
     f = torch.empty(N, 1, device=rays_o.device)
-    check(lib().samnerf_near_far(_ptr(rays_o.contiguous()), _ptr(rays_d.contiguous()), N, box,
+    ro, rd = rays_o.contiguous(), rays_d.contiguous()      # held until the launch: _ptr keeps no reference
+    check(lib().samnerf_near_far(_ptr(ro), _ptr(rd), N, box,
                                  float(min_near), _ptr(n), _ptr(f), _stream(rays_o)), "near_far")
     return n, f
 
