@@ -20,8 +20,9 @@
 //   k_mt_bwd     16 rows per workgroup: g_o = w_k dL/dlogits_n, dz2 = (W2^T g_o) *
 //                leaky'(h2), dz1 = (W1^T dz2) * leaky'(h1), dx = W0^T dz1, and
 //                the trilinear scatter of dx's m_grid part into the embedding
-//                gradient (one float atomic per corner and channel, the
-//                reference encoder's backward, gridencoder.cu:252-349);
+//                gradient (float atomics per corner and channel as the
+//                reference encoder's backward, gridencoder.cu:252-349, one per
+//                run of the block's rows that share a corner row);
 //   k_mt_dw      dW0 = dz1^T x, dW1 = dz2^T h1, dW2 = g_o^T h2 over all rows: one
 //                32x32 output tile x 1,024 rows per wave, float atomics.
 // Rows are sample-major (row = k * N + slot), the order in which the render
@@ -272,29 +273,43 @@ __global__ void __launch_bounds__(256) k_mt_bwd(BwdArgs a) {
     // dx of the m_grid part (tiles 0..7 of 9; geo_feat is detached) into Q
     bwd_layer<0, 8>(a.wb, P, w, lane, [&](int v, int j, float d) { Q[v * kRows + j] = d; });
     __syncthreads();
-    // trilinear scatter: one (row, level) per wave-instruction, lane = (corner
-    // c, channel ch): each float atomic instruction adds to 8 corner rows of
-    // 32 contiguous bytes (a thread per (row, level) with 64 atomics of its
-    // own sent 64 lanes to 64 different rows: ~17x slower per byte,
-    // MI355X_MICROARCH.md "Global float atomics")
+    // trilinear scatter: wave w takes levels w, w + 4, .., lane = (corner c,
+    // channel ch), the block's 16 rows in order: each float atomic instruction
+    // adds to 8 corner rows of 32 contiguous bytes (a thread per (row, level)
+    // with 64 atomics of its own sent 64 lanes to 64 different rows: ~17x
+    // slower per byte, MI355X_MICROARCH.md "Global float atomics").  The rows
+    // are neighbouring rays at one sample index, so on the coarse levels
+    // consecutive rows fall in the same cell: a lane keeps adding to its
+    // corner row while the row repeats and sends one atomic per run.
     const int c = lane >> 3, ch = lane & 7;
-    for (int it = w; it < kRows * 16; it += 4) {              // 16 rows x 16 levels over 4 waves
-        const int j = it & 15, l = it >> 4;
-        const uint32_t r = r0 + (uint32_t)j;
-        if (r >= sv.R) continue;                              // wave-uniform
-        const uint32_t k = r / N, s = r % N;
-        const float* up = a.in.u + (size_t)k * 3u * N + s;
-        uint32_t off[8];
-        float cw[8];
-        corner_rows<8>(sLv[l], up[0], up[N], up[2u * N], off, cw);
-        uint32_t o = off[0];
-        float wc = cw[0];
+    for (int l = w; l < 16; l += 4) {
+        uint32_t run = 0xffffffffu;                           // the lane's current corner row (byte offset)
+        float acc = 0.0f;
+        for (int j = 0; j < kRows; ++j) {
+            const uint32_t r = r0 + (uint32_t)j;
+            if (r >= sv.R) break;                             // wave-uniform: the tail block's last rows
+            const uint32_t k = r / N, s = r % N;
+            const float* up = a.in.u + (size_t)k * 3u * N + s;
+            uint32_t off[8];
+            float cw[8];
+            corner_rows<8>(sLv[l], up[0], up[N], up[2u * N], off, cw);
+            uint32_t o = off[0];
+            float wc = cw[0];
 #pragma unroll
-        for (int q = 1; q < 8; ++q) {
-            o = c == q ? off[q] : o;
-            wc = c == q ? cw[q] : wc;
+            for (int q = 1; q < 8; ++q) {
+                o = c == q ? off[q] : o;
+                wc = c == q ? cw[q] : wc;
+            }
+            const float v = wc * Q[(8 * l + ch) * kRows + j];
+            if (o == run) {
+                acc += v;
+            } else {
+                if (run != 0xffffffffu) atomicAdd(a.gemb + run / 4u + ch, acc);
+                run = o;
+                acc = v;
+            }
         }
-        atomicAdd(a.gemb + o / 4u + ch, wc * Q[(8 * l + ch) * kRows + j]);
+        if (run != 0xffffffffu) atomicAdd(a.gemb + run / 4u + ch, acc);
     }
 }
 

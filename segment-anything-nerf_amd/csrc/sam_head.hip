@@ -668,14 +668,8 @@ k_sam_head_h16(HeadArgsH a) {
         }
 }
 
-#ifdef SAMNERF_DIAG_VARIANTS
 // ======================================================= f16x3, persistent
-// Diagnostic form (measured, not faster): one workgroup per CU over its
-// tiles cuts the cycles per tile 9 % (142 k vs 156 k per wave, gap between
-// blocks included), but the shader clock over the kernel falls from 1.89 to
-// 1.77 GHz (s_memtime / s_memrealtime, tools/head_stamps.py): the head runs at
-// the power limit, so the time stays (0.687 vs 0.678 ms, bit-identical).
-// k_sam_head_h16's arithmetic (the same MFMA products in
+// The product head: k_sam_head_h16's arithmetic (the same MFMA products in
 // the same order, the same scales, finishing and LayerNorm: bit-identical
 // output) in a persistent workgroup per CU that walks its 128-ray tiles
 // (tile = blockIdx.x + i * gridDim.x).  Per tile, k_sam_head_h16 spent ~20 k
@@ -691,7 +685,13 @@ k_sam_head_h16(HeadArgsH a) {
 //     (step 11's barrier long passed); layer 0 and the skip input read x
 //     from LDS (conflict-free: row stride 656 B = 41 slots);
 //   * the output stores of tile i drain under tile i + 1's first step.
-// LDS: 48 KiB ring + 84 KiB x + 7 KiB biases / LayerNorm / scales.
+// LDS: 64 KiB ring (4 buffers: the DMA three steps ahead, so an x piece has
+// three steps to arrive from HBM) + 84 KiB x + 7 KiB biases / LayerNorm / scales.
+// Measured (profiles/r3_head_clock.txt): 9 % fewer cycles per tile (142 k vs
+// 156 k per wave), but the head runs at the power limit -- its clock falls
+// from 1.89 to 1.77 GHz when it runs back to back -- so alone it is no
+// faster (0.687 vs 0.678 ms); inside the view (2.1 GHz) it saves 0.04 ms per
+// view (2.955 vs 2.99 ms, tools/head_view_ab.py).  Bit-identical.
 constexpr int kTileBytes = kRaysV5 * kRowIn * 4;    // 83,968 B = 82 KiB
 constexpr int kXPieces = 21;                        // per wave: 84 pieces per tile, 82 carry rows
 constexpr int kXVec = 4 * kXPieces * 64;            // uint4 of the x region
@@ -939,8 +939,6 @@ k_sam_head_h16q(HeadArgsH a, uint32_t ntiles) {
         }
     }                                             // the DMA past the last tile drained
 }
-
-#endif  // SAMNERF_DIAG_VARIANTS
 
 #ifdef SAMNERF_DIAG_VARIANTS
 // ============================================================ f16x3, paired
@@ -1222,7 +1220,6 @@ k_sam_head_h16p(HeadArgsH a) {
 
 }  // namespace
 
-#ifdef SAMNERF_DIAG_VARIANTS
 // compute units of the current device (the persistent head's grid)
 static int device_cus() {
     static int cus[64] = {0};
@@ -1235,7 +1232,6 @@ static int device_cus() {
     }
     return cus[dev];
 }
-#endif
 
 size_t sam_head_packed_floats() {
     const size_t f32 = (size_t)8 * kTotalGroups * 64 * 4;
@@ -1269,12 +1265,12 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         // = the paired 2 / 4-waves-per-SIMD forms (0.78 / 0.84 vs 0.72 ms),
         // 5 / 7 / 8 = two k-blocks per barrier, 6 / 8 = four buffers, 11 = no
         // weight DMA (timing only), 12 = lazy split, 13 = phase stamps,
-        // 20 / 22 = persistent with 3 / 4 buffers, 21 = 22 with clock stamps
+        // 4 = one block per tile (k_sam_head_h16, round 3), 20 = persistent
+        // with 3 buffers, 21 = the product with clock stamps
         const char* v = diag_env("SAMNERF_HEAD_V");
-        const int form = v ? atoi(v) : 4;
+        const int form = v ? atoi(v) : 0;
         const uint32_t grid = blocks < (uint32_t)device_cus() ? blocks : (uint32_t)device_cus();
         if (form == 20) k_sam_head_h16q<3><<<grid, 256, 0, s>>>(a, blocks);
-        else if (form == 22) k_sam_head_h16q<4><<<grid, 256, 0, s>>>(a, blocks);
         else if (form == 21 || form == 13) {                   // stamps (tools/head_stamps.py)
             const char* p = diag_env("SAMNERF_HEAD_STAMPS");
             a.stamps = reinterpret_cast<unsigned long long*>(p ? strtoull(p, nullptr, 16) : 0ull);
@@ -1291,9 +1287,13 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         else if (form == 8) k_sam_head_h16<4, true, 2><<<blocks, 256, 0, s>>>(a);
         else if (form == 11) k_sam_head_h16<3, true, 0><<<blocks, 256, 0, s>>>(a);
         else if (form == 12) k_sam_head_h16<3, true, 1, true><<<blocks, 256, 0, s>>>(a);
+        else if (form == 4) k_sam_head_h16<3, true, 1><<<blocks, 256, 0, s>>>(a);   // one block per tile
         else
 #endif
-        k_sam_head_h16<3, true, 1><<<blocks, 256, 0, s>>>(a);   // 3 buffers, DMA between the MFMAs
+        {
+            const uint32_t grid = blocks < (uint32_t)device_cus() ? blocks : (uint32_t)device_cus();
+            k_sam_head_h16q<4><<<grid, 256, 0, s>>>(a, blocks);   // persistent, one workgroup per CU
+        }
         return check_launch("sam_head_h16");
     }
     const uint32_t nvec = 8u * kTotalGroups * 64u;

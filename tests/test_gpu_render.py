@@ -249,6 +249,34 @@ def test_sam_head_f16x3_scaling_over_wide_ranges(hip_lib, cuda):
     assert e["f16x3"] <= 2.0 * min(e["exact_mfma"], e["cpu_fp32"]) + 1e-7, e
 
 
+@pytest.mark.parametrize("n", [1000, 128 * 300 + 37, 128 * 1024])
+def test_sam_head_persistent_form_bit_identical(hip_lib, cuda, n):
+    """The product head (k_sam_head_h16q: one workgroup per CU over 128-ray
+    tiles, the next tile's rows streamed into LDS, the weight ring running on
+    across tiles) equals the one-block-per-tile kernel (diagnostic form 4) bit
+    for bit: ragged tails, more tiles than compute units (several tiles per
+    workgroup), rows ending at the allocation's end (clamped row pieces)."""
+    from samnerf_amd import _lib
+    from samnerf_amd.fused import FusedRenderer
+    spec = synth.ModelSpec(with_sam=True, grid_log2=12, s_grid_log2=11, prop_log2=10)
+    params = synth.make_params(spec, seed=6, emb_scale=0.5, ln_jitter=0.1)
+    net = make_net(spec, params, cuda)
+    g = torch.Generator().manual_seed(n)
+    rows = torch.randn(n, 164, generator=g)
+    rows *= 10.0 ** (torch.rand(n, 1, generator=g) * 8 - 4)
+    rows[:, 163] = 0.0
+    rows = rows.to(cuda)
+    prod = FusedRenderer(net).sam_head(rows)
+    os.environ["SAMNERF_HEAD_V"] = "4"
+    try:
+        with _lib.diag_library():
+            tile = FusedRenderer(net).sam_head(rows)
+    finally:
+        os.environ.pop("SAMNERF_HEAD_V", None)
+    assert torch.isfinite(prod).all()
+    assert torch.equal(prod, tile)
+
+
 def test_exact_fp32_mode_vs_oracle(hip_lib, cuda):
     """head_mode 1 runs grid_mlp on v_mfma_f32_32x32x2_f32 (an fma chain per
     k pair) as well as the SAM head: against the oracle (torch CPU GEMMs in
