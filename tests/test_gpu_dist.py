@@ -7,6 +7,11 @@ Under the fp32 transport the gathered view must equal, bit for bit, the same
 bands rendered by one process (the same kernels run at the same launch size);
 under q16 each rank's own band is exact and the other band's samvit within
 the codec's bound (2^-14 of the ray's max |samvit|, tile_codec.hip).
+
+The RCCL branch of the gather (`nccl` backend: all_gather_into_tensor on
+RCCL's stream, asynchronous behind the next view) runs here in a world-1
+group on the box's one GPU (two RCCL ranks may not share a device); the 8-GPU
+bench runs it at world 8.
 """
 import os
 import socket
@@ -30,17 +35,18 @@ def _setup():
     return spec, params, pose, intr
 
 
-def _worker(rank, world, port, codec, out_path, q):
+def _worker(rank, world, port, codec, out_path, q, backend="gloo"):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         from samnerf_amd import ops
         from samnerf_amd.dist import ShardedViewPipeline
         from samnerf_amd.fused import FusedRenderer
-        dev = torch.device("cuda", 0)
-        torch.cuda.set_device(dev)
+        assert dist.get_backend() == backend
         spec, params, pose, intr = _setup()
         fr = FusedRenderer(make_net(spec, params, dev))
 
@@ -62,7 +68,7 @@ def _worker(rank, world, port, codec, out_path, q):
         dist.destroy_process_group()
 
 
-def _run_world2(codec, path):
+def _run_world2(codec, path, world=2, backend="gloo"):
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -70,7 +76,7 @@ def _run_world2(codec, path):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, codec, path, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, codec, path, q, backend)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=110) for _ in procs]
@@ -115,3 +121,15 @@ def test_sharded_view_real_renderer_world2(hip_lib, cuda, tmp_path, codec):
     for k in KEYS:
         tol = 1e-4 * (1 + ref[k].abs().max().item()) if k == "depth" else 1e-4
         assert (whole[k] - ref[k]).abs().max().item() < tol, k
+
+
+@pytest.mark.parametrize("codec", ["fp32", "q16"])
+def test_sharded_view_rccl_branch_world1(hip_lib, cuda, tmp_path, codec):
+    """The `nccl` (RCCL) gather path of ShardedViewPipeline on the GPU: a
+    world-1 group renders the whole view as its band; the gathered outputs
+    equal the one-launch render bit for bit (q16: its own band is restored
+    exactly, so also bit for bit)."""
+    got = _run_world2(codec, str(tmp_path / f"rccl_{codec}.pt"), world=1, backend="nccl")
+    _, whole = _single_process_bands(cuda)
+    for k in KEYS:
+        assert torch.equal(got[k], whole[k]), (codec, k, (got[k] - whole[k]).abs().max().item())
