@@ -656,7 +656,7 @@ class ViewRunner:
         return dt, last, stage_avg, stage_src
 
 
-def rooflines(stage_avg, band_rays, head_mode, rates):
+def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None):
     """`roofline` of the dominant kernel and every stage, each against the
     guide peak of the unit closest to saturation:
       l2   -- algorithmic bytes (embedding gathers + ray I/O, ALG_BYTES_PER_RAY)
@@ -669,7 +669,8 @@ def rooflines(stage_avg, band_rays, head_mode, rates):
               x 8 tiles x 3 v_mfma_f32_32x32x16_f16 per 32 rays) / (1024 x 2.4
               GHz x live time), with the PMC MFMA-busy cycles beside it.
     The nominal clock makes every busy fraction a lower bound (the chip runs
-    below 2.4 GHz under load)."""
+    below 2.4 GHz under load); `frac_at_measured_clock` rescales the VALU / MFMA
+    fractions by the stage's measured clock (profiles/kernel_clock.json)."""
     st_rates = (rates or {}).get("stages", {})
     cyc_avail = lambda ms: N_SIMD * CLOCK_GHZ * 1e9 * ms * 1e-3
 
@@ -709,6 +710,12 @@ def rooflines(stage_avg, band_rays, head_mode, rates):
             e["alg_gather_tbs"] = alg / (ms * 1e-3) / 1e12
         e.update(cand[bound])
         e["other_bounds"] = {k: v["frac"] for k, v in cand.items() if k != bound}
+        clk = (clocks or {}).get("stages", {}).get(st)
+        if clk and bound in ("valu", "mfma"):
+            # the same busy cycles over the cycles the stage had at the clock it
+            # ran at (profiles/kernel_clock.json, tools/kernel_clock.py)
+            e["measured_clock_ghz"] = clk
+            e["frac_at_measured_clock"] = e["frac"] * CLOCK_GHZ / clk
         if "ta_busy_frac_in_pmc_run" in r:
             e["ta_busy_frac_in_pmc_run"] = r["ta_busy_frac_in_pmc_run"]
         return e
@@ -732,6 +739,14 @@ def pmc_rates():
     """profiles/pmc_rates.json (tools/pmc_rates.py), or None."""
     try:
         return json.load(open(PMC_RATES))
+    except Exception:
+        return None
+
+
+def stage_clocks():
+    """profiles/kernel_clock.json (tools/kernel_clock.py --json), or None."""
+    try:
+        return json.load(open(os.path.join(REPO, "profiles", "kernel_clock.json")))
     except Exception:
         return None
 
@@ -771,7 +786,7 @@ def main():
     runner = ViewRunner(args, renderer, world, dev, H, W, pose, intr, r0, r1, codec)
     dt, last, stage_avg, stage_src = runner.run(args.steps, args.warmup)
     value = n_total * args.steps / dt
-    roof, stage_roof = rooflines(stage_avg, band_rays, args.head_mode, pmc_rates())
+    roof, stage_roof = rooflines(stage_avg, band_rays, args.head_mode, pmc_rates(), stage_clocks())
 
     side = {}
     if not args.no_alt and world > 1 and with_sam and args.chunks == 0:
