@@ -691,7 +691,8 @@ k_sam_head_h16(HeadArgsH a) {
 // 156 k per wave), but the head runs at the power limit -- its clock falls
 // from 1.89 to 1.77 GHz when it runs back to back -- so alone it is no
 // faster (0.687 vs 0.678 ms); inside the view (2.1 GHz) it saves 0.04 ms per
-// view (2.955 vs 2.99 ms, tools/head_view_ab.py).  Bit-identical.
+// view (2.955 vs 2.99 ms; tools/view_ab.py SAMNERF_HEAD_V=4 times the
+// per-tile form against it).  Bit-identical.
 constexpr int kTileBytes = kRaysV5 * kRowIn * 4;    // 83,968 B = 82 KiB
 constexpr int kXPieces = 21;                        // per wave: 84 pieces per tile, 82 carry rows
 constexpr int kXVec = 4 * kXPieces * 64;            // uint4 of the x region
