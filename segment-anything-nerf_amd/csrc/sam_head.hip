@@ -262,30 +262,48 @@ __device__ __forceinline__ float seg_weight(const float* const* W, int seg, int 
 // packed[step 86][hi/lo][tile 8][lane 64] (8 f16 = 16 B each), then kexp[5]:
 // each weight tensor scaled by the power of two that puts its max |w| in
 // [2^13, 2^14) (f16x3.h), kexp = log2 of that scale.  k_head_wmax finds the
-// five maxima (one workgroup per tensor), k_pack_h16 writes the fragments (one
-// thread per fragment).
+// five maxima as kWmaxParts partial maxima per tensor (5 x 32 workgroups: the
+// one-workgroup-per-tensor form took 32 us per view, a serial chain of ~100
+// loads per thread), k_pack_h16 folds a tensor's partials per workgroup, keeps
+// kexp and writes the fragments (one thread per fragment).
+constexpr int kWmaxParts = 32;
 struct PackArgs {
     const float* W[5];
     uint4* packed;
     int* kexp;
+    float* part;             // [5][kWmaxParts] partial maxima
 };
-__global__ void __launch_bounds__(1024) k_head_wmax(PackArgs a) {
-    __shared__ float wm[16];
-    const int layer = blockIdx.x, tid = threadIdx.x;
+__global__ void __launch_bounds__(256) k_head_wmax(PackArgs a) {
+    __shared__ float wm[4];
+    const int layer = blockIdx.y, tid = threadIdx.x;
     const int n = 256 * kLogicalIn[layer];
+    const int chunk = (n + kWmaxParts - 1) / kWmaxParts;
+    const int i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
     const float* W = a.W[layer];
     float m = 0.0f;
-    for (int i = tid; i < n; i += 1024) m = fmaxf(m, fabsf(W[i]));
+    for (int i = i0 + tid; i < i1; i += 256) m = fmaxf(m, fabsf(W[i]));
     m = wave_max64(m);
     if ((tid & 63) == 0) wm[tid >> 6] = m;
     __syncthreads();
-    if (tid == 0) {
-        for (int w = 1; w < 16; ++w) m = fmaxf(m, wm[w]);
-        a.kexp[layer] = scale_exp_of_max(m);
-    }
+    if (tid == 0) a.part[layer * kWmaxParts + blockIdx.x] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
 }
 __global__ void __launch_bounds__(256) k_pack_h16(PackArgs a) {
+    __shared__ int kx;
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;   // one (step, tile, lane)
+    // a workgroup's 256 fragments are half of one step: one layer
+    const int bstep = (int)((blockIdx.x * blockDim.x) >> 9);
+    int bseg = 0;
+    while (bseg < 5 && bstep >= segBase(bseg + 1)) ++bseg;
+    const int layer = kSegLayer[bseg];
+    if (threadIdx.x < 64) {
+        float m = threadIdx.x < kWmaxParts ? a.part[layer * kWmaxParts + threadIdx.x] : 0.0f;
+        m = wave_max64(m);
+        if (threadIdx.x == 0) {
+            kx = scale_exp_of_max(m);
+            a.kexp[layer] = kx;                 // the same value from every workgroup of the layer
+        }
+    }
+    __syncthreads();
     if (t >= (uint32_t)kSteps * 8u * 64u) return;
     const int lane = (int)(t & 63u), tile = (int)((t >> 6) & 7u), step = (int)(t >> 9);
     int seg = 0;
@@ -296,7 +314,7 @@ __global__ void __launch_bounds__(256) k_pack_h16(PackArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = seg_weight(a.W, seg, kb, h, e, unit);
     uint4 hi, lo;
-    split8_f16(v, exp2i(a.kexp[kSegLayer[seg]]), hi, lo);
+    split8_f16(v, exp2i(kx), hi, lo);
     a.packed[(size_t)step * kStepVec + tile * 64 + lane] = hi;
     a.packed[(size_t)step * kStepVec + 512 + tile * 64 + lane] = lo;
 }
@@ -1236,7 +1254,7 @@ static int device_cus() {
 
 size_t sam_head_packed_floats() {
     const size_t f32 = (size_t)8 * kTotalGroups * 64 * 4;
-    const size_t h16 = (size_t)kPackedVec * 4 + 8;           // fragments + the tensors' log2 scales
+    const size_t h16 = (size_t)kPackedVec * 4 + 8 + 5 * kWmaxParts;   // fragments, log2 scales, partial maxima
     return f32 > h16 ? f32 : h16;
 }
 
@@ -1247,7 +1265,8 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         for (int i = 0; i < 5; ++i) p.W[i] = m->sam_w[i];
         p.packed = reinterpret_cast<uint4*>(packed);
         p.kexp = reinterpret_cast<int*>(packed + (size_t)kPackedVec * 4);
-        k_head_wmax<<<5, 1024, 0, s>>>(p);
+        p.part = packed + (size_t)kPackedVec * 4 + 8;
+        k_head_wmax<<<dim3(kWmaxParts, 5), 256, 0, s>>>(p);
         k_pack_h16<<<div_up((uint32_t)kSteps * 8u * 64u, 256), 256, 0, s>>>(p);
         HeadArgsH a;
         a.rows = rows;
