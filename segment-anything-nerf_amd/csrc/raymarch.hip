@@ -646,8 +646,12 @@ __global__ void __launch_bounds__(256) k_pack_grid_mlp(FinalArgs a, uint4* gpack
     __shared__ int ke[3];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     float m0 = 0.0f, m1 = 0.0f, m2 = 0.0f;
+    // unrolled: the 28 loads per thread issue together (one memory round trip)
+#pragma unroll
     for (int i = tid; i < 64 * 32; i += 256) m0 = fmaxf(m0, fabsf(a.G0[i]));
+#pragma unroll
     for (int i = tid; i < 64 * 64; i += 256) m1 = fmaxf(m1, fabsf(a.G1[i]));
+#pragma unroll
     for (int i = tid; i < 16 * 64; i += 256) m2 = fmaxf(m2, fabsf(a.G2[i]));
     m0 = wave_max64(m0);
     m1 = wave_max64(m1);

@@ -281,6 +281,7 @@ __global__ void __launch_bounds__(256) k_head_wmax(PackArgs a) {
     const int i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
     const float* W = a.W[layer];
     float m = 0.0f;
+#pragma unroll 4
     for (int i = i0 + tid; i < i1; i += 256) m = fmaxf(m, fabsf(W[i]));
     m = wave_max64(m);
     if ((tid & 63) == 0) wm[tid >> 6] = m;
