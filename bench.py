@@ -356,7 +356,7 @@ def train_steps(dev, steps, warmup, torch_adam=False, head="hip"):
         loss = step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return dt * 1e3 / steps, float(loss)
+    return dt * 1e3 / steps, float(loss.detach())
 
 
 def rgb_train_steps(dev, steps, warmup, fused=True, h=64, w=128):

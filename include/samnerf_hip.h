@@ -274,6 +274,12 @@ int samnerf_mask_forward(const samnerf_model* model, uint32_t N, float* instance
  * reference encoder's backward).  weights and geo_feat carry no gradient
  * (.detach() in the reference), the sample positions none (no parameter).
  * Replaces the reference's per-chunk torch ops and autograd of that branch. */
+/* The workspace keeps the head's fp32 activations of all 32 samples of every
+ * ray for the backward -- input (144), both hidden layers and their
+ * gradients (4 x 256) and the logits and their gradient (2 x 32): about 157 KB
+ * per ray, 0.64 GB at the reference's 4,096-ray batch (and the render's own
+ * workspace stays alive until the backward).  Batches of 65,536 rays need
+ * ~10 GB. */
 size_t samnerf_mask_train_workspace_size(uint32_t N);
 int samnerf_mask_train_forward(const samnerf_model* model, uint32_t N, float* instance_mask_logits,
                                const void* render_ws, size_t render_ws_bytes, void* workspace,
@@ -411,10 +417,11 @@ int samnerf_tile_decode(const void* tile, uint32_t N, float* image, float* depth
                         float* weights_sum, float* samvit, samnerf_stream_t stream);
 
 /* Parity taps (tests only; no reference counterpart -- they expose what
- * nerf/renderer.py:261-307 computes between its ops).  While set, every
- * samnerf_render_forward call of this thread over exactly N rays writes the
- * proposal stages' intermediates to these device buffers instead of its
- * workspace (the same kernels run; outputs are unchanged), sample-major:
+ * nerf/renderer.py:261-326 and network.py:221-259 compute between its ops).
+ * While set, every samnerf_render_forward call of this thread over exactly N
+ * rays writes the stages' intermediates to these device buffers as well (the
+ * same kernels run, with one predicated store per tapped value; outputs are
+ * unchanged; rays are not regrouped into pixel tiles), sample-major:
  *   ds0 [128][N], ds1 [64][N]   optical depth delta * sigma of each proposal
  *                               sample (renderer.py:310-311)
  *   w0 [128][N], w1 [64][N]     their composited weights (renderer.py:312-326),
@@ -423,6 +430,21 @@ int samnerf_tile_decode(const void* tile, uint32_t N, float* image, float* depth
  *                               (renderer.py:274-275)
  *   inds1 [65][N], inds2 [33][N]  its torch.searchsorted(cdf, u, right=True)
  *                               indices (renderer.py:105), int32
+ *   sigma2 [32][N]              the final stage's sigma = trunc_exp(density)
+ *                               of every sample (network.py:227, k_final)
+ *   w2 [32][N]                  the final stage's composited weights
+ *                               (renderer.py:312-326)
+ *   u2 [32][3][N]               the final samples' grid-space positions
+ *                               (contract(xyz) + bound) / (2 bound), grid.py:156
+ *   rows2, srows [ceil(N / row_stride)][32][16][8]  uint32, for the rays
+ *                               r % row_stride == 0: the level-relative corner
+ *                               row each trilinear weight multiplies, per final
+ *                               sample, level and corner (bit 0 x, 1 y, 2 z, as
+ *                               gridencoder.cu:61-79): rows2 those of k_final's
+ *                               grid gathers, srows those of the s_grid
+ *                               composite (k_sgrid_box4, N >= 32768 only;
+ *                               samples whose weight is 0 on all 64 rays of a
+ *                               wave are skipped and left unwritten)
  * Any pointer may be NULL.  taps = NULL clears them; a render over another
  * ray count fails with SAMNERF_EINVAL while they are set.  Thread-local. */
 typedef struct {
@@ -434,6 +456,12 @@ typedef struct {
     float* bins2;
     int32_t* inds1;
     int32_t* inds2;
+    float* sigma2;
+    float* w2;
+    float* u2;
+    uint32_t row_stride;
+    uint32_t* rows2;
+    uint32_t* srows;
 } samnerf_taps;
 int samnerf_set_taps(const samnerf_taps* taps, uint32_t N);
 

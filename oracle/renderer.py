@@ -245,6 +245,33 @@ class OracleNeRF:
             sigma, _, _ = self.common_forward(x)
         return {"sigma": sigma}
 
+    @torch.no_grad()
+    def stage_sigmas(self, rays_o, rays_d, bins, stage):
+        """One stage of renderer.py:250-300 at GIVEN bins [N, T+1] (the fused
+        path's own, read through its parity taps): real bins (:250-265),
+        sample positions (:276-281), contract, then network.density with
+        proposal=stage (network.py:248-259) for stages 0-1 or common_forward's
+        sigma (network.py:221-229) for the final stage.  Returns sigmas
+        [N, T], deltas * sigmas [N, T] (renderer.py:310-311, the last sample's
+        as computed, before :313-315 replaces it by inf), real_bins
+        [N, T+1] and the grid-space positions (x + bound) / (2 bound)
+        [N, T, 3] (grid.py:156)."""
+        rays_o = rays_o.contiguous()
+        rays_d = rays_d.contiguous()
+        nears, fars = near_far_from_aabb(rays_o, rays_d, self.aabb, self.spec.min_near)
+        s_nears = spacing_fn(nears)
+        s_fars = spacing_fn(fars)
+        real_bins = spacing_fn_inv(s_nears * (1 - bins) + s_fars * bins)
+        rays_t = (real_bins[..., 1:] + real_bins[..., :-1]) / 2
+        xyzs = rays_o.unsqueeze(1) + rays_d.unsqueeze(1) * rays_t.unsqueeze(2)
+        xyzs = contract(xyzs)
+        if stage < len(self.prop_grids):
+            sigmas = self.density(xyzs, proposal=stage)["sigma"]
+        else:
+            sigmas, _, _ = self.common_forward(xyzs)
+        deltas = real_bins[..., 1:] - real_bins[..., :-1]
+        return sigmas, deltas * sigmas, real_bins, (xyzs + self.bound) / (2 * self.bound)
+
     def sam_head(self, f):
         """samvit_mlp = Sequential(SkipConnMLP(163,256,256,5,skip=[2]), LayerNorm(256))."""
         x = skip_mlp(f, self.sam_layers)

@@ -456,9 +456,10 @@ int mask_train_backward(const samnerf_model* m, const GridDesc<16>& grid, const 
     if (ws_bytes < L.bytes)
         return fail(SAMNERF_EWORKSPACE, "mask_train_backward: workspace needs %zu bytes, got %zu", L.bytes,
                     ws_bytes);
-    (void)hipMemsetAsync(grad_w[0], 0, sizeof(float) * 256 * kIn0, s);
-    (void)hipMemsetAsync(grad_w[1], 0, sizeof(float) * 256 * 256, s);
-    (void)hipMemsetAsync(grad_w[2], 0, sizeof(float) * mw.K * 256, s);
+    if (hipMemsetAsync(grad_w[0], 0, sizeof(float) * 256 * kIn0, s) != hipSuccess ||
+        hipMemsetAsync(grad_w[1], 0, sizeof(float) * 256 * 256, s) != hipSuccess ||
+        hipMemsetAsync(grad_w[2], 0, sizeof(float) * mw.K * 256, s) != hipSuccess)
+        return fail(SAMNERF_ELAUNCH, "mask_train_backward: zeroing the weight gradients failed");
     BwdArgs b;
     b.in = SampleIn{grid, u_f, w_f, geo_f, N};
     b.wb = L.wb;

@@ -541,6 +541,12 @@ struct FinalArgs {
     } n1;
     double* st_d;      // [3][N] optical depth, sum w, sum w t (slot order)
     float* st_f;       // [16][N] sum w * grid_mlp rows
+    // parity taps (samnerf_taps; null in every product render): sigma of
+    // every sample [T][N], and the corner rows of every level of the samples
+    // of slots r % tap_stride == 0, [N / tap_stride][T][16][8]
+    float* sigma_tap;
+    uint32_t* rows_tap;
+    uint32_t tap_stride;
 };
 
 constexpr int kAeff = 240;          // columns of the adaptive heads' effective matrix
@@ -637,7 +643,7 @@ __device__ float grid_weight_exact(const FinalArgs& a, int step, int lane) {
 
 // grid_mlp fragments for the f16x3 form (head_mode 0, f16x3.h), once per
 // render (one workgroup): each weight tensor scaled by the power of two that
-// puts its max |w| in [2^14, 2^15), in grid_weight's slot layout, hi then lo;
+// puts its max |w| in [2^13, 2^14) (scale_exp_of_max), in grid_weight's slot layout, hi then lo;
 // gexp[l] = log2 of tensor l's scale.  (A per-tensor scale: the scaled
 // accumulators of a sample column then differ from the true values by one
 // factor, so each layer's outputs are rescaled straight from their max.)
@@ -702,10 +708,16 @@ struct SlotKinds {
     uint32_t dense, hashed;
 };
 
+// tap (parity taps only, samnerf_taps.rows2; null otherwise): the level-
+// relative row each corner weight multiplies, tap[l * tap_ls + c] for slot l
+// and corner c (bit 0 x, 1 y, 2 z, as gridencoder.cu:61-79 / the oracle's
+// corner order) -- the rows the loads below read.  A dense pair's top cell
+// reads (top - 1, top) with weights (0, 1), recorded as such.
 template <int NL>
 __device__ __forceinline__ void gather_issue_c2(const float2* __restrict__ emb, const LevelDesc* d,
                                                 float ux, float uy, float uz, GatherC2<NL>& g,
-                                                SlotKinds kinds = SlotKinds{0u, 0u}) {
+                                                SlotKinds kinds = SlotKinds{0u, 0u},
+                                                uint32_t* tap = nullptr, int tap_ls = 8) {
     // byte offsets of every corner (dense-pair slots: of the 4 pairs) first,
     // then all loads, so they are in flight together
     uint32_t row[NL][8];
@@ -750,6 +762,22 @@ __device__ __forceinline__ void gather_issue_c2(const float2* __restrict__ emb, 
             for (int c = 0; c < 8; ++c) {
                 const uint32_t xs = X[c & 1], ys = Y[(c >> 1) & 1], zs = Z[c >> 2];
                 row[l][c] = (d[l].off + (hashed ? ((xs ^ ys ^ zs) & mask) : (xs + ys + zs))) << 3;
+            }
+        }
+    }
+    if (tap) {
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            if ((kinds.dense >> l) & 1u) {
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const uint32_t r0 = (row[l][p] >> 3) - d[l].off;
+                    tap[l * tap_ls + 2 * p] = r0;
+                    tap[l * tap_ls + 2 * p + 1] = r0 + 1u;
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) tap[l * tap_ls + c] = (row[l][c] >> 3) - d[l].off;
             }
         }
     }
@@ -816,9 +844,10 @@ __device__ __forceinline__ void gather_finish_c2(const GatherC2<NL>& g, float* f
 template <int NL, bool PK = false>
 __device__ __forceinline__ void gather_levels_c2(const float2* __restrict__ emb, const LevelDesc* d,
                                                  float ux, float uy, float uz, float* f,
-                                                 SlotKinds kinds = SlotKinds{0u, 0u}) {
+                                                 SlotKinds kinds = SlotKinds{0u, 0u},
+                                                 uint32_t* tap = nullptr, int tap_ls = 8) {
     GatherC2<NL> g;
-    gather_issue_c2<NL>(emb, d, ux, uy, uz, g, kinds);
+    gather_issue_c2<NL>(emb, d, ux, uy, uz, g, kinds, tap, tap_ls);
     gather_finish_c2<NL, PK>(g, f);
 }
 
@@ -921,7 +950,7 @@ k_final(FinalArgs a) {
             d[c] = a.rays_d[(size_t)ray * 3 + c];
         }
     }
-    const int i_begin = EXIT ? a.i0 : 0, i_end = EXIT ? a.i1 : TS;
+    const int i_begin = EXIT ? a.i0 : 0, i_end = EXIT ? min(a.i1, TS) : TS;
     const float sn = a.snf[rr], sf = a.snf[N + rr];
     float rb_prev = real_bin(sn, sf, a.bins_in[(size_t)(i_begin * S + seg) * N + rr]);
     double cum = 0.0, wsum = 0.0, depth = 0.0;            // cum: optical depth before this step
@@ -1036,7 +1065,7 @@ k_final(FinalArgs a) {
         floatx16 h1a = {}, h1b = {};
         float fk[AD ? 16 : 1];                           // AD: this sample's grid features (by k-block)
         // f16x3 (f16x3.h): each layer's B operands are scaled by the power of
-        // two that puts the sample column's max |input| in [2^14, 2^15);
+        // two that puts the sample column's max |input| in [2^13, 2^14);
         // e_h1 / e_h2 / e_o3 = log2 of the factor a layer's accumulators carry
         // over the true values (input scales + weight-tensor scales).  Layer 1
         // takes its two k-blocks one at a time (holding the first block's
@@ -1055,7 +1084,11 @@ k_final(FinalArgs a) {
             } else {
                 LevelDesc dl[4];
                 levels(kb, dl);
-                gather_levels_c2<4, S == 1>(emb, dl, ux, uy, uz, f, kinds(kb));
+                // parity taps: this half-wave's levels 8 kb + hh + 2 q of the sample
+                uint32_t* rt = nullptr;
+                if (a.rows_tap && live && r % a.tap_stride == 0u)
+                    rt = a.rows_tap + ((size_t)(r / a.tap_stride) * T + k) * 128u + (8 * kb + hh) * 8;
+                gather_levels_c2<4, S == 1>(emb, dl, ux, uy, uz, f, kinds(kb), rt, 16);
             }
             if constexpr (AD > 0) {
 #pragma unroll
@@ -1198,6 +1231,7 @@ k_final(FinalArgs a) {
         }
         const float w = nan_to_num((1.0f - expf(-ds)) * expf(-(float)before));
         if (sample_writer) a.w_out[(size_t)k * N + r] = w;
+        if (a.sigma_tap && sample_writer) a.sigma_tap[(size_t)k * N + r] = sigma;
         wsum += (double)w;
         depth += (double)(w * t);
 #pragma unroll
@@ -1402,6 +1436,11 @@ struct SgridArgs {
     const float* u_in;   // [T][3][N]
     const float* w_in;   // [T][N]
     float* rows;         // [N, kRow]
+    // parity taps (samnerf_taps.srows; null in every product render): the
+    // corner rows of every level of the samples of slots r % tap_stride == 0,
+    // [N / tap_stride][T][16][8] (k_sgrid_box4)
+    uint32_t* rows_tap;
+    uint32_t tap_stride;
 };
 
 // f_sam = sum_k w_k * s_grid(x_k).  A block is one level x 64 neighbouring
@@ -1492,7 +1531,11 @@ constexpr uint32_t kBoxSlots = 256;          // 32 B slots per wave (8 KiB)
 #ifndef SAMNERF_DIAG_SGRID_WAVES
 #define SAMNERF_DIAG_SGRID_WAVES 4
 #endif
-template <int T>
+// TAP: the parity-tap instantiation (samnerf_taps.srows): the same kernel plus
+// the corner-row stores, its own instantiation because the tap code raised the
+// product form's spills (20 -> 60 bytes of scratch at 4 waves per SIMD); the
+// tapped render's outputs are checked bit-identical to the product's.
+template <int T, bool TAP = false>
 __global__ void __launch_bounds__(256)
 #if SAMNERF_DIAG_SGRID_WAVES
 __attribute__((amdgpu_waves_per_eu(SAMNERF_DIAG_SGRID_WAVES, SAMNERF_DIAG_SGRID_WAVES)))
@@ -1557,15 +1600,19 @@ k_sgrid_box4(SgridArgs a) {
             for (int l = 0; l < 4; ++l) {
                 const PBox b = pbox_read(p0, p1, p2, l);
                 float f[8];
+                uint32_t* rt = nullptr;                     // parity taps only
+                if (TAP && live && r % a.tap_stride == 0u)
+                    rt = a.rows_tap + ((size_t)(r / a.tap_stride) * T + k) * 128u + (4 * g + l) * 8;
                 if (b.slots <= kBoxSlots) {
                     wave_lds_sync();                        // previous level's reads done
                     stage_pbox<8>(base, L[l], b, slice, lane);
                     wave_lds_sync();
                     if (ordered)
-                        lookup_level3_pbox<8, false>(a.grid.emb, L[l], b, slice, ux, uy, uz, f);
+                        lookup_level3_pbox<8, false>(a.grid.emb, L[l], b, slice, ux, uy, uz, f, rt);
                     else
-                        lookup_level3_pbox<8, true>(a.grid.emb, L[l], b, slice, ux, uy, uz, f);
+                        lookup_level3_pbox<8, true>(a.grid.emb, L[l], b, slice, ux, uy, uz, f, rt);
                 } else {
+                    if (rt) tap_direct_rows<8>(L[l], ux, uy, uz, rt);
                     lookup_level3<8>(a.grid.emb, L[l], ux, uy, uz, f);
                 }
                 add(l, f);
@@ -2110,8 +2157,10 @@ void launch_final(int seg, bool pf, uint32_t N, hipStream_t s, const FinalArgs& 
         return;
     }
     if (fa.exit_depth < INFINITY) {                      // N1 (no prefetch form)
+        // a pass marches [p cs, (p + 1) cs) of the TS = 32 / seg steps of each
+        // slot (passes over chunks only with seg == 1: n1_passes)
         const int chunks = seg == 1 && fa.n1.list ? n1_chunks() : 1;
-        const int cs = 32 / chunks;
+        const int cs = (32 / seg) / chunks;
         uint32_t* list[2] = {fa.n1.list, fa.n1.list + N};
         for (int p = 0; p < chunks; ++p) {              // ray compaction between sample chunks
             FinalArgs f = fa;
@@ -2175,6 +2224,17 @@ Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
     w.n1_stf = take(n1 ? 16 * n : 0);
     w.bytes = off;
     return w;
+}
+
+// Parity taps: the final samples' weights and positions, which the render
+// keeps in its workspace, copied out after the stages that read them.
+int copy_final_taps(const samnerf_taps& tp, const Workspace& w, uint32_t N, hipStream_t s) {
+    const size_t n = N;
+    if (tp.w2 && hipMemcpyAsync(tp.w2, w.w_f, 32 * n * sizeof(float), hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return fail(SAMNERF_ELAUNCH, "render: copying the w2 tap failed");
+    if (tp.u2 && hipMemcpyAsync(tp.u2, w.u_f, 96 * n * sizeof(float), hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return fail(SAMNERF_ELAUNCH, "render: copying the u2 tap failed");
+    return SAMNERF_OK;
 }
 
 int make_grid_desc(const samnerf_grid& g, uint32_t C, uint32_t L, GridDesc<16>& d,
@@ -2478,8 +2538,13 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     if (!(m->t_thresh >= 0.0f && m->t_thresh < 1.0f))
         return fail(SAMNERF_EINVAL, "render_forward: t_thresh %g outside [0, 1)", (double)m->t_thresh);
     fa.exit_depth = m->t_thresh > 0.0f ? -logf(m->t_thresh) : INFINITY;
+    if (tp.row_stride == 0 && (tp.rows2 || tp.srows))
+        return fail(SAMNERF_EINVAL, "render: taps rows2 / srows need row_stride > 0");
+    fa.sigma_tap = tp.sigma2;
+    fa.rows_tap = tp.rows2;
+    fa.tap_stride = tp.row_stride ? tp.row_stride : 1u;
     fa.i0 = 0;
-    fa.i1 = 32;                                          // reset below for S > 1 (EXIT only reads it)
+    fa.i1 = 32;                                          // steps per slot, 32 / seg (set below; EXIT only)
     if (m->t_thresh > 0.0f) {                            // N1: ray compaction buffers (k_final passes)
         fa.n1.list = w.n1_list;
         fa.n1.cnt = w.n1_cnt;
@@ -2547,23 +2612,32 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
         sa.u_in = w.u_f;
         sa.w_in = w.w_f;
         sa.rows = rows;
+        sa.rows_tap = tp.srows;
+        sa.tap_stride = tp.row_stride ? tp.row_stride : 1u;
         mark_stage(3, s);
         const dim3 sg(xcd_blocks(div_up(N, 64)), 16);
-        if (look == kLookRef) k_sgrid<32, kLookRef><<<sg, 256, 0, s>>>(sa);
-        else if ((look == kLookBox4 || (look == kLookAuto && N >= kBox4MinRays)) && box4_ok(gs) &&
-                 (uint64_t)N * 384u < (1ull << 32))
-            k_sgrid_box4<32><<<dim3(xcd_blocks(div_up(N, 64)), 4), 256, 0, s>>>(sa);
-        else k_sgrid<32, kLookPacked><<<sg, 256, 0, s>>>(sa);
+        const dim3 sb(xcd_blocks(div_up(N, 64)), 4);
+        if (look == kLookRef) {
+            k_sgrid<32, kLookRef><<<sg, 256, 0, s>>>(sa);
+        } else if ((look == kLookBox4 || (look == kLookAuto && N >= kBox4MinRays)) && box4_ok(gs) &&
+                   (uint64_t)N * 384u < (1ull << 32)) {
+            if (sa.rows_tap) k_sgrid_box4<32, true><<<sb, 256, 0, s>>>(sa);
+            else k_sgrid_box4<32><<<sb, 256, 0, s>>>(sa);
+        } else {
+            k_sgrid<32, kLookPacked><<<sg, 256, 0, s>>>(sa);
+        }
         if ((rc = check_launch("render"))) return rc;
         mark_stage(4, s);
         if (samvit) rc = sam_head_forward(m, rows, N, samvit, w.packed, s);
         mark_stage(5, s);
+        if (rc == SAMNERF_OK) rc = copy_final_taps(tp, w, N, s);
         return rc;
     }
     mark_stage(3, s);
     mark_stage(4, s);
     mark_stage(5, s);
-    return check_launch("render");
+    if ((rc = check_launch("render"))) return rc;
+    return copy_final_taps(tp, w, N, s);
 }
 
 int samnerf_set_stage_events(void* const* events, uint32_t n) {

@@ -234,12 +234,27 @@ __device__ __forceinline__ bool wave_positions_ordered(float ux, float uy, float
     return __builtin_amdgcn_ballot_w64(ux != ux || uy != uy || uz != uz) == 0;
 }
 
+// Parity taps (samnerf_taps.srows; never in a product render): the
+// level-relative rows of the 8 corners a direct lookup_level3<C> reads.
+template <int C>
+__device__ __forceinline__ void tap_direct_rows(const LevelDesc& d, float ux, float uy, float uz,
+                                                uint32_t* tap) {
+    uint32_t off[8];
+    float w[8];
+    corner_rows<C>(d, ux, uy, uz, off, w);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) tap[c] = off[c] / (uint32_t)(C * 4) - d.off;
+}
+
 // lookup_level3 from a staged padded box (same rows, weights, FMA order);
 // with CHECK, a lane whose corners are outside the box gathers directly.
+// tap (parity taps only; null otherwise): the row staged into each LDS slot
+// the 8 corners read (stage_pbox's slot -> cell decoding), level-relative.
 template <int C, bool CHECK = true>
 __device__ __forceinline__ void lookup_level3_pbox(const float* __restrict__ emb, const LevelDesc& d,
                                                    const PBox& b, const float* slice, float ux,
-                                                   float uy, float uz, float* acc) {
+                                                   float uy, float uz, float* acc,
+                                                   uint32_t* tap = nullptr) {
     uint32_t cx, cy, cz;
     float fx, fy, fz;
     locate_axis(ux, d, cx, fx);
@@ -253,6 +268,7 @@ __device__ __forceinline__ void lookup_level3_pbox(const float* __restrict__ emb
     if constexpr (CHECK) {
         const bool inside = lx0 < b.ex && lx1 < b.ex && ly0 < b.ey && ly1 < b.ey && lz0 < b.ez && lz1 < b.ez;
         if (!inside) {
+            if (tap) tap_direct_rows<C>(d, ux, uy, uz, tap);
             lookup_level3<C>(emb, d, ux, uy, uz, acc);
             return;
         }
@@ -272,6 +288,14 @@ __device__ __forceinline__ void lookup_level3_pbox(const float* __restrict__ emb
     off[5] = off[4] + DX;
     off[6] = off[4] + DY;
     off[7] = off[6] + DX;
+    if (tap) {
+        const uint32_t xm = (1u << b.lx) - 1u, ym = (1u << b.ly) - 1u;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t j = off[c] / RB;
+            tap[c] = dense_or_hash_row(b.x0 + (j & xm), b.y0 + ((j >> b.lx) & ym), b.z0 + (j >> lxy), d);
+        }
+    }
     f2v wc[4];
     corner_weights_pk(fx, fy, fz, wc);
     const char* sb = reinterpret_cast<const char*>(slice);

@@ -106,7 +106,8 @@ class SamnerfAdamTensor(ctypes.Structure):
 class SamnerfTaps(ctypes.Structure):
     """samnerf_taps (include/samnerf_hip.h): parity-test taps of the render."""
     _fields_ = [("ds0", _vp), ("ds1", _vp), ("w0", _vp), ("w1", _vp), ("bins1", _vp),
-                ("bins2", _vp), ("inds1", _vp), ("inds2", _vp)]
+                ("bins2", _vp), ("inds1", _vp), ("inds2", _vp), ("sigma2", _vp), ("w2", _vp),
+                ("u2", _vp), ("row_stride", _u32), ("rows2", _vp), ("srows", _vp)]
 
 
 class SamnerfRgbTrainOpts(ctypes.Structure):
@@ -157,10 +158,12 @@ _diag = None
 
 @contextlib.contextmanager
 def diag_library():
-    """Tests only: route every call of this thread's renders through the
-    diagnostic build (libsamnerf_hip_diag.so), whose kernels read the A/B
-    variant switches (SAMNERF_LOOKUP, SAMNERF_FINAL_S, ...) from the
-    environment -- the product library has one path per configuration."""
+    """Tests and tools only: while the context is active, EVERY call of the
+    process (all threads: the swap is of the module-global library handle)
+    goes through the diagnostic build (libsamnerf_hip_diag.so), whose kernels
+    read the A/B variant switches (SAMNERF_LOOKUP, SAMNERF_FINAL_S, ...) from
+    the environment -- the product library has one path per configuration.
+    Not for use while product renders run on other threads."""
     global _lib, _diag
     if _diag is None:
         _diag = _load(DIAG_LIB_PATH)

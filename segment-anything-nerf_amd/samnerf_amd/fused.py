@@ -200,10 +200,15 @@ class FusedRenderer:
         (optional [N,164] tensor) receives the head input cat(f_sam, f_image,
         image, depth).  feats=False skips the SAM-feature stages (the
         reference computes and discards them when return_feats == 0).
-        taps=True (parity tests) adds the proposal stages' intermediates
+        taps=True (parity tests) adds the stages' intermediates
         (samnerf_set_taps): ds0 [N,128], ds1 [N,64], their weights w0, w1, bins1 [N,65],
-        bins2 [N,33] and their searchsorted indices inds1, inds2 (int32),
-        ray-major views of the kernels' sample-major buffers.
+        bins2 [N,33] and their searchsorted indices inds1, inds2 (int32), the
+        final stage's sigma2, w2 [N,32] and positions u2 [N,32,3] -- ray-major
+        views of the kernels' sample-major buffers -- and, for the rays
+        tap_rays = arange(0, N, stride), the corner rows rows2 (grid, k_final)
+        and srows (s_grid, k_sgrid_box4; -1 where a sample was skipped)
+        [len(tap_rays), 32, 16, 8] int32 (level-relative).  taps=<int> sets
+        that stride (default 61).
         own_workspace=True renders into a fresh workspace (from torch's
         caching allocator) instead of the per-stream one, so a caller can
         keep it (training: the backward reads its sample weights/positions).
@@ -268,13 +273,20 @@ class FusedRenderer:
         tap = None
         if taps:
             steps = [int(v) for v in m.num_steps]
+            stride = 61 if taps is True else int(taps)
+            n_tap = (N + stride - 1) // stride
             tap = {"ds0": torch.empty(steps[0], N, device=dev), "ds1": torch.empty(steps[1], N, device=dev),
                    "w0": torch.empty(steps[0], N, device=dev), "w1": torch.empty(steps[1], N, device=dev),
                    "bins1": torch.empty(steps[1] + 1, N, device=dev),
                    "bins2": torch.empty(steps[2] + 1, N, device=dev),
                    "inds1": torch.empty(steps[1] + 1, N, device=dev, dtype=torch.int32),
-                   "inds2": torch.empty(steps[2] + 1, N, device=dev, dtype=torch.int32)}
-            st = SamnerfTaps(*[t.data_ptr() for t in tap.values()])
+                   "inds2": torch.empty(steps[2] + 1, N, device=dev, dtype=torch.int32),
+                   "sigma2": torch.empty(steps[2], N, device=dev), "w2": torch.empty(steps[2], N, device=dev),
+                   "u2": torch.empty(steps[2], 3, N, device=dev)}
+            rows_tap = {"rows2": torch.full((n_tap, steps[2], 16, 8), -1, device=dev, dtype=torch.int32),
+                        "srows": torch.full((n_tap, steps[2], 16, 8), -1, device=dev, dtype=torch.int32)}
+            st = SamnerfTaps(*[t.data_ptr() for t in tap.values()], stride,
+                             rows_tap["rows2"].data_ptr(), rows_tap["srows"].data_ptr())
             check(lib().samnerf_set_taps(ctypes.byref(st), N), "set_taps")
         try:
             check(lib().samnerf_render_forward(
@@ -294,7 +306,11 @@ class FusedRenderer:
         if mask and mask_logits:
             out["instance_mask_logits"] = logits
         if tap is not None:
+            u2 = tap.pop("u2")
             out.update({k: v.t() for k, v in tap.items()})
+            out["u2"] = u2.permute(2, 0, 1)
+            out.update(rows_tap)
+            out["tap_rays"] = torch.arange(0, N, stride)
         if samvit is not None:
             out["samvit"] = samvit
         if keep_workspace:

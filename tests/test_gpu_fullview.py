@@ -18,7 +18,17 @@ nerf/renderer.py:221-362 without the SAM branch) and a with_sam model (config
   oracle's full render, with the end-to-end index mismatch rate reported: there
   the two sides' float chains are independent (the proposal MLPs sum in
   another order than torch's CPU GEMM, exp is another libm), so an index can
-  flip where u_j lies within an ulp of a cdf entry.
+  flip where u_j lies within an ulp of a cdf entry;
+* per sample, every sample of every ray, all three stages: sigma
+  (network.py:221-259) against the oracle's density at the fused path's own
+  sample positions (its bins, read through the taps) -- the proposal stages'
+  delta * sigma, the final stage's sigma itself -- within 1e-3 relative (the
+  north star's sigma bar); the final positions bit-exact; the final weights
+  against the oracle's compositing (renderer.py:310-326) of the ORACLE's sigma;
+* the corner rows (gridencoder.cu:61-79) of every level and corner of every
+  final sample of a subset of rays (every 61st), for the main grid (k_final)
+  and the s_grid composite (k_sgrid_box4), bit-exact against the oracle's
+  get_grid_index restatement (oracle/encoders_oracle.c corner_row).
 """
 import numpy as np
 import pytest
@@ -136,3 +146,93 @@ def test_view_invariants(view):
     assert int(o["inds1"].min()) >= 1 and int(o["inds1"].max()) <= 129
     assert int(o["inds2"].min()) >= 1 and int(o["inds2"].max()) <= 65
     np.testing.assert_array_equal(o["image"].shape, (N, 3))
+
+
+SIG_TOL = 1e-3             # north star: sigma within 1e-3 (relative here)
+
+
+def _rel_err(got, ref):
+    """max |got - ref| / |ref| over ref != 0; exact where ref == 0."""
+    nz = ref != 0
+    assert torch.equal(got[~nz], ref[~nz]), "sigma differs where the oracle's is 0"
+    return ((got[nz] - ref[nz]).abs() / ref[nz].abs()).max().item() if nz.any() else 0.0
+
+
+def test_sigma_every_sample_matches_oracle(view):
+    """sigma of every sample of all three stages against the oracle's density
+    at the fused path's own positions (OracleNeRF.stage_sigmas, pinned to the
+    goldens by tests/test_oracle.py::test_stage_sigmas_restates_run)."""
+    o, model = view["out"], oracle_for(view["spec"], view["params"])
+    errs = {"ds0_rel": 0.0, "ds1_rel": 0.0, "sigma2_rel": 0.0, "w2_abs": 0.0}
+    u2_same = 0
+    for h in range(0, N, CHUNK):
+        sl = slice(h, h + CHUNK)
+        ro, rd = view["ro"][sl], view["rd"][sl]
+        n = ro.shape[0]
+        bins0 = torch.linspace(0, 1, 129).unsqueeze(0).expand(n, -1)
+        for st, bins, key in ((0, bins0, "ds0"), (1, o["bins1"][sl], "ds1")):
+            _, ds, _, _ = model.stage_sigmas(ro, rd, bins, st)
+            errs[f"{key}_rel"] = max(errs[f"{key}_rel"], _rel_err(o[key][sl], ds))
+        sig, _, rb, u01 = model.stage_sigmas(ro, rd, o["bins2"][sl], 2)
+        errs["sigma2_rel"] = max(errs["sigma2_rel"], _rel_err(o["sigma2"][sl], sig))
+        w_ref = orc.composite_weights(rb, sig)                # the ORACLE's sigma composited
+        errs["w2_abs"] = max(errs["w2_abs"], (o["w2"][sl] - w_ref).abs().max().item())
+        u2_same += int(torch.equal(o["u2"][sl], u01))
+    print(f"512x512 per-sample ({'cfg3' if view['with_sam'] else 'cfg2'}):", errs,
+          f"final positions bit-exact in {u2_same} of {N // CHUNK} chunks")
+    assert u2_same == N // CHUNK
+    for k in ("ds0_rel", "ds1_rel", "sigma2_rel"):
+        assert errs[k] < SIG_TOL, (k, errs)
+    assert errs["w2_abs"] < 1e-4, errs
+
+
+def _check_rows(got, pos, grid, what):
+    """got [n, 32, 16, 8] int32 (-1 = sample skipped), pos [n, 32, 3]:
+    against the oracle's corner rows.  k_final's dense pair loads read the
+    top x cell as the pair (top - 1, top) with weights (0, 1) where the
+    reference reads (top, top) with (1, 0): same sum bit for bit
+    (samnerf_common.h lookup_dense_c2_paired), recorded as such by the tap."""
+    from oracle import encoders as enc
+    n = got.shape[0]
+    _, ref = enc.grid_encode_forward(pos.reshape(-1, 3).numpy(), grid.embeddings, grid.offsets,
+                                     grid.L, grid.S, grid.H, return_rows=True)
+    ref = torch.from_numpy(ref.astype(np.int64)).reshape(grid.L, n, 32, 8).permute(1, 2, 0, 3)
+    g = got.long()
+    written = g[..., 0] >= 0
+    frac = written.float().mean().item()
+    eq = (g == ref).all(-1)
+    # dense top-x-cell pairs: corners (2p, 2p + 1) read (R - 1, R) where the
+    # reference reads (R, R)
+    e, o_ = g[..., 0::2], g[..., 1::2]
+    re, ro_ = ref[..., 0::2], ref[..., 1::2]
+    edge = ((e == re) & (o_ == ro_)) | ((e == re - 1) & (o_ == re) & (ro_ == re))
+    eq_edge = edge.all(-1)
+    n_edge = int((eq_edge & ~eq & written).sum())
+    bad = int((written & ~eq_edge).sum())
+    print(f"{what}: {int(written.sum())} (sample, level) entries written ({frac:.4%}), "
+          f"{bad} differ, {n_edge} top-cell pairs")
+    assert bad == 0
+    return frac
+
+
+def test_corner_rows_bit_exact(view):
+    """k_final's and k_sgrid_box4's corner rows of every level, for the final
+    samples of every 61st ray, against the oracle's get_grid_index."""
+    o, model = view["out"], oracle_for(view["spec"], view["params"])
+    rays = o["tap_rays"]
+    pos = o["u2"][rays]                                     # [n, 32, 3], bit-exact vs the oracle
+    assert _check_rows(o["rows2"], pos, model.grid, "grid (k_final)") == 1.0
+    if view["with_sam"]:
+        assert _check_rows(o["srows"], pos, model.s_grid, "s_grid (k_sgrid_box4)") > 0.99
+    else:
+        assert (o["srows"] == -1).all()
+
+
+def test_taps_leave_outputs_unchanged(view, cuda):
+    """The tapped render (the taps' stores, k_sgrid_box4's TAP instantiation)
+    gives the product render's outputs bit for bit."""
+    from samnerf_amd.fused import FusedRenderer
+    net = make_net(view["spec"], view["params"], cuda)
+    out = FusedRenderer(net).render(view["ro"].to(cuda), view["rd"].to(cuda))
+    for k in ("image", "depth", "weights_sum") + (("samvit",) if view["with_sam"] else ()):
+        assert torch.equal(out[k].cpu(), view["out"][k]), k

@@ -130,3 +130,38 @@ def test_compaction_error_bounded_by_threshold(hip_lib, scene, monkeypatch, diag
     assert (drop > 0).float().mean().item() > 0.1
     assert drop.max().item() <= t * 1.001 + 1e-6
     assert max_abs(out["image"], ref["image"]) <= t + 1e-3
+
+
+def _align256(nbytes):
+    return (nbytes + 255) // 256 * 256
+
+
+def test_early_exit_nan_sigma_stays_in_its_segment(hip_lib, cuda):
+    """a small view's rays are cut into 4 segments of 8
+    steps (N < 32768), and k_final's N1 form must stop at 8 steps even when no
+    ray ever closes -- here every sigma is NaN (cum NaN never exceeds
+    -ln t).  The head-input rows region, which follows the final weights in
+    the workspace (raymarch.hip carve) and is unused by an RGB-only render,
+    is filled with a canary that must survive."""
+    from samnerf_amd.fused import FusedRenderer
+    spec = synth.ModelSpec(with_sam=False, grid_log2=14, prop_log2=12)
+    net = make_net(spec, synth.make_params(spec, seed=5, emb_scale=0.5), cuda)
+    from oracle import renderer as orc
+    pose, intr = synth.gui_camera(W, H, rot=synth.random_rotation(1))
+    ro, rd = orc.get_rays(pose, intr, H, W)
+    ro, rd = ro.to(cuda), rd.to(cuda)
+    N = ro.shape[0]
+    assert N < 32768                                     # 4 segments per ray
+    fr = FusedRenderer(net, t_thresh=1e-3)
+    ws = fr.render(ro, rd, keep_workspace=True)["_workspace"][0]
+    with torch.no_grad():
+        net.grid_mlp.net[2].weight[0].fill_(float("nan"))   # sigma row of grid_mlp's last layer
+    # carve(): snf 2N, bins1 65N, bins2 33N, wtmp 128N, u_f 96N, w_f 32N, rows 164N floats
+    off = sum(_align256(4 * f * N) for f in (2, 65, 33, 128, 96, 32))
+    region = ws[off:off + 4 * 164 * N]
+    region.fill_(0x5A)
+    out = fr.render(ro, rd, keep_workspace=True)
+    torch.cuda.synchronize()
+    assert out["_workspace"][0].data_ptr() == ws.data_ptr()
+    assert bool((region == 0x5A).all()), "k_final wrote past its segment's steps"
+    print("NaN-sigma N1 render: weights_sum range", out["weights_sum"].min().item(), out["weights_sum"].max().item())

@@ -46,6 +46,27 @@ def test_oracle_render_matches_reference_golden(oracle_lib, name):
         assert np.array_equal(out["instance_mask_logits"].numpy(), fx["instance_mask_logits"])
 
 
+@pytest.mark.parametrize("name", ["render_small_sam", "render_small_rgb"])
+def test_stage_sigmas_restates_run(oracle_lib, name):
+    """OracleNeRF.stage_sigmas (the per-sample sigma checker of the GPU
+    parity tests) at run()'s own bins gives run()'s sigmas and weights bit for
+    bit, so it carries run()'s pin to the reference goldens (above)."""
+    fx = np.load(os.path.join(GOLDEN, name + ".npz"))
+    spec = _spec_from(fx)
+    params = synth.make_params(spec, seed=int(fx["seed"]), emb_scale=float(fx["emb_scale"]),
+                               ln_jitter=float(fx["ln_jitter"]))
+    ro, rd = orc.get_rays(fx["pose"], fx["intrinsics"], int(fx["H"]), int(fx["W"]))
+    model = orc.OracleNeRF(spec, params)
+    keep = {}
+    model.run(ro, rd, return_feats=1, keep=keep)
+    for st in range(3):
+        sig, ds, rb, u01 = model.stage_sigmas(ro, rd, keep[f"bins{st}"], st)
+        assert torch.equal(sig, keep[f"sigmas{st}"]), st
+        assert torch.equal(orc.composite_weights(rb, sig), keep[f"weights{st}"]), st
+        assert torch.equal(orc.composite_from_ds(ds), keep[f"weights{st}"]), st
+        assert u01.shape == (ro.shape[0], sig.shape[1], 3) and bool(((u01 >= 0) & (u01 <= 1)).all())
+
+
 def test_oracle_steps_match_reference_golden():
     u = np.load(os.path.join(GOLDEN, "units.npz"))
     ro, rd = orc.get_rays(u["rays_pose"], u["rays_intr"], 16, 24)

@@ -31,23 +31,26 @@ def main():
     filt = sys.argv[2] if len(sys.argv) > 2 else ""
     kernels = collections.OrderedDict()
     meta = collections.defaultdict(dict)
-    cur = None
+    cur = last = None
     for line in open(path):
+        t = line.strip()
+        if last is not None and t.startswith(";"):
+            # the register / occupancy comments follow the kernel's .Lfunc_end
+            mm = re.match(r";\s*(NumVgprs|NumAgprs|TotalNumVgprs|ScratchSize|Occupancy|LDSByteSize|NumSgprs):\s*(\S+)", t)
+            if mm:
+                meta[last][mm.group(1)] = mm.group(2)
         m = re.match(r"^(_Z\S+):\s*(;.*)?$", line)
         if m and not line.startswith("\t"):
             cur = m.group(1)
+            last = None
             kernels[cur] = collections.Counter()
             continue
         if cur is None:
             continue
         if line.startswith(".Lfunc_end"):
-            cur = None
+            last, cur = cur, None
             continue
-        t = line.strip()
         if t.startswith(";"):
-            mm = re.match(r";\s*(NumVgprs|NumAgprs|TotalNumVgprs|ScratchSize|Occupancy|LDSByteSize|NumSgprs):\s*(\S+)", t)
-            if mm:
-                meta[cur][mm.group(1)] = mm.group(2)
             continue
         if not t or t.startswith(".") or t.endswith(":"):
             continue
