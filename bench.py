@@ -560,7 +560,11 @@ class ViewRunner:
         self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                            for _ in range(n_streams - 1)]
         self.n_step = 0
-        self.pipe = (ShardedViewPipeline(renderer.render, H, W, codec=codec)
+        # fp32 transport: each rank renders its band straight into its slice of
+        # the gather buffer (samnerf_render_forward_tile), no pack copy
+        keys = ("image", "depth", "weights_sum") + (() if args.no_sam else ("samvit",))
+        tile_cols = (5 if args.no_sam else 261) if codec == "fp32" else None
+        self.pipe = (ShardedViewPipeline(renderer.render, H, W, keys=keys, codec=codec, tile_cols=tile_cols)
                      if world > 1 and args.chunks == 0 else None)
 
     def _step_on_stream(self, raws=None):
@@ -573,10 +577,10 @@ class ViewRunner:
         def ray_fn(row0, rows):
             return ops.get_rays(self.pose, self.intr, H, W, device=dev, row0=row0, rows=rows)
 
-        def render_fn(ro, rd):
+        def render_fn(ro, rd, out_tile=None):
             raw = next(it, None)
             lib().samnerf_set_stage_events(raw, 6 if raw is not None else 0)
-            return self.renderer.render(ro, rd, view_width=W if self.args.tiles else 0)
+            return self.renderer.render(ro, rd, view_width=W if self.args.tiles else 0, out_tile=out_tile)
 
         if self.world > 1 and self.args.chunks > 0:
             return render_view_sharded(render_fn, ray_fn, H, W, chunks=self.chunks)

@@ -63,30 +63,49 @@ __device__ __forceinline__ float exp2i(int k) {
     return __builtin_bit_cast(float, (uint32_t)(k + 127) << 23);
 }
 
-// hi / lo halves of x * s and y * s (s a power of two, so x * s is exact),
-// packed as two f16 each: hi = f16(x s), lo = f16(x s - hi), each one
+// hi / lo halves of 8 values times s (s a power of two, so x * s is exact),
+// packed as two f16 per dword: hi = f16(x s), lo = f16(x s - hi), each one
 // v_fma_mix (fp32 fma of f32 / f16 sources rounded once to f16): 4
 // instructions per pair where multiply, convert, convert back, subtract and
 // convert took 6.  The same bits as that sequence (x s and x s - hi are exact
 // in fp32, so both round the same value once).
-__device__ __forceinline__ void split_pair_f16(float x, float y, float s, uint32_t& hi, uint32_t& lo) {
-    uint32_t h, l;
-    asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
-        "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
-        "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-        : "=&v"(h), "=&v"(l)
-        : "v"(x), "v"(y), "v"(s));
-    hi = h;
-    lo = l;
-}
-
-// 8 values (times the scale s) -> one B (or A) fragment pair
+//
+// Wait states (nothing inside an asm string is padded by hipcc): a
+// v_fma_mixhi_f16 writes the HIGH half of its destination (op_sel dst), and a
+// VALU that reads a VGPR right after such a partial write needs one wait state
+// (gfx950's dst-sel forwarding hazard) -- so all four hi dwords are written
+// first and each is read by the lo half 4+ instructions later; the string ends
+// with s_nop 1 because its outputs feed MFMA A/B operands, which need two wait
+// states after a VALU write (the guide's VALU -> MFMA operand rule).  The round-1
+// to round-3 form (hi, then lo, of each pair back to back) read the hi dword
+// one instruction after its partial write: on a busy SIMD another wave's
+// instruction usually sat between them, so the outputs were right on most
+// launches and wrong on a few (the k_final prefetch variants'
+// "nondeterminism").
 __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
-    split_pair_f16(v[0], v[1], s, hi.x, lo.x);
-    split_pair_f16(v[2], v[3], s, hi.y, lo.y);
-    split_pair_f16(v[4], v[5], s, hi.z, lo.z);
-    split_pair_f16(v[6], v[7], s, hi.w, lo.w);
+    uint32_t h0, h1, h2, h3, l0, l1, l2, l3;
+    asm("v_fma_mixlo_f16 %0, %8, %16, 0\n\t"
+        "v_fma_mixhi_f16 %0, %9, %16, 0\n\t"
+        "v_fma_mixlo_f16 %1, %10, %16, 0\n\t"
+        "v_fma_mixhi_f16 %1, %11, %16, 0\n\t"
+        "v_fma_mixlo_f16 %2, %12, %16, 0\n\t"
+        "v_fma_mixhi_f16 %2, %13, %16, 0\n\t"
+        "v_fma_mixlo_f16 %3, %14, %16, 0\n\t"
+        "v_fma_mixhi_f16 %3, %15, %16, 0\n\t"
+        "v_fma_mixlo_f16 %4, %8, %16, -%0 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %4, %9, %16, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %5, %10, %16, -%1 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %5, %11, %16, -%1 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %6, %12, %16, -%2 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %6, %13, %16, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %7, %14, %16, -%3 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %7, %15, %16, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "s_nop 1"
+        : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3)
+        : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
+          "v"(s));
+    hi = make_uint4(h0, h1, h2, h3);
+    lo = make_uint4(l0, l1, l2, l3);
 }
 
 // running max |a|, |b| into m (one v_max3_f32 with |.| source modifiers)

@@ -46,7 +46,7 @@ using namespace samnerf;
 
 namespace samnerf {
 int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, float* samvit,
-                     float* packed, hipStream_t s);
+                     float* packed, hipStream_t s, uint32_t ld = 256u);
 size_t sam_head_packed_floats();
 int mask_head_forward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
                       const float* geo_f, uint32_t N, float* out, RayTiles tiles, float* packed,
@@ -506,9 +506,10 @@ struct FinalArgs {
     const float* snf;       // [2][N]
     float* u_out;      // [T][3][N] grid-space sample positions
     float* w_out;      // [T][N] final weights
-    float* image;      // [N,3]
-    float* depth;      // [N]
-    float* wsum;       // [N]
+    float* image;      // [N,3], row stride img_ld
+    float* depth;      // [N], stride scal_ld
+    float* wsum;       // [N], stride scal_ld
+    uint32_t img_ld, scal_ld;   // 3 / 1, or the gather tile's row (samnerf_render_forward_tile)
     float* rows;       // [N, kRow] or null
     RayTiles tiles;    // slot -> ray: rays_o / rays_d and the per-ray outputs are in ray order
     // N1 (flagged, non-parity; samnerf_model.t_thresh): optical depth
@@ -1414,10 +1415,10 @@ k_final(FinalArgs a) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {                // rows 0..2 of v3 = registers 0..2, lower half
         img[c] = sigmoidf(SA ? rgb[c] : v3[c]) + (1.0f - ws) * a.bg;
-        a.image[(size_t)ray * 3 + c] = img[c];
+        a.image[(size_t)ray * a.img_ld + c] = img[c];
     }
-    a.depth[ray] = dp;
-    a.wsum[ray] = ws;
+    a.depth[(size_t)ray * a.scal_ld] = dp;
+    a.wsum[(size_t)ray * a.scal_ld] = ws;
     if (row) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) row[143 + i] = sh[i] * ws;
@@ -2393,17 +2394,27 @@ size_t samnerf_render_workspace_size(const samnerf_model* model, uint32_t N) {
     return carve(model, N, nullptr).bytes;
 }
 
-int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const float* rays_d,
-                           uint32_t N, const float* cam_near_far, uint32_t n_cnf, float bg_color,
-                           float* image, float* depth, float* weights_sum, float* samvit,
-                           float* feature_rows, void* workspace, size_t workspace_bytes,
-                           samnerf_stream_t stream) {
-    // N = 0 is a no-op whatever the buffers (an empty torch tensor has a null
-    // data pointer)
-    if (!m) return fail(SAMNERF_EINVAL, "render: null pointer");
-    if (N == 0) return SAMNERF_OK;
-    if (!rays_o || !rays_d || !image || !depth || !weights_sum)
-        return fail(SAMNERF_EINVAL, "render: null pointer");
+}  // extern "C"
+
+namespace {
+
+// Where the per-ray outputs go: separate arrays (samnerf_render_forward) or
+// the rows of one gather tile (samnerf_render_forward_tile).
+struct OutLayout {
+    float* image;
+    float* depth;
+    float* wsum;
+    float* samvit;
+    uint32_t img_ld, scal_ld, sv_ld;
+};
+
+int render_impl(const samnerf_model* m, const float* rays_o, const float* rays_d, uint32_t N,
+                const float* cam_near_far, uint32_t n_cnf, float bg_color, const OutLayout& ol,
+                float* feature_rows, void* workspace, size_t workspace_bytes, samnerf_stream_t stream) {
+    float* const image = ol.image;
+    float* const depth = ol.depth;
+    float* const weights_sum = ol.wsum;
+    float* const samvit = ol.samvit;
     if (m->num_steps[0] != 128 || m->num_steps[1] != 64 || m->num_steps[2] != 32)
         return fail(SAMNERF_EINVAL, "render: fused path is built for num_steps = [128, 64, 32]");
     // with_sam and samvit == NULL: the caller does not want the features
@@ -2535,6 +2546,8 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     fa.image = image;
     fa.depth = depth;
     fa.wsum = weights_sum;
+    fa.img_ld = ol.img_ld;
+    fa.scal_ld = ol.scal_ld;
     if (!(m->t_thresh >= 0.0f && m->t_thresh < 1.0f))
         return fail(SAMNERF_EINVAL, "render_forward: t_thresh %g outside [0, 1)", (double)m->t_thresh);
     fa.exit_depth = m->t_thresh > 0.0f ? -logf(m->t_thresh) : INFINITY;
@@ -2628,7 +2641,7 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
         }
         if ((rc = check_launch("render"))) return rc;
         mark_stage(4, s);
-        if (samvit) rc = sam_head_forward(m, rows, N, samvit, w.packed, s);
+        if (samvit) rc = sam_head_forward(m, rows, N, samvit, w.packed, s, ol.sv_ld);
         mark_stage(5, s);
         if (rc == SAMNERF_OK) rc = copy_final_taps(tp, w, N, s);
         return rc;
@@ -2638,6 +2651,42 @@ int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const fl
     mark_stage(5, s);
     if ((rc = check_launch("render"))) return rc;
     return copy_final_taps(tp, w, N, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int samnerf_render_forward(const samnerf_model* m, const float* rays_o, const float* rays_d,
+                           uint32_t N, const float* cam_near_far, uint32_t n_cnf, float bg_color,
+                           float* image, float* depth, float* weights_sum, float* samvit,
+                           float* feature_rows, void* workspace, size_t workspace_bytes,
+                           samnerf_stream_t stream) {
+    // N = 0 is a no-op whatever the buffers (an empty torch tensor has a null
+    // data pointer)
+    if (!m) return fail(SAMNERF_EINVAL, "render: null pointer");
+    if (N == 0) return SAMNERF_OK;
+    if (!rays_o || !rays_d || !image || !depth || !weights_sum)
+        return fail(SAMNERF_EINVAL, "render: null pointer");
+    const OutLayout ol{image, depth, weights_sum, samvit, 3u, 1u, 256u};
+    return render_impl(m, rays_o, rays_d, N, cam_near_far, n_cnf, bg_color, ol, feature_rows, workspace,
+                       workspace_bytes, stream);
+}
+
+int samnerf_render_forward_tile(const samnerf_model* m, const float* rays_o, const float* rays_d,
+                                uint32_t N, const float* cam_near_far, uint32_t n_cnf, float bg_color,
+                                float* tile, uint32_t ld, int feats, float* feature_rows, void* workspace,
+                                size_t workspace_bytes, samnerf_stream_t stream) {
+    if (!m) return fail(SAMNERF_EINVAL, "render_tile: null pointer");
+    if (N == 0) return SAMNERF_OK;
+    if (!rays_o || !rays_d || !tile) return fail(SAMNERF_EINVAL, "render_tile: null pointer");
+    const bool sv = feats && m->with_sam;
+    if (ld < (sv ? 261u : 5u))
+        return fail(SAMNERF_EINVAL, "render_tile: row of %u floats cannot hold the outputs (needs %u)", ld,
+                    sv ? 261u : 5u);
+    const OutLayout ol{tile, tile + 3, tile + 4, sv ? tile + 5 : nullptr, ld, ld, ld};
+    return render_impl(m, rays_o, rays_d, N, cam_near_far, n_cnf, bg_color, ol, feature_rows, workspace,
+                       workspace_bytes, stream);
 }
 
 int samnerf_set_stage_events(void* const* events, uint32_t n) {

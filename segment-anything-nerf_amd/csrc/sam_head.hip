@@ -149,8 +149,24 @@ struct HeadArgs {
     const float* b[5];
     const float* ln_w;
     const float* ln_b;
-    float* out;            // [N, 256]
+    float* out;            // [N, 256], row stride ld
+    uint32_t ld;           // 256, or the gather tile's row (samnerf_render_forward_tile)
+    bool vec_out;          // rows 16-B aligned: float4 stores
 };
+
+// samvit output store of 4 consecutive features: one 16-B store when the rows
+// are 16-B aligned (the [N, 256] output), four 4-B stores inside a gather tile
+// whose rows are not (kernel-uniform branch)
+__device__ __forceinline__ void store_out4(float* p, const float4& y, bool vec) {
+    if (vec) {
+        *reinterpret_cast<float4*>(p) = y;
+    } else {
+        p[0] = y.x;
+        p[1] = y.y;
+        p[2] = y.z;
+        p[3] = y.w;
+    }
+}
 
 __global__ void __launch_bounds__(256) k_sam_head(HeadArgs a) {
     __shared__ float X[kRows * kXStride];
@@ -193,14 +209,14 @@ __global__ void __launch_bounds__(256) k_sam_head(HeadArgs a) {
     const float mf = (float)mean;
     const uint32_t ray = ray0 + row;
     if (ray < a.N) {
-        float* o = a.out + (size_t)ray * 256 + q * 32;
+        float* o = a.out + (size_t)ray * a.ld + q * 32;
         for (int c = 0; c < 32; c += 4) {
             float4 y;
             y.x = ((hr[c + 0] - mf) * rstd) * a.ln_w[q * 32 + c + 0] + a.ln_b[q * 32 + c + 0];
             y.y = ((hr[c + 1] - mf) * rstd) * a.ln_w[q * 32 + c + 1] + a.ln_b[q * 32 + c + 1];
             y.z = ((hr[c + 2] - mf) * rstd) * a.ln_w[q * 32 + c + 2] + a.ln_b[q * 32 + c + 2];
             y.w = ((hr[c + 3] - mf) * rstd) * a.ln_w[q * 32 + c + 3] + a.ln_b[q * 32 + c + 3];
-            *reinterpret_cast<float4*>(o + c) = y;
+            store_out4(o + c, y, a.vec_out);
         }
     }
 }
@@ -328,7 +344,9 @@ struct HeadArgsH {
     const float* b[5];
     const float* ln_w;
     const float* ln_b;
-    float* out;
+    float* out;            // [N, 256], row stride ld
+    uint32_t ld;
+    bool vec_out;
     unsigned long long* stamps;   // diagnostic form 13 only: [block][wave][16] s_memtime marks
 };
 
@@ -670,7 +688,7 @@ k_sam_head_h16(HeadArgsH a) {
             for (int i = 0; i < 16; ++i) a.stamps[((size_t)blockIdx.x * 4 + wave) * 16 + i] = ts[i];
     }
     if (!live) return;
-    float* o = a.out + (size_t)ray * 256;
+    float* o = a.out + (size_t)ray * a.ld;
     const float* lw = Bs + 5 * 256;
     const float* lb = Bs + 6 * 256;
 #pragma unroll
@@ -683,7 +701,7 @@ k_sam_head_h16(HeadArgsH a) {
             y.y = ((acc[t][4 * mm + 1] - mf) * rstd) * lw[u + 1] + lb[u + 1];
             y.z = ((acc[t][4 * mm + 2] - mf) * rstd) * lw[u + 2] + lb[u + 2];
             y.w = ((acc[t][4 * mm + 3] - mf) * rstd) * lw[u + 3] + lb[u + 3];
-            *reinterpret_cast<float4*>(o + u) = y;
+            store_out4(o + u, y, a.vec_out);
         }
 }
 
@@ -930,7 +948,7 @@ k_sam_head_h16q(HeadArgsH a, uint32_t ntiles) {
         const float rstd = (float)(1.0 / sqrt(var / 256.0 + 1e-5));
         const float mf = (float)mean;
         if (live) {
-            float* o = a.out + (size_t)ray * 256;
+            float* o = a.out + (size_t)ray * a.ld;
             const float* lw = Bs + 5 * 256;
             const float* lb = Bs + 6 * 256;
 #pragma unroll
@@ -943,7 +961,7 @@ k_sam_head_h16q(HeadArgsH a, uint32_t ntiles) {
                     y.y = ((acc[t][4 * mm + 1] - mf) * rstd) * lw[u + 1] + lb[u + 1];
                     y.z = ((acc[t][4 * mm + 2] - mf) * rstd) * lw[u + 2] + lb[u + 2];
                     y.w = ((acc[t][4 * mm + 3] - mf) * rstd) * lw[u + 3] + lb[u + 3];
-                    *reinterpret_cast<float4*>(o + u) = y;
+                    store_out4(o + u, y, a.vec_out);
                 }
         }
         st.rot = (st.rot + kSteps) % NBUF;
@@ -1218,7 +1236,7 @@ k_sam_head_h16p(HeadArgsH a) {
     const float rstd = (float)(1.0 / sqrt(var / 256.0 + 1e-5));
     const float mf = (float)mean;
     if (!live) return;
-    float* o = a.out + (size_t)ray * 256;
+    float* o = a.out + (size_t)ray * a.ld;
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
@@ -1232,7 +1250,7 @@ k_sam_head_h16p(HeadArgsH a) {
             y.y = ((v.y - mf) * rstd) * lw.y + lb.y;
             y.z = ((v.z - mf) * rstd) * lw.z + lb.z;
             y.w = ((v.w - mf) * rstd) * lw.w + lb.w;
-            *reinterpret_cast<float4*>(o + u) = y;
+            store_out4(o + u, y, a.vec_out);
         }
 }
 
@@ -1260,7 +1278,8 @@ size_t sam_head_packed_floats() {
 }
 
 int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, float* samvit,
-                     float* packed, hipStream_t s) {
+                     float* packed, hipStream_t s, uint32_t ld) {
+    const bool vec = ld % 4u == 0u && reinterpret_cast<uintptr_t>(samvit) % 16u == 0u;
     if (m->head_mode == 0) {                                     // f16x3 (default)
         PackArgs p;
         for (int i = 0; i < 5; ++i) p.W[i] = m->sam_w[i];
@@ -1278,6 +1297,8 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         a.ln_w = m->ln_w;
         a.ln_b = m->ln_b;
         a.out = samvit;
+        a.ld = ld;
+        a.vec_out = vec;
         a.stamps = nullptr;
         const uint32_t blocks = div_up(N, (uint32_t)kRaysV5);
 #ifdef SAMNERF_DIAG_VARIANTS
@@ -1328,6 +1349,8 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
     a.ln_w = m->ln_w;
     a.ln_b = m->ln_b;
     a.out = samvit;
+    a.ld = ld;
+    a.vec_out = vec;
     k_sam_head<<<div_up(N, kRows), 256, 0, s>>>(a);
     return check_launch("sam_head");
 }
@@ -1355,7 +1378,7 @@ int samnerf_sam_head_forward(const samnerf_model* m, const float* rows, uint32_t
         return fail(SAMNERF_EWORKSPACE, "sam_head_forward: workspace needs %zu bytes, got %zu", need,
                     workspace_bytes);
     return sam_head_forward(m, rows, N, samvit, static_cast<float*>(workspace),
-                            reinterpret_cast<hipStream_t>(stream));
+                            reinterpret_cast<hipStream_t>(stream), 256u);
 }
 
 }  // extern "C"

@@ -67,6 +67,8 @@ _SIGS = {
     "samnerf_render_workspace_size": ([ctypes.POINTER(SamnerfModel), _u32], _sz),
     "samnerf_render_forward": ([ctypes.POINTER(SamnerfModel), _vp, _vp, _u32, _vp, _u32, _f32,
                                 _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp], _int),
+    "samnerf_render_forward_tile": ([ctypes.POINTER(SamnerfModel), _vp, _vp, _u32, _vp, _u32, _f32,
+                                     _vp, _u32, _int, _vp, _vp, _sz, _vp], _int),
     "samnerf_sgrid_backward": ([ctypes.POINTER(SamnerfModel), _vp, _u32, _vp, _vp, _sz, _vp],
                                _int),
     "samnerf_mask_forward": ([ctypes.POINTER(SamnerfModel), _u32, _vp, _vp, _sz, _vp], _int),

@@ -24,6 +24,10 @@ def shard_range(n, rank, world):
     return start, start + base + (1 if rank < extra else 0)
 
 
+KEYS_ALL = ("image", "depth", "weights_sum", "samvit")
+KEY_WIDTHS = (3, 1, 1, 256)
+
+
 def pack_outputs(out, keys):
     return torch.cat([out[k].reshape(out[k].shape[0], -1).float() for k in keys], dim=1)
 
@@ -159,11 +163,22 @@ class ShardedViewPipeline:
     quantisation.  q16 needs CUDA outputs with samvit (there is no CPU codec)."""
 
     def __init__(self, render_fn, H, W, keys=("image", "depth", "weights_sum", "samvit"),
-                 group=None, depth=1, codec="fp32"):
+                 group=None, depth=1, codec="fp32", tile_cols=None):
+        """tile_cols (fp32 transport): render_fn accepts out_tile= (as
+        FusedRenderer.render) and writes a band's outputs as rows of this many
+        columns (261 with samvit, 5 without; samnerf_render_forward_tile's
+        layout = `keys` in order) -- straight into this rank's slice of the
+        gather buffer, which the all-gather then fills in place: no pack copy
+        of the band before the collective.  None: render into separate
+        tensors and pack them (any render_fn)."""
         if codec not in ("fp32", "q16"):
             raise ValueError(f"codec must be 'fp32' or 'q16', got {codec!r}")
+        if tile_cols is not None and (codec != "fp32" or tuple(keys) != KEYS_ALL[:len(keys)]
+                                      or tile_cols != sum(KEY_WIDTHS[:len(keys)])):
+            raise ValueError("tile_cols: fp32 transport of (image, depth, weights_sum[, samvit]) only")
         self.render_fn, self.H, self.W = render_fn, H, W
         self.keys, self.group, self.depth, self.codec = keys, group, depth, codec
+        self.tile_cols = tile_cols
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         if H % self.world:
@@ -174,6 +189,16 @@ class ShardedViewPipeline:
 
     def submit(self, ray_fn, render_fn=None):
         ro, rd = ray_fn(self.rank * self.band, self.band)
+        if self.tile_cols is not None:
+            n = ro.shape[0]
+            buf = torch.empty(self.world * n, self.tile_cols, device=ro.device)
+            own = buf[self.rank * n:(self.rank + 1) * n]
+            out = (render_fn or self.render_fn)(ro, rd, out_tile=own)
+            keys = list(self.keys)
+            widths = list(KEY_WIDTHS[:len(keys)])
+            work = _all_gather(buf, own, self.group, async_op=True)   # in place
+            self.inflight.append((work, buf, own, keys, widths, out))
+            return
         out = (render_fn or self.render_fn)(ro, rd)
         keys = [k for k in self.keys if k in out]
         widths = [out[k].reshape(out[k].shape[0], -1).shape[1] for k in keys]

@@ -194,7 +194,7 @@ class FusedRenderer:
     @torch.no_grad()
     def render(self, rays_o, rays_d, cam_near_far=None, bg_color=None, rows=None,
                keep_workspace=False, feats=True, taps=False, own_workspace=False, view_width=0,
-               mask=False, perturb=False, mask_logits=True):
+               mask=False, perturb=False, mask_logits=True, out_tile=None):
         """rays_o, rays_d [N,3] (CUDA fp32) -> dict(image [N,3], depth [N],
         weights_sum [N], samvit [N,256] if with_sam and feats).  `rows`
         (optional [N,164] tensor) receives the head input cat(f_sam, f_image,
@@ -220,6 +220,11 @@ class FusedRenderer:
         (samnerf_mask_forward on the render's workspace); with
         mask_logits=False the samples' geo_feat are stored for a later
         samnerf_mask_train_forward and no logits are computed.
+        out_tile: a contiguous fp32 CUDA tensor [N, C] (C >= 261 with SAM
+        features, >= 5 without): the outputs are written into its rows --
+        columns 0-2 image, 3 depth, 4 weights_sum, 5-260 samvit
+        (samnerf_render_forward_tile; the all-gather record of a sharded view)
+        -- and returned as views of it.
         perturb: False (default), True (draw the perturbed sample positions
         with torch's generator, perturbed_positions -- the reference's
         perturb=True), or a (bins0, u1, u2) tuple of them [N, 129], [N, 65],
@@ -259,10 +264,22 @@ class FusedRenderer:
             bg = float(bg_color)
         else:
             bg = float(bg_color)
-        image = torch.empty(N, 3, device=dev)
-        depth = torch.empty(N, device=dev)
-        wsum = torch.empty(N, device=dev)
-        samvit = torch.empty(N, 256, device=dev) if (m.with_sam and feats) else None
+        if out_tile is not None:
+            need_c = 261 if (m.with_sam and feats) else 5
+            if (out_tile.dim() != 2 or out_tile.shape[0] != N or out_tile.shape[1] < need_c
+                    or out_tile.dtype != torch.float32 or not out_tile.is_contiguous()
+                    or out_tile.device != dev):
+                raise ValueError(f"fused render: out_tile must be a contiguous fp32 [{N}, >={need_c}] "
+                                 f"tensor on {dev}")
+            if mask:
+                raise NotImplementedError("fused render: out_tile with mask outputs")
+            image, depth, wsum = out_tile[:, 0:3], out_tile[:, 3], out_tile[:, 4]
+            samvit = out_tile[:, 5:261] if need_c == 261 else None
+        else:
+            image = torch.empty(N, 3, device=dev)
+            depth = torch.empty(N, device=dev)
+            wsum = torch.empty(N, device=dev)
+            samvit = torch.empty(N, 256, device=dev) if (m.with_sam and feats) else None
         cnf = None
         n_cnf = 0
         if cam_near_far is not None:
@@ -289,10 +306,16 @@ class FusedRenderer:
                              rows_tap["rows2"].data_ptr(), rows_tap["srows"].data_ptr())
             check(lib().samnerf_set_taps(ctypes.byref(st), N), "set_taps")
         try:
-            check(lib().samnerf_render_forward(
-                ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, _ptr(cnf), n_cnf, bg, _ptr(image),
-                _ptr(depth), _ptr(wsum), _ptr(samvit), _ptr(rows), _ptr(ws), need, _stream(rays_o)),
-                "render_forward")
+            if out_tile is not None:
+                check(lib().samnerf_render_forward_tile(
+                    ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, _ptr(cnf), n_cnf, bg, _ptr(out_tile),
+                    out_tile.shape[1], int(samvit is not None), _ptr(rows), _ptr(ws), need, _stream(rays_o)),
+                    "render_forward_tile")
+            else:
+                check(lib().samnerf_render_forward(
+                    ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, _ptr(cnf), n_cnf, bg, _ptr(image),
+                    _ptr(depth), _ptr(wsum), _ptr(samvit), _ptr(rows), _ptr(ws), need, _stream(rays_o)),
+                    "render_forward")
             if mask and mask_logits:
                 logits = torch.empty(N, int(m.mask_out), device=dev)
                 check(lib().samnerf_mask_forward(ctypes.byref(m), N, _ptr(logits), _ptr(ws), need,

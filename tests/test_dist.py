@@ -15,6 +15,20 @@ def _fake_render(o, d):
             "samvit": torch.cat([o, d], -1).repeat(1, 43)[:, :256]}
 
 
+def _fake_render_tile(o, d, out_tile=None):
+    # the out_tile form (FusedRenderer.render(out_tile=...), the layout of
+    # samnerf_render_forward_tile): outputs written into the caller's rows
+    r = _fake_render(o, d)
+    if out_tile is None:
+        return r
+    out_tile[:, 0:3] = r["image"]
+    out_tile[:, 3] = r["depth"]
+    out_tile[:, 4] = r["weights_sum"]
+    out_tile[:, 5:261] = r["samvit"]
+    return {"image": out_tile[:, 0:3], "depth": out_tile[:, 3], "weights_sum": out_tile[:, 4],
+            "samvit": out_tile[:, 5:261]}
+
+
 def _worker(rank, world, port, n, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -56,6 +70,18 @@ def _worker(rank, world, port, n, q):
         ok = ok and len(got) == 3
         for v, g in enumerate(got):
             refv = _fake_render(o[:H * W] + v, d[:H * W])
+            ok = ok and all(torch.equal(g[k], refv[k]) for k in refv)
+        # the same pipeline rendering into its slice of the gather buffer
+        # (tile_cols): the band is never packed, the gather fills the buffer in place
+        pipe = ShardedViewPipeline(_fake_render_tile, H, W, tile_cols=261)
+        for v in range(3):
+            def ray_fn_t(row0, rows, v=v):
+                return (o[row0 * W:(row0 + rows) * W] - v, d[row0 * W:(row0 + rows) * W])
+            pipe.submit(ray_fn_t)
+        got = pipe.flush()
+        ok = ok and len(got) == 3
+        for v, g in enumerate(got):
+            refv = _fake_render(o[:H * W] - v, d[:H * W])
             ok = ok and all(torch.equal(g[k], refv[k]) for k in refv)
         q.put((rank, ok, {k: tuple(v.shape) for k, v in out.items()}))
     finally:
