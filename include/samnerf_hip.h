@@ -287,8 +287,17 @@ int samnerf_mask_forward(const samnerf_model* model, uint32_t N, float* instance
  * grad_m_grid (the m_grid embedding gradient, accumulated into: the
  * reference encoder's backward).  weights and geo_feat carry no gradient
  * (.detach() in the reference), the sample positions none (no parameter).
- * Replaces the reference's per-chunk torch ops and autograd of that branch. */
-/* The workspace keeps the head's fp32 activations of all 32 samples of every
+ * Replaces the reference's per-chunk torch ops and autograd of that branch.
+ * 'adaptive' heads (mask_kind 1 'density', network.py:167-180, the reference's
+ * scripts/train_mask.sh:16,20,21 configuration; 2 'rgb' with sum_after_mlp,
+ * network.py:148-160): the render leaves each ray's weighted sums of the
+ * head's (detached) inputs in `render_ws`; forward runs the bias-free Linear
+ * chain on them (the head is linear: the logits of the per-sample chain and
+ * weighted sum, to rounding), backward writes the gradients of every
+ * mask_w[i] ([96,32] .. [mask_out,96], overwritten, fixed-order sums) -- the
+ * only tensors the reference's loss reaches; grad_m_grid is unused (may be
+ * NULL).  Workspace (same size function): 2 x 7 x 96 floats per ray. */
+/* The 'default' head's workspace keeps its fp32 activations of all 32 samples of every
  * ray for the backward -- input (144), both hidden layers and their
  * gradients (4 x 256) and the logits and their gradient (2 x 32): about 157 KB
  * per ray, 0.64 GB at the reference's 4,096-ray batch (and the render's own

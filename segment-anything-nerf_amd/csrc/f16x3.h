@@ -82,6 +82,25 @@ __device__ __forceinline__ float exp2i(int k) {
 // instruction usually sat between them, so the outputs were right on most
 // launches and wrong on a few (the k_final prefetch variants'
 // "nondeterminism").
+#ifdef SAMNERF_AB_OLDSPLIT   // timing A/B only: the round-3 form (hazard-exposed)
+__device__ __forceinline__ void split_pair_f16_old(float x, float y, float s, uint32_t& hi, uint32_t& lo) {
+    uint32_t h, l;
+    asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+        "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+        "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(h), "=&v"(l)
+        : "v"(x), "v"(y), "v"(s));
+    hi = h;
+    lo = l;
+}
+__device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
+    split_pair_f16_old(v[0], v[1], s, hi.x, lo.x);
+    split_pair_f16_old(v[2], v[3], s, hi.y, lo.y);
+    split_pair_f16_old(v[4], v[5], s, hi.z, lo.z);
+    split_pair_f16_old(v[6], v[7], s, hi.w, lo.w);
+}
+#else
 __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
     uint32_t h0, h1, h2, h3, l0, l1, l2, l3;
     asm("v_fma_mixlo_f16 %0, %8, %16, 0\n\t"
@@ -107,6 +126,7 @@ __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, u
     hi = make_uint4(h0, h1, h2, h3);
     lo = make_uint4(l0, l1, l2, l3);
 }
+#endif
 
 // running max |a|, |b| into m (one v_max3_f32 with |.| source modifiers)
 __device__ __forceinline__ float max_abs3(float m, float a, float b) {

@@ -418,11 +418,259 @@ int mask_weights(const samnerf_model* m, MaskW& mw) {
     return SAMNERF_OK;
 }
 
+// ------------------------------------------------- adaptive heads (kinds 1-2)
+// 'adaptive' / 'density' (network.py:167-180, renderer.py:424-436; the
+// reference's own scripts/train_mask.sh:16,20,21) and 'adaptive' / 'rgb'
+// (network.py:148-160, renderer.py:400-413): bias-free Linear layers on
+// concatenations [intermediate ; m] with no activation,
+//     m0 = W0 g,  m_i = W_i [x_i ; m_{i-1}],  logits = W_last m_{last-1},
+// where g = grid_output.detach() and the x_i are grid_mlp's (and, for 'rgb',
+// the per-sample view_mlp's) saved intermediates, all detached
+// (network.py:28-33).  Linear in the per-sample inputs, so with
+// X = sum_k weights_k.detach() x_k (k_final<AD> writes X per ray, in the
+// column order of the effective matrix: g 32 | h1 64 | h2 64 | o3 16 | v1 32 |
+// v2 32) the ray's logits are the chain applied to X, and the gradient of
+// every W_i is sum over rays of g_i (x) in_i(X) with g_i the chain's backward
+// of dL/dlogits -- the same sums the reference's per-sample chain and
+// weighted sum produce, reassociated (rounding-level differences).  Only the
+// mask_mlp weights receive gradient (every input is detached).
+//   k_adt_fwd   16 rays per workgroup: the chain, m_0 .. m_{L-2} saved, logits;
+//   k_adt_bwd   16 rays per workgroup: g_{L-1} = dL/dlogits, g_{i-1} =
+//               W_i[:, m part]^T g_i, saved;
+//   k_adt_dw    dW_i = sum_r g_i[r] in_i[r]^T, one 32 x 32 output tile of one
+//               layer per workgroup over all rays in ray order (fixed order:
+//               bitwise reproducible, no atomics).
+// fp32 VALU fma chains (4,096 rays x ~60 K MACs: the render dominates).
+constexpr int kAdU = 96;                      // hidden width (network.py:147 mask_mlp_dim)
+constexpr int kAdX = 240;                     // X row (raymarch.hip kAeff)
+constexpr int kAdRays = 16;                   // rays per workgroup (fwd / bwd)
+constexpr int kAdMaxL = 8;
+
+struct AdLayer {
+    int xo, xw;          // the X part of the input: columns [xo, xo + xw) of X (0 width: none)
+    int mw;              // the m part (the previous layer's output): 96 or 0
+    int out;             // 96, or K for the last layer
+    const float* W;      // [out][xw + mw], torch layout: cat([x part, m part]) (renderer.py:402-433)
+};
+
+struct AdArgs {
+    AdLayer L[kAdMaxL];
+    int nl;
+    uint32_t N;
+    const float* X;      // [N][kAdX] (ray order)
+    float* m;            // [nl - 1][N][96] saved layer outputs
+    float* g;            // [nl - 1][N][96] their gradients (bwd)
+    const float* G;      // [N][K] dL/dlogits (bwd)
+    float* logits;       // [N][K] (fwd)
+};
+
+int ad_layers(const samnerf_model* m, AdLayer* L) {
+    const int K = (int)m->mask_out;
+    if (m->mask_kind == 1) {                    // density: g | h1 | h2 | o3, then two plain layers
+        const AdLayer t[6] = {{0, 32, 0, kAdU, m->mask_w[0]},   {32, 64, kAdU, kAdU, m->mask_w[1]},
+                              {96, 64, kAdU, kAdU, m->mask_w[2]}, {160, 16, kAdU, kAdU, m->mask_w[3]},
+                              {0, 0, kAdU, kAdU, m->mask_w[4]},   {0, 0, kAdU, K, m->mask_w[5]}};
+        for (int i = 0; i < 6; ++i) L[i] = t[i];
+        return 6;
+    }
+    const AdLayer t[8] = {{0, 32, 0, kAdU, m->mask_w[0]},    {32, 64, kAdU, kAdU, m->mask_w[1]},
+                          {96, 64, kAdU, kAdU, m->mask_w[2]},  {160, 16, kAdU, kAdU, m->mask_w[3]},
+                          {176, 32, kAdU, kAdU, m->mask_w[4]}, {208, 32, kAdU, kAdU, m->mask_w[5]},
+                          {0, 0, kAdU, kAdU, m->mask_w[6]},    {0, 0, kAdU, K, m->mask_w[7]}};
+    for (int i = 0; i < 8; ++i) L[i] = t[i];
+    return 8;
+}
+
+// 192 threads: unit u = t % 96 of rays (t / 96) * 8 .. + 7 of the block's 16
+__global__ void __launch_bounds__(192) k_adt_fwd(AdArgs a) {
+    __shared__ float Xs[kAdRays][kAdX];
+    __shared__ float Ms[2][kAdRays][kAdU];
+    const int t = threadIdx.x, u = t % kAdU, rh = t / kAdU;
+    const uint32_t r0 = blockIdx.x * kAdRays, N = a.N;
+    for (int e = t; e < kAdRays * kAdX; e += 192) {
+        const uint32_t r = r0 + e / kAdX;
+        Xs[e / kAdX][e % kAdX] = r < N ? a.X[(size_t)r * kAdX + e % kAdX] : 0.0f;
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int l = 0; l < a.nl; ++l) {
+        const AdLayer& L = a.L[l];
+        const int ld = L.xw + L.mw;
+        float acc[8] = {};
+        if (u < L.out) {
+            const float* w = L.W + (size_t)u * ld;
+            for (int k = 0; k < L.xw; ++k) {
+                const float wk = w[k];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) acc[i] = __builtin_fmaf(wk, Xs[rh * 8 + i][L.xo + k], acc[i]);
+            }
+            for (int k = 0; k < L.mw; ++k) {
+                const float wk = w[L.xw + k];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) acc[i] = __builtin_fmaf(wk, Ms[cur][rh * 8 + i][k], acc[i]);
+            }
+        }
+        const bool last = l == a.nl - 1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t r = r0 + rh * 8 + i;
+            if (u >= L.out || r >= N) continue;
+            if (last) a.logits[(size_t)r * L.out + u] = acc[i];
+            else {
+                Ms[cur ^ 1][rh * 8 + i][u] = acc[i];
+                a.m[((size_t)l * N + r) * kAdU + u] = acc[i];
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+}
+
+__global__ void __launch_bounds__(192) k_adt_bwd(AdArgs a) {
+    __shared__ float Gs[2][kAdRays][kAdU];
+    const int t = threadIdx.x, u = t % kAdU, rh = t / kAdU;
+    const uint32_t r0 = blockIdx.x * kAdRays, N = a.N;
+    const int K = a.L[a.nl - 1].out;
+    for (int e = t; e < kAdRays * K; e += 192) {
+        const uint32_t r = r0 + e / K;
+        Gs[0][e / K][e % K] = r < N ? a.G[(size_t)r * K + e % K] : 0.0f;
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int l = a.nl - 1; l >= 1; --l) {        // g_{l-1} = W_l[:, m part]^T g_l
+        const AdLayer& L = a.L[l];
+        const int ld = L.xw + L.mw;
+        float acc[8] = {};
+        for (int o = 0; o < L.out; ++o) {
+            const float wk = L.W[(size_t)o * ld + L.xw + u];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[i] = __builtin_fmaf(wk, Gs[cur][rh * 8 + i][o], acc[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t r = r0 + rh * 8 + i;
+            Gs[cur ^ 1][rh * 8 + i][u] = acc[i];
+            if (r < N) a.g[((size_t)(l - 1) * N + r) * kAdU + u] = acc[i];
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+}
+
+// dW_l[o][c] = sum_r g_l[r][o] in_l[r][c], in_l = [X part ; m_{l-1}]; one
+// 32 x 32 tile per workgroup (tile list from the host), 32-ray LDS tiles, a
+// 2 x 2 register tile per thread, rays summed in order
+struct AdTile {
+    int layer, o0, c0;
+};
+constexpr int kAdMaxTiles = 160;
+struct AdDwArgs {
+    AdArgs a;
+    float* dW[kAdMaxL];
+    AdTile tile[kAdMaxTiles];
+};
+
+__global__ void __launch_bounds__(256) k_adt_dw(AdDwArgs d) {
+    __shared__ float Gt[32][33], It[32][33];          // [ray][o], [ray][c]
+    const AdArgs& a = d.a;
+    const AdTile tl = d.tile[blockIdx.x];
+    const AdLayer& L = a.L[tl.layer];
+    const int ld = L.xw + L.mw, tid = threadIdx.x, ti = tid >> 4, tj = tid & 15;
+    const uint32_t N = a.N;
+    const bool lastl = tl.layer == a.nl - 1;
+    float acc[2][2] = {};
+    for (uint32_t rb = 0; rb < N; rb += 32) {
+        for (int e = tid; e < 32 * 32; e += 256) {
+            const int rr = e >> 5, j = e & 31;
+            const uint32_t r = rb + rr;
+            const int o = tl.o0 + j, c = tl.c0 + j;
+            float gv = 0.0f, iv = 0.0f;
+            if (r < N && o < L.out)
+                gv = lastl ? a.G[(size_t)r * L.out + o] : a.g[((size_t)tl.layer * N + r) * kAdU + o];
+            if (r < N && c < ld)
+                iv = c < L.xw ? a.X[(size_t)r * kAdX + L.xo + c]
+                              : a.m[((size_t)(tl.layer - 1) * N + r) * kAdU + (c - L.xw)];
+            Gt[rr][j] = gv;
+            It[rr][j] = iv;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int rr = 0; rr < 32; ++rr) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_fmaf(Gt[rr][ti * 2 + i], It[rr][tj * 2 + j], acc[i][j]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int o = tl.o0 + ti * 2 + i, c = tl.c0 + tj * 2 + j;
+            if (o < L.out && c < ld) d.dW[tl.layer][(size_t)o * ld + c] = acc[i][j];
+        }
+}
+
+size_t ad_ws_floats(uint32_t N) { return (size_t)2 * (kAdMaxL - 1) * N * kAdU; }
+
 }  // namespace
 
 namespace samnerf {
 
-size_t mask_train_workspace_bytes(uint32_t N) { return carve(N, nullptr).bytes; }
+size_t mask_train_workspace_bytes(uint32_t N) {
+    return std::max(carve(N, nullptr).bytes, ad_ws_floats(N) * sizeof(float));
+}
+
+// The adaptive heads (mask_kind 1 / 2): X [N][240] per-ray input sums from the
+// render (k_final<AD>, ray order)
+int adaptive_train_forward(const samnerf_model* m, const float* X, uint32_t N, float* logits, void* ws,
+                           size_t ws_bytes, hipStream_t s) {
+    if (ws_bytes < ad_ws_floats(N) * sizeof(float))
+        return fail(SAMNERF_EWORKSPACE, "mask_train_forward: workspace too small");
+    AdArgs a{};
+    a.nl = ad_layers(m, a.L);
+    for (int i = 0; i < a.nl; ++i)
+        if (!a.L[i].W) return fail(SAMNERF_EINVAL, "mask_train_forward: null mask_mlp weight %d", i);
+    a.N = N;
+    a.X = X;
+    a.m = static_cast<float*>(ws);
+    a.g = a.m + (size_t)(kAdMaxL - 1) * N * kAdU;
+    a.logits = logits;
+    k_adt_fwd<<<div_up(N, (uint32_t)kAdRays), 192, 0, s>>>(a);
+    return check_launch("mask_train_forward (adaptive)");
+}
+
+int adaptive_train_backward(const samnerf_model* m, const float* X, uint32_t N, const float* grad_logits,
+                            float* const* grad_w, void* ws, size_t ws_bytes, hipStream_t s) {
+    if (ws_bytes < ad_ws_floats(N) * sizeof(float))
+        return fail(SAMNERF_EWORKSPACE, "mask_train_backward: workspace too small");
+    AdDwArgs d{};
+    AdArgs& a = d.a;
+    a.nl = ad_layers(m, a.L);
+    a.N = N;
+    a.X = X;
+    a.m = static_cast<float*>(ws);
+    a.g = a.m + (size_t)(kAdMaxL - 1) * N * kAdU;
+    a.G = grad_logits;
+    for (int i = 0; i < a.nl; ++i) {
+        if (!grad_w[i]) return fail(SAMNERF_EINVAL, "mask_train_backward: null gradient %d", i);
+        d.dW[i] = grad_w[i];
+    }
+    k_adt_bwd<<<div_up(N, (uint32_t)kAdRays), 192, 0, s>>>(a);
+    int nt = 0;
+    for (int l = 0; l < a.nl; ++l) {
+        const int ld = a.L[l].xw + a.L[l].mw;
+        for (int o0 = 0; o0 < a.L[l].out; o0 += 32)
+            for (int c0 = 0; c0 < ld; c0 += 32) {
+                if (nt == kAdMaxTiles) return fail(SAMNERF_EINVAL, "mask_train_backward: tile table full");
+                d.tile[nt++] = AdTile{l, o0, c0};
+            }
+    }
+    k_adt_dw<<<nt, 256, 0, s>>>(d);
+    return check_launch("mask_train_backward (adaptive)");
+}
 
 // positions / weights / geo_feat of the render's final samples (sample-major,
 // slot order) and its ray order

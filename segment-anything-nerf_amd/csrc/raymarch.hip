@@ -59,6 +59,10 @@ int mask_train_forward(const samnerf_model* m, const GridDesc<16>& grid, const f
 int mask_train_backward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
                         const float* geo_f, uint32_t N, RayTiles tiles, const float* grad_logits,
                         float* const* grad_w, float* grad_m_grid, void* ws, size_t ws_bytes, hipStream_t s);
+int adaptive_train_forward(const samnerf_model* m, const float* X, uint32_t N, float* logits, void* ws,
+                           size_t ws_bytes, hipStream_t s);
+int adaptive_train_backward(const samnerf_model* m, const float* X, uint32_t N, const float* grad_logits,
+                            float* const* grad_w, void* ws, size_t ws_bytes, hipStream_t s);
 }  // namespace samnerf
 
 namespace {
@@ -521,6 +525,8 @@ struct FinalArgs {
     // features and MLP intermediates, so sum_k w_k head(x_k) = E . sum_k w_k x_k
     const float* aeff; // [K][240] E, blocks g 32 | h1 64 | h2 64 | o3 16 | v1 32 | v2 32 (k_mask_eff)
     float* mlog;       // [N][K] instance_mask_logits (ray order)
+    float* xsum;       // [N][kAeff] the per-ray sums sum_k w_k x_k in E's column order (ray
+                       // order), the adaptive head's input for its training (mask_head_train.hip)
     uint32_t mask_out;
     // N1 ray compaction (EXIT form): this pass marches samples [i0, i1) of
     // the slots in list_in (n_in of them, a device count; null: every slot);
@@ -1399,6 +1405,25 @@ k_final(FinalArgs a) {
             sacc += __shfl_xor(sacc, 32);
             if (live && hh == 0) a.mlog[(size_t)a.tiles(r) * K + c] = sacc;
         }
+        if (live) {                                      // this lane's components of X
+            float* X = a.xsum + (size_t)a.tiles(r) * kAeff;
+#pragma unroll
+            for (int m = 0; m < 16; ++m) X[2 * final_level(m >> 3, hh, (m & 7) >> 1) + (m & 1)] = gacc[m];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int u = rho(q) + 4 * hh;
+                X[32 + u] = h1acc[q];
+                X[64 + u] = h1acc[16 + q];
+                X[96 + u] = h2acc[q];
+                X[128 + u] = h2acc[16 + q];
+                if constexpr (AD == 2) {
+                    X[176 + u] = v1acc[q];
+                    X[208 + u] = v2acc[q];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) X[160 + rho(q) + 4 * hh] = fg[q];
+        }
     }
     if (!live || seg != 0 || cont) return;
     const uint32_t ray = a.tiles(r);                     // per-ray outputs in ray order
@@ -1937,6 +1962,7 @@ struct Workspace {
     float* mpacked;    // mask head weight stream (with_mask, kind 0)
     float* aeff;       // [K][240] adaptive heads' effective matrix (with_mask, kinds 1-2)
     float* mlog;       // [N][K] adaptive heads' logits (with_mask, kinds 1-2)
+    float* xsum;       // [N][kAeff] their per-ray input sums (with_mask, kinds 1-2; training)
     uint32_t* n1_list; // [2][N] N1 compaction: the passes' slot lists (t_thresh > 0)
     uint32_t* n1_cnt;  // [2] their lengths
     uint64_t* n1_mask; // [ceil(N / 32)] the waves' ballot masks of open rays
@@ -2216,6 +2242,7 @@ Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
     w.mpacked = take(mdef ? mask_head_packed_floats() : 0);
     w.aeff = take(madapt ? (size_t)32 * kAeff : 0);
     w.mlog = take(madapt ? (size_t)m->mask_out * n : 0);
+    w.xsum = take(madapt ? (size_t)kAeff * n : 0);
     const bool n1 = m->t_thresh > 0.0f;
     w.n1_list = reinterpret_cast<uint32_t*>(take(n1 ? 2 * n : 0));
     w.n1_cnt = reinterpret_cast<uint32_t*>(take(n1 ? 2 : 0));
@@ -2590,6 +2617,7 @@ int render_impl(const samnerf_model* m, const float* rays_o, const float* rays_d
             k_mask_eff<<<1, 256, 0, s>>>(ea);
             fa.aeff = w.aeff;
             fa.mlog = w.mlog;
+            fa.xsum = w.xsum;
             fa.mask_out = m->mask_out;
             ad = m->mask_kind;
         }
@@ -2739,15 +2767,17 @@ size_t samnerf_mask_train_workspace_size(uint32_t N) { return mask_train_workspa
 static int mask_train_inputs(const samnerf_model* m, uint32_t N, const void* render_ws, size_t render_bytes,
                              Workspace& w, GridDesc<16>& gm, const char* what) {
     if (!m) return fail(SAMNERF_EINVAL, "%s: null model", what);
-    if (!m->with_mask || m->mask_kind != 0)
-        return fail(SAMNERF_EINVAL, "%s: model has no 'default' mask head (with_mask = 1, mask_kind = 0)", what);
+    if (!m->with_mask || m->mask_kind < 0 || m->mask_kind > 2)
+        return fail(SAMNERF_EINVAL, "%s: model has no fused mask head (with_mask = 1, mask_kind 0-2)", what);
+    if (m->mask_out < 1 || m->mask_out > 32)
+        return fail(SAMNERF_EINVAL, "%s: mask_out %u outside 1..32", what, m->mask_out);
     if (m->num_steps[2] != 32) return fail(SAMNERF_EINVAL, "%s: fused path is built for 32 final samples", what);
     if (!render_ws) return fail(SAMNERF_EINVAL, "%s: null render workspace", what);
     w = carve(m, N, const_cast<void*>(render_ws));
     if (render_bytes < w.bytes)
         return fail(SAMNERF_EWORKSPACE, "%s: render workspace needs %zu bytes, got %zu", what, w.bytes,
                     render_bytes);
-    return make_grid_desc(m->m_grid, 8, 16, gm, "m_grid");
+    return m->mask_kind == 0 ? make_grid_desc(m->m_grid, 8, 16, gm, "m_grid") : SAMNERF_OK;
 }
 
 int samnerf_mask_train_forward(const samnerf_model* m, uint32_t N, float* logits, const void* render_ws,
@@ -2759,6 +2789,9 @@ int samnerf_mask_train_forward(const samnerf_model* m, uint32_t N, float* logits
     if (rc) return rc;
     if (N == 0) return SAMNERF_OK;
     if (!logits || !workspace) return fail(SAMNERF_EINVAL, "mask_train_forward: null pointer");
+    if (m->mask_kind != 0)                               // adaptive: the chain on the per-ray sums
+        return adaptive_train_forward(m, w.xsum, N, logits, workspace, workspace_bytes,
+                                      reinterpret_cast<hipStream_t>(stream));
     const RayTiles tiles = g_taps_on ? RayTiles{0u, 0u} : make_ray_tiles(N, m->view_width);
     return mask_train_forward(m, gm, w.u_f, w.w_f, w.geo_f, N, tiles, logits, workspace, workspace_bytes,
                               reinterpret_cast<hipStream_t>(stream));
@@ -2773,8 +2806,12 @@ int samnerf_mask_train_backward(const samnerf_model* m, uint32_t N, const float*
     int rc = mask_train_inputs(m, N, render_ws, render_bytes, w, gm, "mask_train_backward");
     if (rc) return rc;
     if (N == 0) return SAMNERF_OK;
-    if (!grad_logits || !grad_mask_w || !grad_m_grid || !workspace)
+    if (!grad_logits || !grad_mask_w || !workspace)
         return fail(SAMNERF_EINVAL, "mask_train_backward: null pointer");
+    if (m->mask_kind != 0)                               // adaptive: no grid gradient (all inputs detached)
+        return adaptive_train_backward(m, w.xsum, N, grad_logits, grad_mask_w, workspace, workspace_bytes,
+                                       reinterpret_cast<hipStream_t>(stream));
+    if (!grad_m_grid) return fail(SAMNERF_EINVAL, "mask_train_backward: null m_grid gradient");
     for (int i = 0; i < 3; ++i)
         if (!grad_mask_w[i]) return fail(SAMNERF_EINVAL, "mask_train_backward: null gradient");
     const RayTiles tiles = g_taps_on ? RayTiles{0u, 0u} : make_ray_tiles(N, m->view_width);

@@ -158,6 +158,9 @@ struct HeadArgs {
 // are 16-B aligned (the [N, 256] output), four 4-B stores inside a gather tile
 // whose rows are not (kernel-uniform branch)
 __device__ __forceinline__ void store_out4(float* p, const float4& y, bool vec) {
+#ifdef SAMNERF_AB_STORE4   // timing A/B only
+    vec = true;
+#endif
     if (vec) {
         *reinterpret_cast<float4*>(p) = y;
     } else {

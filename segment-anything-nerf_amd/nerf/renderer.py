@@ -206,14 +206,16 @@ class NeRFRenderer(nn.Module):
                 and (not torch.is_tensor(bg_color) or bg_color.numel() == 1))
 
     def _fused_mask_train_ok(self, rays_o, bg_color, perturb, return_feats, return_mask):
-        """Train mode under grad with return_mask=1 for a 'default' mask head
-        (the --with_mask step, utils.py:946-948): the HIP mask-head training
-        kernels (samnerf_amd.fused.render_mask_train)."""
+        """Train mode under grad with return_mask=1 for a fused mask head --
+        'default', 'adaptive' / 'density' (the reference's scripts/train_mask.sh)
+        or 'adaptive' / 'rgb' with sum_after_mlp (the --with_mask step,
+        utils.py:946-948): the HIP mask-head training kernels
+        (samnerf_amd.fused.render_mask_train)."""
         o = self.opt
         if not (return_mask and not return_feats and getattr(o, "with_mask", False)):
             return False
         from samnerf_amd.fused import mask_kind
-        return (mask_kind(self) == 0 and o.mask_mlp_type == "default" and self.fused and rays_o.is_cuda
+        return (mask_kind(self) is not None and self.fused and rays_o.is_cuda
                 and self.training and torch.is_grad_enabled() and not perturb
                 and not (getattr(o, "sum_after_mlp", False) and o.with_sam)
                 and o.background == "last_sample"

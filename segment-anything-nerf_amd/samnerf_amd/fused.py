@@ -461,15 +461,19 @@ def render_sam_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None,
 
 # ----------------------------------------------------------- mask training --
 class _FusedMaskTrain(torch.autograd.Function):
-    """instance_mask_logits of a 'default' mask head in the --with_mask training
+    """instance_mask_logits of a fused mask head in the --with_mask training
     step (nerf/utils.py:941-977 -> renderer.py:392-395, :451-452), forward and
-    backward on the HIP kernels (mask_head_train.hip, exact fp32 MFMA):
-    differentiable w.r.t. m_grid.embeddings and the three mask_mlp weights,
-    the tensors the reference's loss reaches (weights and geo_feat are
-    detached there).  image / depth / weights_sum come back without gradient."""
+    backward on the HIP kernels (mask_head_train.hip): for a 'default' head
+    (exact fp32 MFMA) differentiable w.r.t. m_grid.embeddings and the three
+    mask_mlp weights, for an 'adaptive' head (density, or rgb with
+    sum_after_mlp) w.r.t. its six / eight mask_mlp weights -- the tensors the
+    reference's loss reaches (weights, geo_feat and the grid_mlp / view_mlp
+    intermediates are detached there).  image / depth / weights_sum come back
+    without gradient.  params = (m_grid.embeddings, W0, W1, W2) for a 'default'
+    head, the mask_mlp weights in order for an adaptive one."""
 
     @staticmethod
-    def forward(ctx, renderer, rays_o, rays_d, cnf, bg, m_emb, w0, w1, w2):
+    def forward(ctx, renderer, rays_o, rays_d, cnf, bg, *params):
         N = rays_o.shape[0]
         dev = rays_o.device
         out = renderer.render(rays_o, rays_d, cnf, bg, keep_workspace=True, feats=False,
@@ -482,7 +486,8 @@ class _FusedMaskTrain(torch.autograd.Function):
         check(lib().samnerf_mask_train_forward(ctypes.byref(m), N, _ptr(logits), _ptr(ws), need, _ptr(tws),
                                                tneed, _stream(rays_o)), "mask_train_forward")
         ctx.state = (m, vw, ws, need, tws, tneed, list(renderer._keep))
-        ctx.shapes = (m_emb.shape, w0.shape, w1.shape, w2.shape)
+        ctx.shapes = tuple(p.shape for p in params)
+        ctx.kind = int(m.mask_kind)
         ctx.mark_non_differentiable(out["image"], out["depth"], out["weights_sum"])
         return logits, out["image"], out["depth"], out["weights_sum"]
 
@@ -491,30 +496,34 @@ class _FusedMaskTrain(torch.autograd.Function):
         m, vw, ws, need, tws, tneed, _ = ctx.state
         g = g_logits.contiguous().float()          # bound: alive through the C call
         dev = g.device
-        g_emb = torch.zeros(ctx.shapes[0], device=dev)
-        gw = [torch.empty(sh, device=dev) for sh in ctx.shapes[1:]]
-        arr = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in gw])
+        adaptive = ctx.kind != 0
+        g_emb = None if adaptive else torch.zeros(ctx.shapes[0], device=dev)
+        gw = [torch.empty(sh, device=dev) for sh in (ctx.shapes if adaptive else ctx.shapes[1:])]
+        arr = (ctypes.c_void_p * 8)(*[t.data_ptr() for t in gw])
         m.with_mask, m.view_width = 1, vw
         check(lib().samnerf_mask_train_backward(ctypes.byref(m), g.shape[0], _ptr(g), arr, _ptr(g_emb),
                                                 _ptr(ws), need, _ptr(tws), tneed, _stream(g)),
               "mask_train_backward")
-        return (None,) * 5 + (g_emb, *gw)
+        return (None,) * 5 + ((*gw,) if adaptive else (g_emb, *gw))
 
 
 def render_mask_train(renderer, rays_o, rays_d, cam_near_far=None, bg_color=None):
-    """NeRFRenderer.run in train mode under grad with return_mask=1 for a
-    'default' mask head (the mask training step's render, utils.py:946-948):
-    image, depth, weights_sum (no gradient) and instance_mask_logits with
-    gradient to m_grid and mask_mlp (_FusedMaskTrain)."""
+    """NeRFRenderer.run in train mode under grad with return_mask=1 for a fused
+    mask head (the mask training step's render, utils.py:946-948): image,
+    depth, weights_sum (no gradient) and instance_mask_logits with gradient to
+    the head's trained tensors (_FusedMaskTrain): m_grid and mask_mlp for a
+    'default' head, the mask_mlp Linears for an adaptive one."""
     net = renderer.net
-    skip = net.mask_mlp[0]
     rays_o = rays_o.contiguous().float()
     rays_d = rays_d.contiguous().float()
     bg = 1.0 if bg_color is None else float(bg_color)
     cnf = None if cam_near_far is None else cam_near_far.contiguous().float()
-    logits, image, depth, wsum = _FusedMaskTrain.apply(
-        renderer, rays_o, rays_d, cnf, bg, net.m_grid.embeddings,
-        skip.net[0].weight, skip.net[1].weight, skip.net[2].weight)
+    if mask_kind(net) == 0:
+        skip = net.mask_mlp[0]
+        params = (net.m_grid.embeddings, skip.net[0].weight, skip.net[1].weight, skip.net[2].weight)
+    else:
+        params = tuple(layer.weight for layer in net.mask_mlp)
+    logits, image, depth, wsum = _FusedMaskTrain.apply(renderer, rays_o, rays_d, cnf, bg, *params)
     return {"image": image, "depth": depth, "weights_sum": wsum, "instance_mask_logits": logits}
 
 
