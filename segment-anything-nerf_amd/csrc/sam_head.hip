@@ -158,9 +158,6 @@ struct HeadArgs {
 // are 16-B aligned (the [N, 256] output), four 4-B stores inside a gather tile
 // whose rows are not (kernel-uniform branch)
 __device__ __forceinline__ void store_out4(float* p, const float4& y, bool vec) {
-#ifdef SAMNERF_AB_STORE4   // timing A/B only
-    vec = true;
-#endif
     if (vec) {
         *reinterpret_cast<float4*>(p) = y;
     } else {
@@ -806,7 +803,12 @@ struct HeadStreamQ {
     }
 };
 
-template <int NBUF, bool STAMP = false>
+// VEC: the output rows are 16-B aligned (the [N, 256] samvit array): float4
+// stores.  The gather-tile form (samnerf_render_forward_tile, rows of 261
+// floats) is its own instantiation with 4-B stores: a run-time choice in the
+// one kernel cost the product head 0.575 -> 0.67 ms per view (measured A/B,
+// the epilogue's packed fp32 math was lost to the second store path).
+template <int NBUF, bool STAMP = false, bool VEC = true>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_sam_head_h16q(HeadArgsH a, uint32_t ntiles) {
     unsigned long long t0 = 0, rt0 = 0;                   // STAMP: the wave's clock over its life
@@ -964,7 +966,7 @@ k_sam_head_h16q(HeadArgsH a, uint32_t ntiles) {
                     y.y = ((acc[t][4 * mm + 1] - mf) * rstd) * lw[u + 1] + lb[u + 1];
                     y.z = ((acc[t][4 * mm + 2] - mf) * rstd) * lw[u + 2] + lb[u + 2];
                     y.w = ((acc[t][4 * mm + 3] - mf) * rstd) * lw[u + 3] + lb[u + 3];
-                    store_out4(o + u, y, a.vec_out);
+                    store_out4(o + u, y, VEC);
                 }
         }
         st.rot = (st.rot + kSteps) % NBUF;
@@ -1337,7 +1339,8 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
 #endif
         {
             const uint32_t grid = blocks < (uint32_t)device_cus() ? blocks : (uint32_t)device_cus();
-            k_sam_head_h16q<4><<<grid, 256, 0, s>>>(a, blocks);   // persistent, one workgroup per CU
+            if (vec) k_sam_head_h16q<4><<<grid, 256, 0, s>>>(a, blocks);   // persistent, one workgroup per CU
+            else k_sam_head_h16q<4, false, false><<<grid, 256, 0, s>>>(a, blocks);
         }
         return check_launch("sam_head_h16");
     }
