@@ -660,23 +660,42 @@ class ViewRunner:
         return dt, last, stage_avg, stage_src
 
 
+VALU_RATE = os.path.join(REPO, "profiles", "r4_valu_rate.json")
+
+
+def valu_cycles_per_inst():
+    """Cycles per wave64 VALU instruction of one SIMD at saturation, measured
+    by tools/valu_rate.hip (profiles/r4_valu_rate.json: independent v_fma_f32
+    streams, the best over 1-8 resident waves per SIMD); the guide's 2 cycles
+    (MI355X_MICROARCH.md, SIMD-32) without the file."""
+    try:
+        r = json.load(open(VALU_RATE))["kinds"]["v_fma_f32"]
+        return min(v["cycles_per_inst"] for v in r.values()), os.path.relpath(VALU_RATE, REPO)
+    except Exception:
+        return 2.0, "MI355X_MICROARCH.md (2 cycles per v_fma_f32, SIMD-32)"
+
+
 def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None):
     """`roofline` of the dominant kernel and every stage, each against the
-    guide peak of the unit closest to saturation:
+    guide peak of its units:
       l2   -- algorithmic bytes (embedding gathers + ray I/O, ALG_BYTES_PER_RAY)
               / live time vs the L2's 34.5 TB/s (the tables are L2/MALL-resident;
               not for s_grid, whose box gathers read a row once per wave);
-      valu -- VALU-issue cycles of the stage's kernels (PMC SQ_ACTIVE_INST_VALU
-              x 4 per ray, profiles/pmc_rates.json) / (1024 SIMDs x 2.4 GHz x
-              live time);
-      mfma -- the SAM head's MFMA issue cycles from its structure (86 k-blocks
-              x 8 tiles x 3 v_mfma_f32_32x32x16_f16 per 32 rays) / (1024 x 2.4
-              GHz x live time), with the PMC MFMA-busy cycles beside it.
-    The nominal clock makes every busy fraction a lower bound (the chip runs
-    below 2.4 GHz under load); `frac_at_measured_clock` rescales the VALU / MFMA
-    fractions by the stage's measured clock (profiles/kernel_clock.json)."""
+      valu -- the VALU pipe's share: issued VALU instructions (PMC SQ_INSTS_VALU
+              per ray, profiles/pmc_rates.json) x the measured cycles per
+              instruction at saturation (tools/valu_rate.hip: 2, the guide's
+              SIMD-32 rate) / (1024 SIMDs x 2.4 GHz x live time);
+      mfma -- MFMA-busy cycles (PMC SQ_VALU_MFMA_BUSY_CYCLES per ray) over the
+              same SIMD cycles; for the SAM head also from its structure (86
+              k-blocks x 8 tiles x 3 v_mfma_f32_32x32x16_f16 per 32 rays).
+    `bound` is the unit with the largest share; when none reaches 0.6 the stage
+    is marked latency-bound (`regime`), with the PMC wave-cycle shares --
+    waiting on memory / barriers, issue stalls, issuing -- beside it.  The nominal clock makes every share a lower
+    bound; `frac_at_measured_clock` rescales by the stage's measured clock
+    (profiles/kernel_clock.json)."""
     st_rates = (rates or {}).get("stages", {})
     cyc_avail = lambda ms: N_SIMD * CLOCK_GHZ * 1e9 * ms * 1e-3
+    cpi, cpi_src = valu_cycles_per_inst()
 
     def entry(st):
         ms = stage_avg.get(st, 0.0)
@@ -689,10 +708,11 @@ def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None):
             cand["l2"] = {"unit": "GB/s", "achieved": alg / (ms * 1e-3) / 1e9, "peak": L2_PEAK_GBS,
                           "alg_bytes_per_ray": ALG_BYTES_PER_RAY[st]}
             cand["l2"]["frac"] = cand["l2"]["achieved"] / L2_PEAK_GBS
-        if "valu_cycles_per_ray" in r:
-            c = r["valu_cycles_per_ray"] * band_rays
-            cand["valu"] = {"unit": "busy cycles / SIMD cycles", "frac": c / cyc_avail(ms),
-                            "valu_cycles_per_ray": r["valu_cycles_per_ray"]}
+        if "valu_insts_per_ray" in r:
+            c = r["valu_insts_per_ray"] * band_rays * cpi
+            cand["valu"] = {"unit": "VALU pipe cycles / SIMD cycles", "frac": c / cyc_avail(ms),
+                            "valu_insts_per_ray": r["valu_insts_per_ray"], "cycles_per_inst": cpi,
+                            "cycles_per_inst_source": cpi_src}
         if st == "sam_head":
             cyc = HEAD_MFMA_CYCLES_PER_32[head_mode] * band_rays / 32
             cand["mfma"] = {"unit": "TFLOP/s", "frac": cyc / cyc_avail(ms),
@@ -703,10 +723,17 @@ def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None):
                                      "2.4 GHz x time)"}
             if "mfma_busy_cycles_per_ray" in r:
                 cand["mfma"]["pmc_mfma_busy_frac"] = r["mfma_busy_cycles_per_ray"] * band_rays / cyc_avail(ms)
+        elif r.get("mfma_busy_cycles_per_ray"):
+            cand["mfma"] = {"unit": "MFMA busy cycles / SIMD cycles",
+                            "frac": r["mfma_busy_cycles_per_ray"] * band_rays / cyc_avail(ms)}
         if not cand:
             return None
         bound = max(cand, key=lambda k: cand[k]["frac"])
         e = {"bound": bound}
+        if cand[bound]["frac"] < 0.6:
+            e["regime"] = "latency-bound: no unit reaches 0.6 of its peak (wave_cycle_shares)"
+        if "wave_cycle_shares" in r:
+            e["wave_cycle_shares"] = r["wave_cycle_shares"]
         if st == "s_grid":
             # the box form reads each distinct corner row once per wave, so the
             # algorithmic gather bytes (every lane's 8 corners) are no traffic

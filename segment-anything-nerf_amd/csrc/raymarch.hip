@@ -1022,10 +1022,13 @@ k_final(FinalArgs a) {
     };
     // rb_prev of sample i is rb_next of sample i - 1 when S == 1 (same bits;
     // saves a division), recomputed from the bins otherwise
-    auto position = [&](int i, float& rbp, float& rbn, float& ux, float& uy, float& uz) {
+    // the sample's position from its two raw bins (b0 read only when S > 1:
+    // for S == 1 rbp is the previous sample's rbn, or the pre-loop rb_prev)
+    auto position_of = [&](int i, float b0, float b1, float& rbp, float& rbn, float& ux, float& uy,
+                           float& uz) {
         const int k = i * S + seg;
-        if (S > 1 || i == i_begin) rbp = real_bin(sn, sf, a.bins_in[(size_t)k * N + rr]);
-        rbn = real_bin(sn, sf, a.bins_in[(size_t)(k + 1) * N + rr]);
+        if (S > 1) rbp = real_bin(sn, sf, b0);
+        rbn = real_bin(sn, sf, b1);
         const float t = (rbn + rbp) / 2.0f;
         float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
         contract3(x, y, z);
@@ -1038,6 +1041,20 @@ k_final(FinalArgs a) {
             a.u_out[((size_t)k * 3 + 2) * N + r] = uz;
         }
     };
+    auto position = [&](int i, float& rbp, float& rbn, float& ux, float& uy, float& uz) {
+        const int k = i * S + seg;
+        position_of(i, S > 1 ? a.bins_in[(size_t)k * N + rr] : 0.0f, a.bins_in[(size_t)(k + 1) * N + rr], rbp,
+                    rbn, ux, uy, uz);
+    };
+    // not PF: the next sample's raw bins are loaded one sample ahead, so the
+    // gathers of a sample start without a dependent global load in front
+    // (the load of sample i + 1's bins is in flight behind sample i's work)
+    float nb0 = 0.0f, nb1 = 0.0f;
+    if constexpr (!PF) {
+        const int kb0 = i_begin * S + seg;
+        if (S > 1) nb0 = a.bins_in[(size_t)kb0 * N + rr];
+        nb1 = a.bins_in[(size_t)(kb0 + 1) * N + rr];
+    }
     GatherC2<4> pre;                                      // PF: kb kPre of the current sample
     float p_rbp = rb_prev, p_rbn = 0.0f, p_ux = 0.0f, p_uy = 0.0f, p_uz = 0.0f;
     if constexpr (PF) {
@@ -1058,7 +1075,13 @@ k_final(FinalArgs a) {
             uy = p_uy;
             uz = p_uz;
         } else {
-            position(i, rb_prev, rb_next, ux, uy, uz);
+            const float b0 = nb0, b1 = nb1;
+            if (i + 1 < i_end) {
+                const int kn = (i + 1) * S + seg;
+                if (S > 1) nb0 = a.bins_in[(size_t)kn * N + rr];
+                nb1 = a.bins_in[(size_t)(kn + 1) * N + rr];
+            }
+            position_of(i, b0, b1, rb_prev, rb_next, ux, uy, uz);
         }
         const float t = (rb_next + rb_prev) / 2.0f;
         // weight fragments are re-read from LDS each sample rather than
@@ -1225,7 +1248,12 @@ k_final(FinalArgs a) {
         // sigma pre-activation = row 0, held by the lower half-wave
         const float s_lo = o3[0];
         const float s_hi = __shfl_xor(s_lo, 32);
-        const float sigma = expf(hh == 0 ? s_lo : s_hi);
+#ifdef SAMNERF_AB_FASTEXP   // timing A/B only
+#define KF_EXP __expf
+#else
+#define KF_EXP expf
+#endif
+        const float sigma = KF_EXP(hh == 0 ? s_lo : s_hi);
         // composite (renderer.py:300-307): w_k = alpha_k * exp(-sum_{j<k} ds_j),
         // the sum in double and in sample order across the ray's S slots
         const float ds = k == T - 1 ? INFINITY : (rb_next - rb_prev) * sigma;
@@ -1236,7 +1264,7 @@ k_final(FinalArgs a) {
             if (s2 < seg) before += (double)d2;
             cum += (double)d2;
         }
-        const float w = nan_to_num((1.0f - expf(-ds)) * expf(-(float)before));
+        const float w = nan_to_num((1.0f - KF_EXP(-ds)) * KF_EXP(-(float)before));
         if (sample_writer) a.w_out[(size_t)k * N + r] = w;
         if (a.sigma_tap && sample_writer) a.sigma_tap[(size_t)k * N + r] = sigma;
         wsum += (double)w;
@@ -1622,21 +1650,39 @@ k_sgrid_box4(SgridArgs a) {
             const bool ordered = wave_positions_ordered(ux, uy, uz);
             uint32_t p0, p1, p2;
             pbox_lane(mine, ur, p0, p1, p2);
+            // the boxes that fit one slice (in level order, kBoxSlots slots in
+            // all) are staged in ONE pass of LDS DMA -- every row in flight at
+            // once, one memory round trip for the 4 levels -- and read from
+            // LDS; a level whose box does not fit gathers directly
+            PBox bb[4];
+            uint32_t boff[4], btot = 0u, staged = 0u;
 #pragma unroll
             for (int l = 0; l < 4; ++l) {
-                const PBox b = pbox_read(p0, p1, p2, l);
+                bb[l] = pbox_read(p0, p1, p2, l);
+                boff[l] = btot;
+                if (btot + bb[l].slots <= kBoxSlots) {
+                    btot += bb[l].slots;
+                    staged |= 1u << l;
+                } else {
+                    bb[l].slots = 0u;                       // not staged: no slots in the slice
+                }
+            }
+            wave_lds_sync();                                // the previous sample's reads done
+            stage_pbox4_dma(base, L, bb, boff, btot, (uint32_t)reinterpret_cast<uintptr_t>(slice), lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the DMA (and the prefetch) landed
+            wave_lds_sync();
+            const char* sc = reinterpret_cast<const char*>(slice);
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
                 float f[8];
                 uint32_t* rt = nullptr;                     // parity taps only
                 if (TAP && live && r % a.tap_stride == 0u)
                     rt = a.rows_tap + ((size_t)(r / a.tap_stride) * T + k) * 128u + (4 * g + l) * 8;
-                if (b.slots <= kBoxSlots) {
-                    wave_lds_sync();                        // previous level's reads done
-                    stage_pbox<8>(base, L[l], b, slice, lane);
-                    wave_lds_sync();
+                if ((staged >> l) & 1u) {
                     if (ordered)
-                        lookup_level3_pbox<8, false>(a.grid.emb, L[l], b, slice, ux, uy, uz, f, rt);
+                        lookup_level3_pbox8_dma<false>(a.grid.emb, L[l], bb[l], sc, boff[l], ux, uy, uz, f, rt);
                     else
-                        lookup_level3_pbox<8, true>(a.grid.emb, L[l], b, slice, ux, uy, uz, f, rt);
+                        lookup_level3_pbox8_dma<true>(a.grid.emb, L[l], bb[l], sc, boff[l], ux, uy, uz, f, rt);
                 } else {
                     if (rt) tap_direct_rows<8>(L[l], ux, uy, uz, rt);
                     lookup_level3<8>(a.grid.emb, L[l], ux, uy, uz, f);

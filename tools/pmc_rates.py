@@ -56,6 +56,18 @@ def main(root):
         e = {"kernels": sorted(d["kernels"]), "counters_per_view": dict(c)}
         if "SQ_ACTIVE_INST_VALU" in c:
             e["valu_cycles_per_ray"] = 4.0 * c["SQ_ACTIVE_INST_VALU"] / RAYS
+        if "SQ_INSTS_VALU" in c:
+            # issued VALU instructions (MFMAs included: they are VALU-encoded; a
+            # handful per sample against ~1,000), priced at the measured issue
+            # rate of independent VALU streams (profiles/r4_valu_rate.json)
+            e["valu_insts_per_ray"] = c["SQ_INSTS_VALU"] / RAYS
+        if "SQ_WAIT_ANY" in c and "SQ_WAVE_CYCLES" in c and c["SQ_WAVE_CYCLES"] > 0:
+            # wave-cycle shares (MI355X_MICROARCH.md rocprofv3 slots: WAIT_ANY +
+            # WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES, disjoint)
+            wc = c["SQ_WAVE_CYCLES"]
+            e["wave_cycle_shares"] = {"wait_any": c["SQ_WAIT_ANY"] / wc,
+                                      "wait_inst_any": c.get("SQ_WAIT_INST_ANY", 0.0) / wc,
+                                      "active_inst_any": c.get("SQ_ACTIVE_INST_ANY", 0.0) / wc}
         if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
             e["mfma_busy_cycles_per_ray"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / RAYS
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
