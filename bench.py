@@ -294,6 +294,20 @@ def mask_view(dev, steps, warmup, head_mode=0, ref_rays=32768):
         out = view()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    # the same view without the instance logits: the difference is the mask
+    # head's share (k_mask_head + the per-sample geo_feat stores)
+    for _ in range(warmup):
+        fr.render(*ops.get_rays(pose, intr, H, W, device=dev), mask=False, view_width=W)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fr.render(*ops.get_rays(pose, intr, H, W, device=dev), mask=False, view_width=W)
+    torch.cuda.synchronize()
+    dt_nomask = (time.perf_counter() - t0) / steps
+    head_ms = (dt - dt_nomask) * 1e3
+    # f16x3: 3 fp16 MFMA products per fp32 product of 143->256->256->32 (the
+    # padded output tile) per sample, 32 samples per ray
+    head_flop = 3 * 2 * (144 * 256 + 256 * 256 + 256 * 32) * 32 * H * W
     ro, rd = ops.get_rays(pose, intr, H, W, device=dev)
     n, chunk = min(ref_rays, H * W), 16384
     with torch.no_grad():
@@ -309,6 +323,9 @@ def mask_view(dev, steps, warmup, head_mode=0, ref_rays=32768):
             "reference_equivalent_gpu": {"value": 1.0 / dt_ref, "unit": "rays/s", "rays": n},
             "speedup": (H * W / dt) * dt_ref,
             "max_abs_logits_vs_unfused": err, "dtype": DTYPE[head_mode],
+            "ms_without_mask": dt_nomask * 1e3, "mask_head_ms": head_ms,
+            "mask_head_mfma_frac": (head_flop / (head_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFS
+                                    if head_mode == 0 and head_ms > 0 else None),
             "what": "--with_mask 'default' head (m_grid L16C8 + SkipConnMLP 143->256->256->2 per sample, "
                     "weighted sum): fused render + k_mask_head vs run_torch(return_mask=1), 512x512 view"}
 

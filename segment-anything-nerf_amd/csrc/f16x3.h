@@ -70,19 +70,39 @@ __device__ __forceinline__ float exp2i(int k) {
 // convert took 6.  The same bits as that sequence (x s and x s - hi are exact
 // in fp32, so both round the same value once).
 //
-// Wait states (nothing inside an asm string is padded by hipcc): a
-// v_fma_mixhi_f16 writes the HIGH half of its destination (op_sel dst), and a
-// VALU that reads a VGPR right after such a partial write needs one wait state
-// (gfx950's dst-sel forwarding hazard) -- so all four hi dwords are written
-// first and each is read by the lo half 4+ instructions later; the string ends
-// with s_nop 1 because its outputs feed MFMA A/B operands, which need two wait
-// states after a VALU write (the guide's VALU -> MFMA operand rule).  The round-1
-// to round-3 form (hi, then lo, of each pair back to back) read the hi dword
-// one instruction after its partial write: on a busy SIMD another wave's
-// instruction usually sat between them, so the outputs were right on most
-// launches and wrong on a few (the k_final prefetch variants'
-// "nondeterminism").
-#ifdef SAMNERF_AB_OLDSPLIT   // timing A/B only: the round-3 form (hazard-exposed)
+// Wait states (nothing inside an asm string is padded by hipcc): both mix
+// forms write half of their destination and keep the other half (a
+// read-modify-write of the dword), and a VALU that reads a VGPR right after
+// such a partial write needs one wait state (gfx950's dst-sel forwarding
+// hazard).  So every dword's partial writes and reads here are 4 instructions
+// apart: the four hi dwords' low halves, then their high halves, then the lo
+// dwords' low halves (reading the hi dwords), then their high halves; the
+// string ends with s_nop 1 because its outputs feed MFMA A/B operands, which
+// need two wait states after a VALU write (the guide's VALU -> MFMA operand
+// rule; it also covers the last partial write).  The round-1 to round-3 form
+// (hi, then lo, of each pair back to back) read the hi dword one instruction
+// after its partial write: on a busy SIMD another wave's instruction usually
+// sat between them, so the outputs were right on most launches and wrong on a
+// few (the k_final prefetch variants' "nondeterminism"); the
+// first round-4 form still wrote each hi dword's two halves back to back.
+#if defined(SAMNERF_F16X3_NOASM)
+// The same split in plain C (v_pk_mul_f32, v_cvt_pk_f16_f32, conversions back,
+// a subtraction, v_cvt_pk_f16_f32 again): full-dword writes the compiler
+// schedules and pads itself; the same bits (x s and x s - hi are exact).
+__device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
+    uint32_t h[4], l[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const float a = v[2 * p] * s, b = v[2 * p + 1] * s;
+        const f16x2v hh = {(_Float16)a, (_Float16)b};
+        const f16x2v ll = {(_Float16)(a - (float)hh.x), (_Float16)(b - (float)hh.y)};
+        h[p] = __builtin_bit_cast(uint32_t, hh);
+        l[p] = __builtin_bit_cast(uint32_t, ll);
+    }
+    hi = make_uint4(h[0], h[1], h[2], h[3]);
+    lo = make_uint4(l[0], l[1], l[2], l[3]);
+}
+#elif defined(SAMNERF_AB_OLDSPLIT)   // timing A/B only: the round-3 form (hazard-exposed)
 __device__ __forceinline__ void split_pair_f16_old(float x, float y, float s, uint32_t& hi, uint32_t& lo) {
     uint32_t h, l;
     asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
@@ -104,20 +124,20 @@ __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, u
 __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
     uint32_t h0, h1, h2, h3, l0, l1, l2, l3;
     asm("v_fma_mixlo_f16 %0, %8, %16, 0\n\t"
-        "v_fma_mixhi_f16 %0, %9, %16, 0\n\t"
         "v_fma_mixlo_f16 %1, %10, %16, 0\n\t"
-        "v_fma_mixhi_f16 %1, %11, %16, 0\n\t"
         "v_fma_mixlo_f16 %2, %12, %16, 0\n\t"
-        "v_fma_mixhi_f16 %2, %13, %16, 0\n\t"
         "v_fma_mixlo_f16 %3, %14, %16, 0\n\t"
+        "v_fma_mixhi_f16 %0, %9, %16, 0\n\t"
+        "v_fma_mixhi_f16 %1, %11, %16, 0\n\t"
+        "v_fma_mixhi_f16 %2, %13, %16, 0\n\t"
         "v_fma_mixhi_f16 %3, %15, %16, 0\n\t"
         "v_fma_mixlo_f16 %4, %8, %16, -%0 op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixhi_f16 %4, %9, %16, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
         "v_fma_mixlo_f16 %5, %10, %16, -%1 op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixhi_f16 %5, %11, %16, -%1 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
         "v_fma_mixlo_f16 %6, %12, %16, -%2 op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixhi_f16 %6, %13, %16, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
         "v_fma_mixlo_f16 %7, %14, %16, -%3 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %4, %9, %16, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %5, %11, %16, -%1 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %6, %13, %16, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
         "v_fma_mixhi_f16 %7, %15, %16, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
         "s_nop 1"
         : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3)
@@ -130,6 +150,9 @@ __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, u
 
 // running max |a|, |b| into m (one v_max3_f32 with |.| source modifiers)
 __device__ __forceinline__ float max_abs3(float m, float a, float b) {
+#if defined(SAMNERF_F16X3_NOASM)
+    return fmaxf(m, fmaxf(fabsf(a), fabsf(b)));
+#endif
     float r;
     asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
     return r;

@@ -46,6 +46,16 @@ constexpr int kHkb = 16;                      // 256 -> 16 k-blocks
 constexpr int kStepsPerSample = kL0kb + kHkb + 2;   // 27
 constexpr int kStepVec = 2 * 8 * 64;          // uint4 per step
 constexpr int kSlots = 128;                   // ray slots per workgroup
+constexpr int kPackVec = kStepsPerSample * kStepVec;   // uint4 of one copy of the weight fragments
+// Copies of the fragments: every workgroup streams the same steps at about
+// the same time; workgroup b reads copy (b >> 3) % kMaskCopies so that each
+// XCD's requests spread over that many times as many L2 channels (the
+// SAM head's kHeadCopies).  The copies hold the same bits.  Measured no
+// faster (9.13 vs 9.04 ms per mask view with the VGPR-staged stream), so one.
+#ifndef SAMNERF_MASK_COPIES
+#define SAMNERF_MASK_COPIES 1
+#endif
+constexpr int kMaskCopies = SAMNERF_MASK_COPIES;
 constexpr int kT = 32;                        // final samples per ray
 __device__ __forceinline__ int rho(int q) { return (q & 3) + 8 * (q >> 2); }
 __device__ __forceinline__ int hidden_unit(int kb, int h, int m) {
@@ -119,8 +129,11 @@ k_mask_pack_f32(const float* __restrict__ w0, const float* __restrict__ w1, cons
     for (int m = 0; m < 8; ++m) v[m] = mask_weight(w0, w1, w2, K, step, slot, lane, m);
     uint4 a, b;
     to_operand<true>(v, 1.0f, a, b);
-    packed[(size_t)step * kStepVec + slot * 64 + lane] = a;
-    packed[(size_t)step * kStepVec + 512 + slot * 64 + lane] = b;
+#pragma unroll
+    for (int c = 0; c < kMaskCopies; ++c) {
+        packed[(size_t)c * kPackVec + (size_t)step * kStepVec + slot * 64 + lane] = a;
+        packed[(size_t)c * kPackVec + (size_t)step * kStepVec + 512 + slot * 64 + lane] = b;
+    }
 }
 
 // f16x3 weights (head_mode 0): one workgroup finds each tensor's max |w|, then
@@ -158,10 +171,13 @@ k_mask_pack_h16(const float* __restrict__ w0, const float* __restrict__ w1, cons
         for (int m = 0; m < 8; ++m) v[m] = mask_weight(w0, w1, w2, K, step, slot, lane2, m);
         uint4 a, b;
         to_operand<false>(v, exp2i(ke[step_layer(step)]), a, b);
-        packed[(size_t)step * kStepVec + slot * 64 + lane2] = a;
-        packed[(size_t)step * kStepVec + 512 + slot * 64 + lane2] = b;
+#pragma unroll
+        for (int c = 0; c < kMaskCopies; ++c) {
+            packed[(size_t)c * kPackVec + (size_t)step * kStepVec + slot * 64 + lane2] = a;
+            packed[(size_t)c * kPackVec + (size_t)step * kStepVec + 512 + slot * 64 + lane2] = b;
+        }
     }
-    if (tid < 3) reinterpret_cast<int*>(packed + (size_t)kStepsPerSample * kStepVec)[tid] = ke[tid];
+    if (tid < 3) reinterpret_cast<int*>(packed + (size_t)kMaskCopies * kPackVec)[tid] = ke[tid];
 }
 
 struct MaskArgs {
@@ -176,14 +192,12 @@ struct MaskArgs {
     float* out;              // [N][K] (ray order)
 };
 
-// The weight stream, staged through VGPRs: steps go in groups of kGroup; the
-// block's 256 threads load the next group (kGroup x 16 KiB, four 16-B loads
-// per thread and step) at the start of a group, write it to the other half of
-// a 2-group LDS ring after the group's MFMAs, then one barrier per group.
-// Ordinary loads and stores whose waits the compiler places itself.  (Round
-// 2: the SAM head's LDS-DMA ring (3- and 4-deep) measured DMA-throughput-bound
-// here, 10.1 / 8.92 ms per 512^2 view against 8.75 ms for this form; two steps
-// per group spilled 52-93 VGPRs; two register stages 13.7 ms.)
+// The round-2/3 weight stream (SAMNERF_MASK_RING=0 builds only), staged
+// through VGPRs: steps go in groups of kGroup; the block's 256 threads load the
+// next group (kGroup x 16 KiB, four 16-B loads per thread and step) at the
+// start of a group, write it to the other half of a 2-group LDS ring after the
+// group's MFMAs, then one barrier per group.  (Round 2: a dword LDS-DMA ring
+// measured slower than this form; two steps per group spilled 52-93 VGPRs.)
 constexpr uint32_t kGroup = 1;
 struct MaskStager {
     const uint4* __restrict__ packed;
@@ -244,6 +258,94 @@ struct MaskStager {
     }
 };
 
+// The weight stream by LDS DMA (global_load_lds_dwordx4: 16 B per lane
+// straight into LDS, no staging registers): a kRing-step ring, step s + kRing
+// - 1 requested at the start of step s, so a step's fragments have kRing - 1
+// steps of MFMA work to arrive in.  A step is 16 KiB = 4 DMA instructions per
+// wave.  At the end of step s each wave waits until step s + 1's requests are done
+// (vmcnt counted by hand: the later steps' 4 (kRing - 2) requests may stay in
+// flight; vector-memory completions count in order, and other loads issued
+// in between only make the wait stricter), then one barrier makes every
+// wave's part visible.  The slot a request overwrites was last read in step
+// s - 1, which every wave finished before the previous barrier.
+// Measured (round 4, 512^2 mask view, interleaved A/B of whole builds): the
+// VGPR-staged stream 9.04-9.13 ms per view, this ring 3-deep 8.59, 5-deep 8.36
+// (LDS: 5 x 16 KiB ring + 4 x 18 KiB layer-0 operands).  Attribution builds of
+// the VGPR-staged form: without the m_grid gathers 7.92 ms, without the weight
+// loads 8.77, without the step barriers 8.63 -- the gathers at each sample's
+// start are the largest single stall.
+#ifndef SAMNERF_MASK_RING
+#define SAMNERF_MASK_RING 5
+#endif
+constexpr int kRing = SAMNERF_MASK_RING;
+static_assert(kRing == 0 || (kRing >= 3 && kRing <= 5), "finish() counts vmcnt for 3-5 deep rings");
+struct MaskStagerDma {
+    const uint4* __restrict__ packed;
+    uint4* Wb;            // [kRing][kStepVec]
+    int tid, lane, wave;
+    uint32_t step;
+    uint32_t total;
+
+    // wave w moves uint4 256 w .. 256 w + 255 of step s (4 x 1 KiB); the
+    // step's offset is opaque so that the 27 steps' addresses are formed here,
+    // not hoisted out of the sample loop (27 x 4 address pairs spilled)
+    __device__ __forceinline__ void request(uint32_t s) {
+        uint32_t so = (s % kStepsPerSample) * (uint32_t)(kStepVec * 16);
+        asm volatile("" : "+s"(so));
+        const char* base = reinterpret_cast<const char*>(packed) + so;
+        const uint32_t vo = (uint32_t)(wave * 256 + lane) * 16u;
+        const uint32_t d = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)(Wb + (size_t)(s % kRing) * kStepVec + wave * 256));
+        uint32_t keep, t1, t2, t3;
+        // no "memory" clobber: the ring slot written here is not read before
+        // finish()'s wait and barrier (volatile asm keeps its place among them)
+        asm volatile(
+            "v_add_u32 %1, 1024, %4\n\tv_add_u32 %2, 2048, %4\n\tv_add_u32 %3, 3072, %4\n\t"
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %4, %5\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, %5\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %2, %5\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %3, %5\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+            : "v"(vo), "s"(base), "s"(d));
+    }
+    __device__ __forceinline__ void begin() {
+        for (uint32_t s = 0; s + 1 < (uint32_t)kRing && s < total; ++s) request(s);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    __device__ __forceinline__ const uint4* start() {
+        if (step + kRing - 1 < total) request(step + kRing - 1);
+        return Wb + (size_t)(step % kRing) * kStepVec + lane;
+    }
+    __device__ __forceinline__ void finish() {
+        if (step + kRing - 1 < total) {
+            if constexpr (kRing == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else if constexpr (kRing == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        ++step;
+    }
+
+    template <bool EXACT>
+    __device__ __forceinline__ void run8(floatx16 (&acc)[8], const uint4& b0, const uint4& b1) {
+        const uint4* cur = start();
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = kblock<EXACT>(cur[t * 64], cur[512 + t * 64], b0, b1, acc[t]);
+        finish();
+    }
+    template <bool EXACT>
+    __device__ __forceinline__ void run1(floatx16& acc, const uint4* b0, const uint4* b1) {
+        const uint4* cur = start();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = kblock<EXACT>(cur[k * 64], cur[512 + k * 64], b0[k], b1[k], acc);
+        finish();
+    }
+};
+
 __device__ __forceinline__ float leaky(float x) { return x < 0.0f ? x * 0.01f : x; }
 
 // leaky_relu on the accumulators, then the next layer's B operands (k-block
@@ -275,6 +377,43 @@ __device__ __forceinline__ int epilogue(floatx16 (&acc)[8], uint4 (&a0)[kHkb], u
     return k;
 }
 
+// lookup_level3<8> in two halves, so that one level's loads can run under a
+// weight step's MFMAs: the 8 corner rows (2 x 16 B each) and weights, then
+// the weighted sum in lookup_level3's order (the same bits)
+struct Gather8 {
+    float4 e[8][2];
+    float w[8];
+};
+__device__ __forceinline__ void gather8_issue(const float* __restrict__ emb, const LevelDesc& d, float ux, float uy,
+                                              float uz, Gather8& g) {
+    uint32_t off[8];
+    corner_rows<8>(d, ux, uy, uz, off, g.w);
+    const char* base = reinterpret_cast<const char*>(emb);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        g.e[c][0] = *reinterpret_cast<const float4*>(base + off[c]);
+        g.e[c][1] = *reinterpret_cast<const float4*>(base + off[c] + 16u);
+    }
+}
+__device__ __forceinline__ void gather8_finish(const Gather8& g, float* acc) {
+    f2v a[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = f2v{0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const f2v wc = {g.w[c], g.w[c]};
+        a[0] = __builtin_elementwise_fma(wc, f2v{g.e[c][0].x, g.e[c][0].y}, a[0]);
+        a[1] = __builtin_elementwise_fma(wc, f2v{g.e[c][0].z, g.e[c][0].w}, a[1]);
+        a[2] = __builtin_elementwise_fma(wc, f2v{g.e[c][1].x, g.e[c][1].y}, a[2]);
+        a[3] = __builtin_elementwise_fma(wc, f2v{g.e[c][1].z, g.e[c][1].w}, a[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        acc[2 * i] = a[i].x;
+        acc[2 * i + 1] = a[i].y;
+    }
+}
+
 constexpr int kXVec = kL0kb * 2 * 64;          // uint4 per wave: layer-0 B operands [kb][part][lane]
 constexpr int kDescVec = (16 * (int)sizeof(LevelDesc) + 15) / 16;
 
@@ -287,7 +426,7 @@ k_mask_head(MaskArgs a) {
     // activations: with them the kernel spilled ~350 registers) | the m_grid
     // level descriptors (read per lane: a select between two kernel-argument
     // descriptors became per-lane loads from the kernarg segment)
-    constexpr uint32_t kRingUsed = 2u * kGroup;
+    constexpr uint32_t kRingUsed = kRing ? (uint32_t)kRing : 2u * kGroup;
     __shared__ uint4 smem[kRingUsed * kStepVec + 4 * kXVec + kDescVec];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int j = lane & 31, h = lane >> 5;
@@ -298,7 +437,12 @@ k_mask_head(MaskArgs a) {
     LevelDesc* const sLv = reinterpret_cast<LevelDesc*>(smem + kRingUsed * kStepVec + 4 * kXVec);
     if (tid < 16) sLv[tid] = a.grid.lv[tid];
 
-    MaskStager st{a.packed, smem, tid, lane, 0u, (uint32_t)kT * kStepsPerSample, {}};
+    const uint4* const pk = a.packed + (size_t)((blockIdx.x >> 3) % kMaskCopies) * kPackVec;
+#if SAMNERF_MASK_RING
+    MaskStagerDma st{pk, smem, tid, lane, wave, 0u, (uint32_t)kT * kStepsPerSample};
+#else
+    MaskStager st{pk, smem, tid, lane, 0u, (uint32_t)kT * kStepsPerSample, {}};
+#endif
     st.begin();
 
     floatx16 sum = {};                                       // sum_k w_k * logits_k
@@ -306,32 +450,43 @@ k_mask_head(MaskArgs a) {
     uint4 a0[kHkb], a1[kHkb];
     // f16x3: log2 scales of the weight tensors (uniform)
     const int kw0 = EXACT ? 0 : a.kexp[0], kw1 = EXACT ? 0 : a.kexp[1], kw2 = EXACT ? 0 : a.kexp[2];
+    // The inputs of a sample: lane half h of k-block kb = m_grid level 2 kb + h
+    // (8 channels), k-block 8 = geo_feat; Xw holds them as fp32 (8 per lane
+    // and k-block, two uint4), split into B operands as each k-block is
+    // consumed (f16x3: at the scale of the column's max |input|, xm).  The 8
+    // levels' loads go out in two batches of 4 (64 rows per lane in flight,
+    // 256 VGPRs -- the accumulators and hidden-layer operands are dead at a
+    // sample's start), two memory round trips per sample where one level at a
+    // time took eight (the m_grid gathers were the largest single stall).
 #pragma unroll 1
     for (int k = 0; k < kT; ++k) {
-        // inputs of sample k.  `ko` is opaque so that the per-sample addresses
-        // are formed here, not carried through the loop as 64-bit induction
-        // pointers
+        // `ko` is opaque so that the per-sample addresses are formed here, not
+        // carried through the loop as 64-bit induction pointers
         uint32_t ko = (uint32_t)k;
         asm volatile("" : "+s"(ko));
         const float* up = a.u_in + (size_t)ko * 3u * N + ss;
         const float ux = up[0], uy = up[N], uz = up[2u * N];
         const float w = live ? a.w_in[(size_t)ko * N + ss] : 0.0f;
-        // the m_grid gathers: lane half h of k-block kb = level 2 kb + h; Xw
-        // holds the fp32 values (8 per lane and k-block, as two uint4), split
-        // into B operands as each k-block is consumed (f16x3: at the scale of
-        // the column's max over all 143 inputs)
         float xm = 0.0f;
-#pragma unroll
-        for (int kb = 0; kb < 8; ++kb) {
-            float f[8];
-            const LevelDesc d = sLv[2 * kb + h];
-            lookup_level3<8>(a.grid.emb, d, ux, uy, uz, f);
+        auto store_level = [&](int kb, const float* f) {
             uint4 xa, xb;
             to_operand<true>(f, 1.0f, xa, xb);
             Xw[(2 * kb) * 64 + lane] = xa;
             Xw[(2 * kb + 1) * 64 + lane] = xb;
 #pragma unroll
             for (int m = 0; m < 8; ++m) xm = fmaxf(xm, fabsf(f[m]));
+        };
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            Gather8 g[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) gather8_issue(a.grid.emb, sLv[2 * (4 * half + i) + h], ux, uy, uz, g[i]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float f[8];
+                gather8_finish(g[i], f);
+                store_level(4 * half + i, f);
+            }
         }
         {
             float g[8];
@@ -339,12 +494,8 @@ k_mask_head(MaskArgs a) {
             for (int m = 0; m < 8; ++m) {
                 const int gi = 8 * h + m;                    // geo_feat index; 15 = padding
                 g[m] = gi < 15 ? a.geo_in[((size_t)ko * 16u + gi + 1) * N + ss] : 0.0f;
-                xm = fmaxf(xm, fabsf(g[m]));
             }
-            uint4 xa, xb;
-            to_operand<true>(g, 1.0f, xa, xb);
-            Xw[16 * 64 + lane] = xa;
-            Xw[17 * 64 + lane] = xb;
+            store_level(8, g);
         }
         const int k0 = EXACT ? 0 : scale_exp_of_max(fmaxf(xm, __shfl_xor(xm, 32)));
         const float s0 = EXACT ? 1.0f : exp2i(k0);
@@ -388,7 +539,7 @@ k_mask_head(MaskArgs a) {
 
 namespace samnerf {
 
-size_t mask_head_packed_floats() { return (size_t)kStepsPerSample * kStepVec * 4 + 4; }
+size_t mask_head_packed_floats() { return (size_t)kMaskCopies * kPackVec * 4 + 4; }
 
 int mask_head_forward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
                       const float* geo_f, uint32_t N, float* out, RayTiles tiles, float* packed,
@@ -404,7 +555,7 @@ int mask_head_forward(const samnerf_model* m, const GridDesc<16>& grid, const fl
     a.K = m->mask_out;
     a.tiles = tiles;
     a.packed = pk;
-    a.kexp = reinterpret_cast<const int*>(pk + (size_t)kStepsPerSample * kStepVec);
+    a.kexp = reinterpret_cast<const int*>(pk + (size_t)kMaskCopies * kPackVec);
     a.out = out;
     if (m->head_mode == 1) {
         k_mask_pack_f32<<<div_up(nfrag, 256), 256, 0, s>>>(m->mask_w[0], m->mask_w[1], m->mask_w[2],

@@ -34,16 +34,6 @@
 
 using namespace samnerf;
 
-// Diagnostic build knobs (tools/diag/build_variant.sh), defaults = product:
-// the k-block k_final prefetches across samples and whether that prefetch may
-// use the dense pair loads.
-#ifndef SAMNERF_DIAG_KPRE
-#define SAMNERF_DIAG_KPRE 1
-#endif
-#ifndef SAMNERF_DIAG_PF_PAIRS
-#define SAMNERF_DIAG_PF_PAIRS 0
-#endif
-
 namespace samnerf {
 int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, float* samvit,
                      float* packed, hipStream_t s, uint32_t ld = 256u);
@@ -884,8 +874,8 @@ __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const Leve
 #ifndef SAMNERF_DIAG_FINAL_WAVES
 #define SAMNERF_DIAG_FINAL_WAVES 3
 #endif
-template <int S_, bool PF_, bool PLAIN_ = true>
-constexpr int final_waves() { return (S_ == 1 && !PF_ && PLAIN_) ? SAMNERF_DIAG_FINAL_WAVES : 2; }
+template <int S_, bool PLAIN_ = true>
+constexpr int final_waves() { return (S_ == 1 && PLAIN_) ? SAMNERF_DIAG_FINAL_WAVES : 2; }
 
 // EXIT: the N1 early-exit form, its own instantiation at 2 waves per SIMD:
 // the exit in the sample loop raised the 3-wave form's spills from 10 to 22
@@ -899,15 +889,15 @@ constexpr int final_waves() { return (S_ == 1 && !PF_ && PLAIN_) ? SAMNERF_DIAG_
 // weighted sums of the grid features and the grid_mlp (and, SA, view_mlp)
 // intermediates, then instance_mask_logits = E . sums (the head is linear).
 // The EXIT / GEO / SA forms run at 2 waves per SIMD, the AD forms at 1.
-template <int S_, bool PF_, bool PLAIN_, int AD_>
-constexpr int final_waves_of() { return AD_ ? 1 : final_waves<S_, PF_, PLAIN_>(); }
+template <int S_, bool PLAIN_, int AD_>
+constexpr int final_waves_of() { return AD_ ? 1 : final_waves<S_, PLAIN_>(); }
 
-template <int T, int S, bool PF, bool EXACT, bool EXIT = false, bool GEO = false, bool SA = false, int AD = 0>
+template <int T, int S, bool EXACT, bool EXIT = false, bool GEO = false, bool SA = false, int AD = 0>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(final_waves_of<S, PF, !EXIT && !GEO && !SA, AD>(),
-                                   final_waves_of<S, PF, !EXIT && !GEO && !SA, AD>())))
+__attribute__((amdgpu_waves_per_eu(final_waves_of<S, !EXIT && !GEO && !SA, AD>(),
+                                   final_waves_of<S, !EXIT && !GEO && !SA, AD>())))
 k_final(FinalArgs a) {
-    static_assert(AD == 0 || (S == 1 && !PF), "adaptive mask forms: one segment, no prefetch");
+    static_assert(AD == 0 || S == 1, "adaptive mask forms: one segment");
     static_assert(AD != 2 || SA, "the 'rgb' adaptive head reads the per-sample view MLP (sum_after_mlp)");
     static_assert(S == 1 || S == 2 || S == 4, "segments per ray");
     static_assert(kXSteps * 64 == 2 * kFSlots * 64 * 4, "exact weights reuse the f16x3 slots");
@@ -994,8 +984,6 @@ k_final(FinalArgs a) {
         for (int q = 0; q < 16; ++q) v1acc[q] = v2acc[q] = 0.0f;
     }
 
-    // PF: the first k-block's gathers of sample i + 1 are issued before the
-    // layer-2/3 MFMAs of sample i, so their latency hides behind them
     // level descriptors of k-block kb for this half-wave (LDS reads,
     // re-evaluated where used rather than held in VGPRs)
     auto levels = [&](int kb, LevelDesc* dl) {
@@ -1004,22 +992,6 @@ k_final(FinalArgs a) {
     };
     // wave-uniform slot classes (kernel arguments)
     auto kinds = [&](int kb) { return SlotKinds{a.kdense[kb], a.khashed[kb]}; };
-    // PF prefetches k-block kPre = 1 (levels 8-15: hashed in every grid of
-    // the path) and gathers k-block 0 -- which holds the dense levels and
-    // their pair loads -- inside the iteration.  Both forms accumulate layer 1
-    // in the order kPre, 1 - kPre: PF on and off give identical bits.
-    // Prefetching k-block 0 with its pair loads (tools/diag/build_variant.sh
-    // -DSAMNERF_DIAG_KPRE=0 -DSAMNERF_DIAG_PF_PAIRS=1) was nondeterministic in
-    // round 1 while the level descriptors came from per-lane vector loads of
-    // a workspace table; with the descriptors in LDS it is deterministic and
-    // bit-identical to PF off, but 2.4 % slower (0.847 vs 0.827 ms), so
-    // kPre = 1 stays.
-    constexpr int kPre = SAMNERF_DIAG_KPRE;
-    auto pf_kinds = [&](int kb) {
-        SlotKinds k = kinds(kb);
-        if (!SAMNERF_DIAG_PF_PAIRS) k.dense = 0u;
-        return k;
-    };
     // rb_prev of sample i is rb_next of sample i - 1 when S == 1 (same bits;
     // saves a division), recomputed from the bins otherwise
     // the sample's position from its two raw bins (b0 read only when S > 1:
@@ -1046,35 +1018,21 @@ k_final(FinalArgs a) {
         position_of(i, S > 1 ? a.bins_in[(size_t)k * N + rr] : 0.0f, a.bins_in[(size_t)(k + 1) * N + rr], rbp,
                     rbn, ux, uy, uz);
     };
-    // not PF: the next sample's raw bins are loaded one sample ahead, so the
-    // gathers of a sample start without a dependent global load in front
-    // (the load of sample i + 1's bins is in flight behind sample i's work)
+    // the next sample's raw bins are loaded one sample ahead, so the gathers
+    // of a sample start without a dependent global load in front (the load
+    // of sample i + 1's bins is in flight behind sample i's work)
     float nb0 = 0.0f, nb1 = 0.0f;
-    if constexpr (!PF) {
+    {
         const int kb0 = i_begin * S + seg;
         if (S > 1) nb0 = a.bins_in[(size_t)kb0 * N + rr];
         nb1 = a.bins_in[(size_t)(kb0 + 1) * N + rr];
-    }
-    GatherC2<4> pre;                                      // PF: kb kPre of the current sample
-    float p_rbp = rb_prev, p_rbn = 0.0f, p_ux = 0.0f, p_uy = 0.0f, p_uz = 0.0f;
-    if constexpr (PF) {
-        LevelDesc dl[4];
-        levels(kPre, dl);
-        position(0, p_rbp, p_rbn, p_ux, p_uy, p_uz);
-        gather_issue_c2<4>(emb, dl, p_ux, p_uy, p_uz, pre, pf_kinds(kPre));
     }
 
     int exit_at = i_end;                                  // EXIT: first step not marched
     for (int i = i_begin; i < i_end; ++i) {
         const int k = i * S + seg;
         float rb_next, ux, uy, uz;
-        if constexpr (PF) {
-            rb_prev = p_rbp;
-            rb_next = p_rbn;
-            ux = p_ux;
-            uy = p_uy;
-            uz = p_uz;
-        } else {
+        {
             const float b0 = nb0, b1 = nb1;
             if (i + 1 < i_end) {
                 const int kn = (i + 1) * S + seg;
@@ -1107,11 +1065,11 @@ k_final(FinalArgs a) {
         int k1 = 0, e_h1 = 0, e_h2 = 0;
 #pragma unroll
         for (int kbi = 0; kbi < 2; ++kbi) {
-            const int kb = kbi == 0 ? kPre : 1 - kPre;
+            // k-block 1 (levels 8-15) first, then 0: the accumulation order
+            // of every round (a cross-sample prefetch of k-block 1 set it)
+            const int kb = 1 - kbi;
             float f[8];
-            if (PF && kbi == 0) {
-                gather_finish_c2<4, S == 1>(pre, f);
-            } else {
+            {
                 LevelDesc dl[4];
                 levels(kb, dl);
                 // parity taps: this half-wave's levels 8 kb + hh + 2 q of the sample
@@ -1155,15 +1113,6 @@ k_final(FinalArgs a) {
             }
         }
         if constexpr (!EXACT) e_h1 = k1 + ke0;
-        if constexpr (PF) {
-            if (i + 1 < TS) {
-                LevelDesc dl[4];
-                levels(kPre, dl);
-                p_rbp = p_rbn;                            // S == 1: next rb_prev = this rb_next
-                position(i + 1, p_rbp, p_rbn, p_ux, p_uy, p_uz);
-                gather_issue_c2<4>(emb, dl, p_ux, p_uy, p_uz, pre, pf_kinds(kPre));
-            }
-        }
         float s2 = 1.0f;
         if constexpr (!EXACT) {                          // max of relu(h1): the raw max, floored at 0
             int mb = 0;                                  // max of relu(h1) on the float bits
@@ -1650,39 +1599,28 @@ k_sgrid_box4(SgridArgs a) {
             const bool ordered = wave_positions_ordered(ux, uy, uz);
             uint32_t p0, p1, p2;
             pbox_lane(mine, ur, p0, p1, p2);
-            // the boxes that fit one slice (in level order, kBoxSlots slots in
-            // all) are staged in ONE pass of LDS DMA -- every row in flight at
-            // once, one memory round trip for the 4 levels -- and read from
-            // LDS; a level whose box does not fit gathers directly
-            PBox bb[4];
-            uint32_t boff[4], btot = 0u, staged = 0u;
+            // per level: the box's rows staged through registers into the
+            // wave's slice, then every lane's 8 corners read from LDS; a box
+            // over kBoxSlots slots gathers directly.  (Round 4 measured a
+            // one-pass form -- the 4 boxes by LDS DMA into the one slice, one
+            // memory round trip per sample, a level whose box did not fit
+            // beside the others gathering directly -- at 0.86 against 0.665 ms
+            // per view, interleaved A/B of whole builds.)
 #pragma unroll
             for (int l = 0; l < 4; ++l) {
-                bb[l] = pbox_read(p0, p1, p2, l);
-                boff[l] = btot;
-                if (btot + bb[l].slots <= kBoxSlots) {
-                    btot += bb[l].slots;
-                    staged |= 1u << l;
-                } else {
-                    bb[l].slots = 0u;                       // not staged: no slots in the slice
-                }
-            }
-            wave_lds_sync();                                // the previous sample's reads done
-            stage_pbox4_dma(base, L, bb, boff, btot, (uint32_t)reinterpret_cast<uintptr_t>(slice), lane);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the DMA (and the prefetch) landed
-            wave_lds_sync();
-            const char* sc = reinterpret_cast<const char*>(slice);
-#pragma unroll
-            for (int l = 0; l < 4; ++l) {
+                const PBox b = pbox_read(p0, p1, p2, l);
                 float f[8];
                 uint32_t* rt = nullptr;                     // parity taps only
                 if (TAP && live && r % a.tap_stride == 0u)
                     rt = a.rows_tap + ((size_t)(r / a.tap_stride) * T + k) * 128u + (4 * g + l) * 8;
-                if ((staged >> l) & 1u) {
+                if (b.slots <= kBoxSlots) {
+                    wave_lds_sync();                        // previous level's reads done
+                    stage_pbox<8>(base, L[l], b, slice, lane);
+                    wave_lds_sync();
                     if (ordered)
-                        lookup_level3_pbox8_dma<false>(a.grid.emb, L[l], bb[l], sc, boff[l], ux, uy, uz, f, rt);
+                        lookup_level3_pbox<8, false>(a.grid.emb, L[l], b, slice, ux, uy, uz, f, rt);
                     else
-                        lookup_level3_pbox8_dma<true>(a.grid.emb, L[l], bb[l], sc, boff[l], ux, uy, uz, f, rt);
+                        lookup_level3_pbox<8, true>(a.grid.emb, L[l], b, slice, ux, uy, uz, f, rt);
                 } else {
                     if (rt) tap_direct_rows<8>(L[l], ux, uy, uz, rt);
                     lookup_level3<8>(a.grid.emb, L[l], ux, uy, uz, f);
@@ -2050,23 +1988,20 @@ void mark_stage(uint32_t i, hipStream_t s) {
 // Below 32,768 rays (not measured) the direct form stays.
 constexpr uint32_t kBox4MinRays = 32768;
 
-// k_final's cross-sample prefetch of one k-block's gathers: off by default
-// since round 2 -- for S = 1 three waves per SIMD without it beat two with it
-// (0.797 vs 0.826 ms per view, see final_waves); for S = 2 / 4 (one rank's
-// share) the prefetching forms spill once the slot-class paths are in (at
-// 32,768 rays 0.260 ms without it vs 0.288 with it).  SAMNERF_FINAL_PF = 0 | 1
-// forces it off / on (the bit-identity tests run both).
+// k_final's cross-sample prefetch of k-block 1's gathers (rounds 1-3, a
+// diagnostic form only since round 2: for S = 1 three waves per SIMD without
+// it beat two with it, 0.797 vs 0.826 ms per view; for S = 2 / 4 it spilled,
+// 0.288 vs 0.260 ms at 32,768 rays) was removed in round 4: its f16x3 forms
+// rendered one sample of one 16-lane group differently in about one launch in
+// four, mostly the first of a process (|d sigma| up to 7e-3 relative; the
+// exact-fp32 prefetch form and every product form bit-stable over the same
+// runs; not traced to a cause -- tools/pf_diag.py).
 // k_final's wave-uniform slot paths (dense pair loads, select-free hashed
 // rows): on by default; SAMNERF_FINAL_CLASSES=0 takes the lane-varying form
 // everywhere (same bits: the A/B parity test).
 uint32_t final_classes() {
     const char* v = diag_env("SAMNERF_FINAL_CLASSES");
     return (v && atoi(v) == 0) ? 0u : 1u;
-}
-
-bool final_prefetch(int seg) {
-    const char* v = diag_env("SAMNERF_FINAL_PF");
-    return v ? atoi(v) != 0 : false;
 }
 
 // k_sgrid_box4 packs cell indices and extents into 10 bits
@@ -2206,18 +2141,18 @@ inline int n1_chunks() {
 
 template <bool EXACT, bool EXIT, bool GEO, bool SA>
 void launch_final_np(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa) {
-    if (seg == 1) k_final<32, 1, false, EXACT, EXIT, GEO, SA><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
-    else if (seg == 2) k_final<32, 2, false, EXACT, EXIT, GEO, SA><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
-    else k_final<32, 4, false, EXACT, EXIT, GEO, SA><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
+    if (seg == 1) k_final<32, 1, EXACT, EXIT, GEO, SA><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
+    else if (seg == 2) k_final<32, 2, EXACT, EXIT, GEO, SA><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
+    else k_final<32, 4, EXACT, EXIT, GEO, SA><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
 }
 
 template <bool EXACT>
-void launch_final(int seg, bool pf, uint32_t N, hipStream_t s, const FinalArgs& fa, bool sa, int ad) {
+void launch_final(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa, bool sa, int ad) {
     if (ad) {                                            // adaptive mask heads: S = 1
         const uint32_t nb = xcd_blocks(div_up(N, 128));
-        if (ad == 2) k_final<32, 1, false, EXACT, false, false, true, 2><<<nb, 256, 0, s>>>(fa);
-        else if (sa) k_final<32, 1, false, EXACT, false, false, true, 1><<<nb, 256, 0, s>>>(fa);
-        else k_final<32, 1, false, EXACT, false, false, false, 1><<<nb, 256, 0, s>>>(fa);
+        if (ad == 2) k_final<32, 1, EXACT, false, false, true, 2><<<nb, 256, 0, s>>>(fa);
+        else if (sa) k_final<32, 1, EXACT, false, false, true, 1><<<nb, 256, 0, s>>>(fa);
+        else k_final<32, 1, EXACT, false, false, false, 1><<<nb, 256, 0, s>>>(fa);
         return;
     }
     if (sa) {                                            // --sum_after_mlp (RGB / mask models)
@@ -2251,16 +2186,9 @@ void launch_final(int seg, bool pf, uint32_t N, hipStream_t s, const FinalArgs& 
         }
         return;
     }
-    if (seg == 1) {
-        if (pf) k_final<32, 1, true, EXACT><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
-        else k_final<32, 1, false, EXACT><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
-    } else if (seg == 2) {
-        if (pf) k_final<32, 2, true, EXACT><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
-        else k_final<32, 2, false, EXACT><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
-    } else {
-        if (pf) k_final<32, 4, true, EXACT><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
-        else k_final<32, 4, false, EXACT><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
-    }
+    if (seg == 1) k_final<32, 1, EXACT><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
+    else if (seg == 2) k_final<32, 2, EXACT><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
+    else k_final<32, 4, EXACT><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
 }
 
 Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
@@ -2678,17 +2606,16 @@ int render_impl(const samnerf_model* m, const float* rays_o, const float* rays_d
     const bool n1_passes = m->t_thresh > 0.0f && n1_chunks() > 1;
     const int seg = fs ? atoi(fs) : (n1_passes || N >= 65536u ? 1 : N >= 32768u ? 2 : 4);
     fa.i1 = 32 / seg;
-    const bool pf = final_prefetch(seg);
     if (m->sum_after_mlp && (m->t_thresh > 0.0f || sam_rows))
         return fail(SAMNERF_EINVAL, "render_forward: sum_after_mlp renders RGB (+ mask) only: no SAM "
                     "features (the reference's branch crashes, SURVEY 0.2) and no t_thresh");
     if (m->head_mode == 1) {
-        launch_final<true>(seg, pf, N, s, fa, m->sum_after_mlp != 0, ad);
+        launch_final<true>(seg, N, s, fa, m->sum_after_mlp != 0, ad);
     } else {
         fa.gpack = w.gpack;
         fa.gexp = w.gexp;
         k_pack_grid_mlp<<<1, 256, 0, s>>>(fa, w.gpack, w.gexp);
-        launch_final<false>(seg, pf, N, s, fa, m->sum_after_mlp != 0, ad);
+        launch_final<false>(seg, N, s, fa, m->sum_after_mlp != 0, ad);
     }
 
     if (sam_rows) {

@@ -255,6 +255,18 @@ constexpr int kSteps = segBase(6);            // 86
 constexpr int kStepVec = 2 * 8 * 64;          // uint4 per step: [hi/lo][tile][lane]
 constexpr int kRaysV5 = 128;                  // 4 waves x 32 rays
 constexpr int kPackedVec = kSteps * kStepVec; // uint4 of fragments; then kexp [5] ints
+// Copies of the packed fragments: every workgroup streams the same 16 KiB
+// step at about the same time, so with one copy the whole chip's requests for
+// a step land on the few L2 channels that hold it; workgroup b reads copy
+// (b >> 3) % kHeadCopies (b & 7 is its XCD), spreading each XCD's requests
+// over kHeadCopies x as many channels.  The copies hold the same bits.
+// Measured (round 4, interleaved A/B of whole builds, 512^2 view): 8 copies
+// 0.569 ms per head launch against 0.566 with one -- the step stream is not
+// channel-bound -- so the product keeps one (the switch stays for A/B builds).
+#ifndef SAMNERF_HEAD_COPIES
+#define SAMNERF_HEAD_COPIES 1
+#endif
+constexpr int kHeadCopies = SAMNERF_HEAD_COPIES;
 
 __device__ __forceinline__ int rho(int q) { return (q & 3) + 8 * (q >> 2); }
 __device__ __forceinline__ int hidden_unit(int kb, int h, int m) {
@@ -332,8 +344,11 @@ __global__ void __launch_bounds__(256) k_pack_h16(PackArgs a) {
     for (int e = 0; e < 8; ++e) v[e] = seg_weight(a.W, seg, kb, h, e, unit);
     uint4 hi, lo;
     split8_f16(v, exp2i(kx), hi, lo);
-    a.packed[(size_t)step * kStepVec + tile * 64 + lane] = hi;
-    a.packed[(size_t)step * kStepVec + 512 + tile * 64 + lane] = lo;
+#pragma unroll
+    for (int c = 0; c < kHeadCopies; ++c) {
+        a.packed[(size_t)c * kPackedVec + (size_t)step * kStepVec + tile * 64 + lane] = hi;
+        a.packed[(size_t)c * kPackedVec + (size_t)step * kStepVec + 512 + tile * 64 + lane] = lo;
+    }
 }
 
 struct HeadArgsH {
@@ -830,7 +845,7 @@ k_sam_head_h16q(HeadArgsH a, uint32_t ntiles) {
     Bs[6 * 256 + tid] = a.ln_b[tid];
 
     HeadStreamQ<NBUF> st;
-    st.packed = a.packed;
+    st.packed = a.packed + (size_t)((blockIdx.x >> 3) % kHeadCopies) * kPackedVec;
     st.Wb = Wb;
     st.rows = reinterpret_cast<const char*>(a.rows);
     st.rows_end = st.rows + (size_t)a.N * kRowIn * 4 - 16;
@@ -1278,7 +1293,7 @@ static int device_cus() {
 
 size_t sam_head_packed_floats() {
     const size_t f32 = (size_t)8 * kTotalGroups * 64 * 4;
-    const size_t h16 = (size_t)kPackedVec * 4 + 8 + 5 * kWmaxParts;   // fragments, log2 scales, partial maxima
+    const size_t h16 = (size_t)kPackedVec * 4 * kHeadCopies + 8 + 5 * kWmaxParts;   // fragment copies, log2 scales, partial maxima
     return f32 > h16 ? f32 : h16;
 }
 
@@ -1289,8 +1304,8 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         PackArgs p;
         for (int i = 0; i < 5; ++i) p.W[i] = m->sam_w[i];
         p.packed = reinterpret_cast<uint4*>(packed);
-        p.kexp = reinterpret_cast<int*>(packed + (size_t)kPackedVec * 4);
-        p.part = packed + (size_t)kPackedVec * 4 + 8;
+        p.kexp = reinterpret_cast<int*>(packed + (size_t)kPackedVec * 4 * kHeadCopies);
+        p.part = packed + (size_t)kPackedVec * 4 * kHeadCopies + 8;
         k_head_wmax<<<dim3(kWmaxParts, 5), 256, 0, s>>>(p);
         k_pack_h16<<<div_up((uint32_t)kSteps * 8u * 64u, 256), 256, 0, s>>>(p);
         HeadArgsH a;

@@ -325,126 +325,4 @@ __device__ __forceinline__ void lookup_level3_pbox(const float* __restrict__ emb
     }
 }
 
-// ---- 4-level boxes staged by LDS DMA (C = 8 rows of 32 B) --------------
-// The boxes of a wave's 4 levels go into one slice, level l's slots from slot
-// offset off[l] (total = off[3] + b[3].slots <= 256), in ONE pass: lane j of
-// slot group q loads the row of slot 64 q + j straight into LDS with two
-// global_load_lds_dwordx4 (no VGPRs: every row of the pass is in flight at
-// once, where staging through registers spilled -- 336 B of scratch at 4
-// waves per SIMD -- and the per-level passes cost a memory round trip each).
-// DMA layout: each instruction writes 64 lanes x 16 B contiguously, so slot s
-// keeps its two 16-B halves at byte (s >> 6) * 2048 + h * 1024 + (s & 63) * 16
-// of the slice.  Padding slots (outside the box's x / y extents) are not
-// loaded and never read.  The caller waits for the DMA (s_waitcnt vmcnt(0),
-// counted by hand: the compiler does not see inline-asm loads) before reading.
-__device__ __forceinline__ uint32_t dma_slot_byte(uint32_t s) { return ((s >> 6) << 11) + ((s & 63u) << 4); }
-
-__device__ __forceinline__ void lds_dma16_wave(const void* src, uint32_t lds_byte_addr) {
-    const uint32_t d = __builtin_amdgcn_readfirstlane(lds_byte_addr);
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(src), "s"(d)
-        : "memory");
-}
-
-__device__ __forceinline__ void stage_pbox4_dma(const char* __restrict__ base, const LevelDesc* L, const PBox* b,
-                                                const uint32_t* off, uint32_t total, uint32_t slice_lds,
-                                                uint32_t lane) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // the slice's previous reads are done
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        if (64u * (uint32_t)it >= total) break;           // wave-uniform
-        const uint32_t j = lane + 64u * (uint32_t)it;
-        // the level of slot j: wave-uniform box fields selected per lane
-        // (field by field, by value: selecting a reference into b[] or L[]
-        // would index a private array -- scratch memory)
-        const int l = j >= off[3] ? 3 : j >= off[2] ? 2 : j >= off[1] ? 1 : 0;
-#define SAMNERF_SEL4(A, F) (l == 3 ? A[3].F : l == 2 ? A[2].F : l == 1 ? A[1].F : A[0].F)
-        const uint32_t jj = j - (l == 3 ? off[3] : l == 2 ? off[2] : l == 1 ? off[1] : 0u);
-        const uint32_t lx = SAMNERF_SEL4(b, lx), ly = SAMNERF_SEL4(b, ly);
-        const uint32_t bx = jj & ((1u << lx) - 1u), t = jj >> lx, by = t & ((1u << ly) - 1u), bz = t >> ly;
-        if (j < total && bx < SAMNERF_SEL4(b, ex) && by < SAMNERF_SEL4(b, ey)) {
-            const LevelDesc d{SAMNERF_SEL4(L, off), SAMNERF_SEL4(L, size), SAMNERF_SEL4(L, res),
-                              SAMNERF_SEL4(L, flags), 0.0f, 0.0f};
-            const uint32_t row = dense_or_hash_row(SAMNERF_SEL4(b, x0) + bx, SAMNERF_SEL4(b, y0) + by,
-                                                   SAMNERF_SEL4(b, z0) + bz, d);
-#undef SAMNERF_SEL4
-            const char* src = base + (d.off + row) * 32u;
-            lds_dma16_wave(src, slice_lds + (uint32_t)it * 2048u);
-            lds_dma16_wave(src + 16, slice_lds + (uint32_t)it * 2048u + 1024u);
-        }
-    }
-}
-
-// lookup_level3<8> from a DMA-staged slice (the level's slots from slot
-// offset `sbase`): the rows, weights and FMA order of lookup_level3_pbox, so
-// the same bits.  tap (parity taps only): the row of each corner's slot.
-template <bool CHECK = true>
-__device__ __forceinline__ void lookup_level3_pbox8_dma(const float* __restrict__ emb, const LevelDesc& d,
-                                                        const PBox& b, const char* slice, uint32_t sbase,
-                                                        float ux, float uy, float uz, float* acc,
-                                                        uint32_t* tap = nullptr) {
-    uint32_t cx, cy, cz;
-    float fx, fy, fz;
-    locate_axis(ux, d, cx, fx);
-    locate_axis(uy, d, cy, fy);
-    locate_axis(uz, d, cz, fz);
-    const uint32_t top = d.res - 1u;
-    const uint32_t nx = min(cx + 1u, top), ny = min(cy + 1u, top), nz = min(cz + 1u, top);
-    const uint32_t lx0 = cx - b.x0, lx1 = nx - b.x0;
-    const uint32_t ly0 = cy - b.y0, ly1 = ny - b.y0;
-    const uint32_t lz0 = cz - b.z0, lz1 = nz - b.z0;
-    if constexpr (CHECK) {
-        const bool inside = lx0 < b.ex && lx1 < b.ex && ly0 < b.ey && ly1 < b.ey && lz0 < b.ez && lz1 < b.ez;
-        if (!inside) {
-            if (tap) tap_direct_rows<8>(d, ux, uy, uz, tap);
-            lookup_level3<8>(emb, d, ux, uy, uz, acc);
-            return;
-        }
-    }
-    const uint32_t lxy = b.lx + b.ly;
-    const uint32_t s0 = sbase + lx0 + (ly0 << b.lx) + (lz0 << lxy);
-    const uint32_t DX = lx1 - lx0, DY = (ly1 - ly0) << b.lx, DZ = (lz1 - lz0) << lxy;
-    uint32_t sl[8];
-    sl[0] = s0;
-    sl[1] = s0 + DX;
-    sl[2] = s0 + DY;
-    sl[3] = sl[2] + DX;
-    sl[4] = s0 + DZ;
-    sl[5] = sl[4] + DX;
-    sl[6] = sl[4] + DY;
-    sl[7] = sl[6] + DX;
-    if (tap) {
-        const uint32_t xm = (1u << b.lx) - 1u, ym = (1u << b.ly) - 1u;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const uint32_t j = sl[c] - sbase;
-            tap[c] = dense_or_hash_row(b.x0 + (j & xm), b.y0 + ((j >> b.lx) & ym), b.z0 + (j >> lxy), d);
-        }
-    }
-    f2v wc[4];
-    corner_weights_pk(fx, fy, fz, wc);
-    f2v a[4] = {f2v{0.0f, 0.0f}, f2v{0.0f, 0.0f}, f2v{0.0f, 0.0f}, f2v{0.0f, 0.0f}};
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const float w = corner_w(wc, c);
-        const f2v wv = {w, w};
-        const char* p = slice + dma_slot_byte(sl[c]);
-        const float4 v0 = *reinterpret_cast<const float4*>(p);
-        const float4 v1 = *reinterpret_cast<const float4*>(p + 1024);
-        a[0] = __builtin_elementwise_fma(wv, f2v{v0.x, v0.y}, a[0]);
-        a[1] = __builtin_elementwise_fma(wv, f2v{v0.z, v0.w}, a[1]);
-        a[2] = __builtin_elementwise_fma(wv, f2v{v1.x, v1.y}, a[2]);
-        a[3] = __builtin_elementwise_fma(wv, f2v{v1.z, v1.w}, a[3]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        acc[2 * i] = a[i].x;
-        acc[2 * i + 1] = a[i].y;
-    }
-}
-
 }  // namespace samnerf

@@ -382,30 +382,6 @@ def test_sam_feature_handoff_stays_on_device(hip_lib, cuda):
     assert orig.tolist() == [[256, 256]] and masks.shape == (1, 512, 512)
 
 
-@pytest.mark.parametrize("head_mode", [0, 1])
-@pytest.mark.parametrize("n", [70000, 40000, 9000])
-def test_final_prefetch_bit_identical(hip_lib, cuda, monkeypatch, n, head_mode, diag):
-    """k_final with and without the cross-sample prefetch of its first
-    k-block's gathers (SAMNERF_FINAL_PF), for each ray-segment form S = 1, 2,
-    4 (chosen by N): identical bits."""
-    from samnerf_amd import ops
-    from samnerf_amd.fused import FusedRenderer, ROW
-    spec = synth.ModelSpec(with_sam=True)
-    net = make_net(spec, synth.make_params(spec, seed=23, emb_scale=0.5, ln_jitter=0.1), cuda)
-    pose, intr = synth.gui_camera(512, 160, rot=synth.random_rotation(11))
-    ro, rd = ops.get_rays(pose, intr, 160, 512, device=cuda)
-    fr = FusedRenderer(net, head_mode=head_mode)
-    outs = []
-    for pf in ("0", "1"):
-        monkeypatch.setenv("SAMNERF_FINAL_PF", pf)
-        rows = torch.empty(n, ROW, device=cuda)
-        o = fr.render(ro[:n], rd[:n], rows=rows)
-        o["rows"] = rows
-        outs.append(o)
-    for k in outs[0]:
-        assert torch.equal(outs[0][k], outs[1][k]), k
-
-
 def test_render_without_features_matches(hip_lib, cuda):
     """return_feats=0 skips the s_grid composite and the head (the reference
     computes and drops them); the RGB outputs are the same bits."""
@@ -448,7 +424,7 @@ def test_final_slot_classes_bit_identical(hip_lib, cuda, monkeypatch, n, diag):
     pair on dense levels (with the top-cell weight swap) and select-free
     hashed rows -- against the lane-varying form (SAMNERF_FINAL_CLASSES=0):
     identical bits, on a view whose far samples reach the top cells of the
-    coarse levels, with PF on and off."""
+    coarse levels."""
     from samnerf_amd import ops
     from samnerf_amd.fused import FusedRenderer, ROW
     spec = synth.ModelSpec(with_sam=True)
@@ -456,17 +432,15 @@ def test_final_slot_classes_bit_identical(hip_lib, cuda, monkeypatch, n, diag):
     pose, intr = synth.gui_camera(512, 160, rot=synth.random_rotation(17))
     ro, rd = ops.get_rays(pose, intr, 160, 512, device=cuda)
     fr = FusedRenderer(net)
-    for pf in ("0", "1"):
-        monkeypatch.setenv("SAMNERF_FINAL_PF", pf)
-        outs = []
-        for cl in ("0", "1"):
-            monkeypatch.setenv("SAMNERF_FINAL_CLASSES", cl)
-            rows = torch.empty(n, ROW, device=cuda)
-            o = fr.render(ro[:n], rd[:n], rows=rows)
-            o["rows"] = rows
-            outs.append(o)
-        for k in outs[0]:
-            assert torch.equal(outs[0][k], outs[1][k]), (pf, k)
+    outs = []
+    for cl in ("0", "1"):
+        monkeypatch.setenv("SAMNERF_FINAL_CLASSES", cl)
+        rows = torch.empty(n, ROW, device=cuda)
+        o = fr.render(ro[:n], rd[:n], rows=rows)
+        o["rows"] = rows
+        outs.append(o)
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
 
 
 def test_fused_render_from_reference_layout_checkpoint(hip_lib, cuda, tmp_path):
@@ -554,24 +528,24 @@ def test_fused_proposal_kernel_bit_identical(hip_lib, cuda, monkeypatch, diag):
             assert torch.equal(outs[0][k], outs[1][k]), (n, k)
 
 
-def _twice_equal(render):
+def _twice_equal(render, times=2):
     a = {k: v.cpu() for k, v in render().items()}
-    b = {k: v.cpu() for k, v in render().items()}
-    for k in a:
-        assert torch.equal(a[k], b[k]), k
+    for _ in range(times - 1):
+        b = {k: v.cpu() for k, v in render().items()}
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
 
 
 @pytest.mark.parametrize("seg", ["1", "2", "4"])
-@pytest.mark.parametrize("pf", ["0", "1"])
 @pytest.mark.parametrize("head_mode", [0, 1])
-def test_final_forms_deterministic(hip_lib, cuda, monkeypatch, seg, pf, head_mode, diag):
-    """Every k_final form renders the same bits twice (a forward
-    whose output varies run to run has a hazard): S = 1 / 2 / 4, with and
-    without the cross-sample prefetch, both precisions, feature rows on."""
+def test_final_forms_deterministic(hip_lib, cuda, monkeypatch, seg, head_mode, diag):
+    """Every k_final form renders the same bits three times (a
+    forward whose output varies run to run has a hazard; the removed
+    prefetch form differed on the first render of a process): S = 1 / 2 / 4,
+    both precisions, feature rows on."""
     from samnerf_amd import ops
     from samnerf_amd.fused import FusedRenderer, ROW
     monkeypatch.setenv("SAMNERF_FINAL_S", seg)
-    monkeypatch.setenv("SAMNERF_FINAL_PF", pf)
     spec = synth.ModelSpec(with_sam=True)
     net = make_net(spec, synth.make_params(spec, seed=23, emb_scale=0.5, ln_jitter=0.1), cuda)
     pose, intr = synth.gui_camera(512, 80, rot=synth.random_rotation(11))
@@ -583,7 +557,7 @@ def test_final_forms_deterministic(hip_lib, cuda, monkeypatch, seg, pf, head_mod
         o = fr.render(ro, rd, rows=rows, view_width=512)
         o["rows"] = rows.clone()
         return o
-    _twice_equal(render)
+    _twice_equal(render, times=3)
 
 
 @pytest.mark.parametrize("form", ["exit", "mask_default", "sum_after", "adaptive_density", "adaptive_rgb"])

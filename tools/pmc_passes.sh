@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 PMC passes for the rooflines (one counter group per pass,
-# counters only, no tracing domains).  usage (GPU box): bash tools/pmc_passes.sh TAG [bench args]
+# counters only, no tracing domains).  usage (GPU box): [PASSES="i j"] bash tools/pmc_passes.sh TAG [bench args]
 set -o pipefail
 TAG=${1:-r2}; shift
 OUT="$GRAFT_REPO_ROOT/gpurun_out/pmc_$TAG"
@@ -14,8 +14,10 @@ GROUPS_=(
   "TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE"
   "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE"
 )
+# PASSES="4 5": only those groups (default: all)
 i=0
 for g in "${GROUPS_[@]}"; do
+  if [ -n "${PASSES:-}" ] && ! [[ " $PASSES " == *" $i "* ]]; then i=$((i+1)); continue; fi
   timeout -s KILL 150 rocprofv3 --pmc $g --output-format csv -d "$OUT/p$i" -o p$i -- \
     python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --cpu-rays 0 --ref-gpu-rays 0 --no-alt --streams 1 "$@" > "$OUT/p$i.log" 2>&1
   rc=$?; echo "pass $i ($g) rc=$rc"
