@@ -7,9 +7,12 @@ For each stage of the view (the kernels bench.py's stage events bracket) it
 averages every counter over the stage's dispatches and sums the stage's
 kernels, per launch of the view (the profiled bench renders the headline
 512x512 view, 262,144 rays).  bench.py prices its live stage times with these
-(stage_roofline): VALU-issue cycles (SQ_ACTIVE_INST_VALU counts quad-cycles,
-MI355X_MICROARCH.md "s_memtime tick vs SQ PMC units"), MFMA-busy cycles, and
-HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (the guide's gfx950 correction).
+(stage_roofline): issued VALU instructions per ray (SQ_INSTS_VALU, priced at
+the measured 2.25 cycles per instruction, tools/valu_rate.hip -- round 4 found
+SQ_ACTIVE_INST_VALU counting one per simple instruction, not quad-cycles),
+MFMA-busy cycles, the wave-cycle shares (SQ_WAIT_ANY / SQ_WAIT_INST_ANY /
+SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES), and HBM bytes = 2 x FETCH_SIZE +
+WRITE_SIZE (the guide's gfx950 correction).
 Every number is recomputable from the table tools/pmc_table.py prints for the
 same directory (profiles/<tag>_pmc_table.txt).
 """
