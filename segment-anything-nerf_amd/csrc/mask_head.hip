@@ -346,7 +346,18 @@ struct MaskStagerDma {
     }
 };
 
-__device__ __forceinline__ float leaky(float x) { return x < 0.0f ? x * 0.01f : x; }
+// leaky_relu(0.01) as max(x, 0.01 x): the same value for every x (x >= 0,
+// -0.0 included, gives x; x < 0 gives 0.01 x; NaN stays NaN).  The max is a
+// plain v_max_f32: fmaxf on an accumulator (not a known arithmetic result)
+// would add a canonicalising v_max per value, and the compare-and-select form
+// takes three VALU.  The multiply comes first and reads x, so the compiler
+// has already placed x's MFMA-result wait states before the asm reads it.
+__device__ __forceinline__ float leaky(float x) {
+    const float t = x * 0.01f;
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(t));
+    return r;
+}
 
 // leaky_relu on the accumulators, then the next layer's B operands (k-block
 // kb = 2t + s <- registers 8s..8s+7 of tile t, hidden_unit order).  f16x3:
