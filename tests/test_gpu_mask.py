@@ -101,6 +101,13 @@ def test_fused_mask_head_matches_unfused_path(hip_lib, cuda, head_mode):
     assert got.shape == (64 * 64, 5)
     assert err < 1e-3 * max(1.0, scale), (err, scale)
     assert torch.equal(got, tiled)
+    # ragged launches: a partial last workgroup (4019 = 31 x 128 + 51 rays) and a
+    # single part-filled one (5 rays) give each ray the bits of the full launch
+    # (a ray's logits depend on that ray only; the weight ring runs regardless)
+    with torch.no_grad():
+        for n in (4019, 5):
+            sub = fr.render(ro[:n], rd[:n], mask=True)["instance_mask_logits"]
+            assert torch.equal(sub, got[:n]), n
 
 
 def test_fused_sum_after_mlp_rgb_matches_unfused(hip_lib, cuda, monkeypatch, diag):
