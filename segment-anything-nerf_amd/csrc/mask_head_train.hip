@@ -45,7 +45,10 @@ constexpr int kT = 32;                        // final samples per ray
 constexpr int kIn0 = 143;                     // 128 m_grid features + 15 geo_feat
 constexpr int kKp[3] = {144, 256, 256};       // padded fan-in per layer
 constexpr int kOp[3] = {256, 256, 32};        // padded fan-out per layer
-constexpr uint32_t kChunk = 1024;             // rows per dW work item
+#ifndef SAMNERF_MT_CHUNK
+#define SAMNERF_MT_CHUNK 1024
+#endif
+constexpr uint32_t kChunk = SAMNERF_MT_CHUNK; // rows per dW work item
 
 __host__ __device__ constexpr int pack_base(int l) {     // floats before layer l (either pack)
     int b = 0;
@@ -282,6 +285,9 @@ __global__ void __launch_bounds__(256) k_mt_bwd(BwdArgs a) {
     // consecutive rows fall in the same cell: a lane keeps adding to its
     // corner row while the row repeats and sends one atomic per run.
     const int c = lane >> 3, ch = lane & 7;
+#ifdef SAMNERF_AB_MT_NOSCATTER   // timing attribution only: no m_grid gradient
+    return;
+#endif
     for (int l = w; l < 16; l += 4) {
         uint32_t run = 0xffffffffu;                           // the lane's current corner row (byte offset)
         float acc = 0.0f;
@@ -351,15 +357,41 @@ __global__ void __launch_bounds__(256) k_mt_dw(DwArgs a) {
     const float* Ga = G + (size_t)(gok ? u : 0) * sv.Rp + c0 + 4 * h;
     const float* Xb = X + (size_t)(xok ? c : 0) * sv.Rp + c0 + 4 * h;
     f32x16 acc = {};
-    for (uint32_t m = 0; m < kChunk / 8u; ++m) {
-        float4 ga = *reinterpret_cast<const float4*>(Ga + 8 * m);
-        float4 xb = *reinterpret_cast<const float4*>(Xb + 8 * m);
-        if (!gok) ga = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (!xok) xb = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.x, xb.x, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.y, xb.y, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.z, xb.z, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.w, xb.w, acc, 0, 0, 0);
+    // the rows in groups of kDwU loop trips, two register buffers in ping-pong
+    // (fp32_chain.h's scheme): a group's loads are in flight while the
+    // previous group's MFMAs run, where one load pair then its four MFMAs
+    // waited for L2 on every trip.  The MFMA order is unchanged.
+    constexpr int kDwU = 2, kDwG = (int)(kChunk / 8u) / kDwU;
+    const float4 zero4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    auto load = [&](float4 (&ga)[kDwU], float4 (&xb)[kDwU], int grp) {
+#pragma unroll
+        for (int u = 0; u < kDwU; ++u) {
+            const int m = grp * kDwU + u;
+            ga[u] = *reinterpret_cast<const float4*>(Ga + 8 * m);   // rows clamped in range:
+            xb[u] = *reinterpret_cast<const float4*>(Xb + 8 * m);   // unconditional loads
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mma = [&](const float4 (&ga)[kDwU], const float4 (&xb)[kDwU]) {
+#pragma unroll
+        for (int u = 0; u < kDwU; ++u) {
+            const float4 g = gok ? ga[u] : zero4, x = xok ? xb[u] : zero4;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(g.x, x.x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(g.y, x.y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(g.z, x.z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(g.w, x.w, acc, 0, 0, 0);
+        }
+    };
+    float4 g0[kDwU], x0[kDwU], g1[kDwU], x1[kDwU];
+    load(g0, x0, 0);
+#pragma unroll 1
+    for (int grp = 0; grp < kDwG; grp += 2) {
+        load(g1, x1, min(grp + 1, kDwG - 1));
+        mma(g0, x0);
+        if (grp + 1 < kDwG) {
+            load(g0, x0, min(grp + 2, kDwG - 1));
+            mma(g1, x1);
+        }
     }
     // acc register q of lane (col i, half h) = dW[32ut + (q & 3) + 8 (q >> 2) + 4h][32kt + i]
     const int lo = logical_out(l, a.K), li = logical_in(l);
