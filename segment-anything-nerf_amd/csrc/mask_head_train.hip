@@ -207,7 +207,32 @@ struct BwdArgs {
     uint32_t K;
     Saved sv;
     float* gemb;             // m_grid embedding gradient (accumulated)
+    float* rep;              // kRep copies of the coarse levels' gradient rows
+    uint32_t rep_levels;     // levels 0 .. rep_levels - 1 scatter into the copies
+    uint32_t rep_floats;     // floats of those levels' rows (one copy)
 };
+
+// The coarse levels' rows are hot: every sample lands in one of a few
+// thousand cells, so their float atomics queue on few addresses (attribution
+// build: levels 0-3 alone cost 0.37 ms of the 3.16 ms training step, levels
+// 4-15 together 0.56).  As the RGB training's scatter (rgb_train.hip kRep),
+// those levels add into kRep copies of their rows, the copy picked by the
+// block's XCD (blocks go to the 8 XCDs round-robin), and k_mt_rep_sum folds
+// the copies into the gradient in a fixed order.  Measured (tools/gpu_r4r.sh,
+// 3 interleaved A/B pairs): 3.16 -> 2.99 ms per 128 x 128 training step; the
+// copies cost 16 MiB of workspace.
+constexpr uint32_t kRep = 8, kRepRows = 65536;          // rows of the replicated levels, at most
+
+// gemb[i] += sum_c rep[c][i] for i < n
+__global__ void __launch_bounds__(256) k_mt_rep_sum(const float* __restrict__ rep, uint32_t n,
+                                                    float* __restrict__ gemb) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    float acc = 0.0f;
+#pragma unroll
+    for (uint32_t c = 0; c < kRep; ++c) acc += rep[(size_t)c * n + i];
+    gemb[i] += acc;
+}
 
 // dx[Kp x 16] = W_l^T g[Op x 16]: output tiles t = w, w + 4, .. of NT (tiles
 // past NT repeat the last and are dropped: the chain stays branch-free)
@@ -289,6 +314,10 @@ __global__ void __launch_bounds__(256) k_mt_bwd(BwdArgs a) {
     return;
 #endif
     for (int l = w; l < 16; l += 4) {
+#ifdef SAMNERF_AB_MT_SCATTER_LEVELS   // timing attribution only: scatter levels [lo, hi) only
+        if (l < (SAMNERF_AB_MT_SCATTER_LEVELS >> 8) || l >= (SAMNERF_AB_MT_SCATTER_LEVELS & 255)) continue;
+#endif
+        float* const tgt = (uint32_t)l < a.rep_levels ? a.rep + (blockIdx.x & (kRep - 1u)) * a.rep_floats : a.gemb;
         uint32_t run = 0xffffffffu;                           // the lane's current corner row (byte offset)
         float acc = 0.0f;
         for (int j = 0; j < kRows; ++j) {
@@ -310,12 +339,12 @@ __global__ void __launch_bounds__(256) k_mt_bwd(BwdArgs a) {
             if (o == run) {
                 acc += v;
             } else {
-                if (run != 0xffffffffu) atomicAdd(a.gemb + run / 4u + ch, acc);
+                if (run != 0xffffffffu) atomicAdd(tgt + run / 4u + ch, acc);
                 run = o;
                 acc = v;
             }
         }
-        if (run != 0xffffffffu) atomicAdd(a.gemb + run / 4u + ch, acc);
+        if (run != 0xffffffffu) atomicAdd(tgt + run / 4u + ch, acc);
     }
 }
 
@@ -405,6 +434,7 @@ __global__ void __launch_bounds__(256) k_mt_dw(DwArgs a) {
 
 struct Layout {
     float *wf, *wb;
+    float* rep;              // kRep x kRepRows x 8 floats (the coarse levels' gradient copies)
     Saved sv;
     size_t bytes;
 };
@@ -426,6 +456,7 @@ Layout carve(uint32_t N, void* base) {
     const size_t Rp = L.sv.Rp;
     L.wf = take(kPackFloats);
     L.wb = take(kPackFloats);
+    L.rep = take((size_t)kRep * kRepRows * 8u);
     L.sv.x = take((size_t)kKp[0] * Rp);
     L.sv.h1 = take((size_t)256 * Rp);
     L.sv.h2 = take((size_t)256 * Rp);
@@ -748,7 +779,16 @@ int mask_train_backward(const samnerf_model* m, const GridDesc<16>& grid, const 
     b.K = mw.K;
     b.sv = L.sv;
     b.gemb = grad_m_grid;
+    // the leading levels whose rows fit kRepRows go through the copies
+    b.rep = L.rep;
+    b.rep_levels = 0u;
+    while (b.rep_levels < 4u && grid.lv[b.rep_levels + 1u].off <= kRepRows) ++b.rep_levels;
+    b.rep_floats = grid.lv[b.rep_levels].off * 8u;
+    if (b.rep_levels &&
+        hipMemsetAsync(L.rep, 0, sizeof(float) * kRep * b.rep_floats, s) != hipSuccess)
+        return fail(SAMNERF_ELAUNCH, "mask_train_backward: zeroing the gradient copies failed");
     k_mt_bwd<<<L.sv.Rp / kRows, 256, 0, s>>>(b);
+    if (b.rep_levels) k_mt_rep_sum<<<div_up(b.rep_floats, 256), 256, 0, s>>>(L.rep, b.rep_floats, grad_m_grid);
     if ((rc = check_launch("mask_train_backward"))) return rc;
     DwArgs d;
     d.sv = L.sv;
