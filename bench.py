@@ -25,6 +25,7 @@ oracle (torch-CPU restatement of the reference renderer + C restatement of its e
 `parity_vs_ref` compares a parity-weight render of the same view with it.
 """
 import argparse
+import hashlib
 import json
 import os
 import subprocess
@@ -324,6 +325,8 @@ def mask_view(dev, steps, warmup, head_mode=0, ref_rays=32768):
             "speedup": (H * W / dt) * dt_ref,
             "max_abs_logits_vs_unfused": err, "dtype": DTYPE[head_mode],
             "ms_without_mask": dt_nomask * 1e3, "mask_head_ms": head_ms,
+            # fingerprint of the full view's logits (bit-identity of A/B builds)
+            "logits_sha16": hashlib.sha256(out["instance_mask_logits"].cpu().numpy().tobytes()).hexdigest()[:16],
             "mask_head_mfma_frac": (head_flop / (head_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFS
                                     if head_mode == 0 and head_ms > 0 else None),
             "what": "--with_mask 'default' head (m_grid L16C8 + SkipConnMLP 143->256->256->2 per sample, "

@@ -15,4 +15,5 @@ import bench  # noqa: E402
 
 r = bench.mask_view(torch.device("cuda", 0), 6, 2, 0, ref_rays=16384)
 print(json.dumps({"ms_per_view": r["ms_per_step"], "rays_per_s": r["value"],
-                  "max_abs_logits_vs_unfused": r["max_abs_logits_vs_unfused"]}))
+                  "max_abs_logits_vs_unfused": r["max_abs_logits_vs_unfused"],
+                  "logits_sha16": r["logits_sha16"]}))
