@@ -199,7 +199,11 @@ typedef struct {
      * Linears on the grid_mlp intermediates, mask_w[0..5] = [96,32] [96,160] [96,160]
      * [96,112] [96,96] [mask_out,96]; 2 = 'adaptive' / 'rgb' (needs sum_after_mlp):
      * eight, also on the view_mlp intermediates, mask_w[0..7] = [96,32] [96,160]
-     * [96,160] [96,112] [96,128] [96,128] [96,96] [mask_out,96]. */
+     * [96,160] [96,112] [96,128] [96,128] [96,96] [mask_out,96].
+     * with_mask = 2: a training render -- the adaptive heads' render also keeps
+     * each ray's weighted input sums (240 floats per ray) in the workspace for
+     * samnerf_mask_train_forward / _backward, which need with_mask = 2 on those
+     * heads; inference renders (1) neither store nor allocate them. */
     int with_mask;
     int mask_kind;
     samnerf_grid m_grid;          /* mask_kind 0 */
@@ -304,6 +308,11 @@ int samnerf_mask_forward(const samnerf_model* model, uint32_t N, float* instance
  * workspace stays alive until the backward).  Batches of 65,536 rays need
  * ~10 GB. */
 size_t samnerf_mask_train_workspace_size(uint32_t N);
+/* The workspace the given mask model needs (what samnerf_mask_train_workspace_size(N)
+ * returns is the maximum over the head kinds): the 'default' head's
+ * activation carve above, or 2 x 7 x 96 floats per ray for the adaptive heads
+ * (mask_kind 1 / 2) -- ~5.4 KB per ray instead of ~157 KB. */
+size_t samnerf_mask_train_workspace_size_model(const samnerf_model* model, uint32_t N);
 int samnerf_mask_train_forward(const samnerf_model* model, uint32_t N, float* instance_mask_logits,
                                const void* render_ws, size_t render_ws_bytes, void* workspace,
                                size_t workspace_bytes, samnerf_stream_t stream);

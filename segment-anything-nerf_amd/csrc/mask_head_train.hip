@@ -48,6 +48,9 @@ constexpr int kOp[3] = {256, 256, 32};        // padded fan-out per layer
 #ifndef SAMNERF_MT_CHUNK
 #define SAMNERF_MT_CHUNK 1024
 #endif
+// dW's work items take the rows of a chunk in groups of 8 x kDwU (kDwU = 2
+// below): a chunk size that is not a multiple of 16 would silently drop rows
+static_assert(SAMNERF_MT_CHUNK % 16 == 0, "SAMNERF_MT_CHUNK must be a multiple of 16 (8 x kDwU)");
 constexpr uint32_t kChunk = SAMNERF_MT_CHUNK; // rows per dW work item
 
 __host__ __device__ constexpr int pack_base(int l) {     // floats before layer l (either pack)
@@ -684,6 +687,12 @@ namespace samnerf {
 
 size_t mask_train_workspace_bytes(uint32_t N) {
     return std::max(carve(N, nullptr).bytes, ad_ws_floats(N) * sizeof(float));
+}
+
+// model-aware: the 'default' head's activation carve (and its
+// per-XCD gradient copies) or the adaptive chain's 2 x 7 x 96 floats per ray
+size_t mask_train_workspace_bytes(int mask_kind, uint32_t N) {
+    return mask_kind == 0 ? carve(N, nullptr).bytes : ad_ws_floats(N) * sizeof(float);
 }
 
 // The adaptive heads (mask_kind 1 / 2): X [N][240] per-ray input sums from the

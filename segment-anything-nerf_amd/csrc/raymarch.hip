@@ -43,6 +43,7 @@ int mask_head_forward(const samnerf_model* m, const GridDesc<16>& grid, const fl
                       hipStream_t s);
 size_t mask_head_packed_floats();
 size_t mask_train_workspace_bytes(uint32_t N);
+size_t mask_train_workspace_bytes(int mask_kind, uint32_t N);
 int mask_train_forward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
                        const float* geo_f, uint32_t N, RayTiles tiles, float* logits, void* ws,
                        size_t ws_bytes, hipStream_t s);
@@ -751,14 +752,20 @@ __device__ __forceinline__ void gather_issue_c2(const float2* __restrict__ emb, 
         } else {
             const bool hashed = d[l].flags & kHashed;
             const uint32_t my = hashed ? kPrime1 : d[l].res, mz = hashed ? kPrime2 : d[l].res * d[l].res;
-            const uint32_t mask = hashed ? d[l].size - 1u : 0xffffffffu;
+            // per-lane choice between the hashed and the dense row as a bitwise
+            // blend on an opaque all-ones / zero mask: written as a select the
+            // compiler turned each of the 8 corners into a divergent
+            // exec-masked branch pair
+            uint32_t hsel = hashed ? 0xffffffffu : 0u;
+            asm volatile("" : "+v"(hsel));
+            const uint32_t hmask = hsel & (d[l].size - 1u), dmask = ~hsel;
             const uint32_t X[2] = {cx, min(cx + 1u, top)};
             const uint32_t Y[2] = {cy * my, ny * my};
             const uint32_t Z[2] = {cz * mz, nz * mz};
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
                 const uint32_t xs = X[c & 1], ys = Y[(c >> 1) & 1], zs = Z[c >> 2];
-                row[l][c] = (d[l].off + (hashed ? ((xs ^ ys ^ zs) & mask) : (xs + ys + zs))) << 3;
+                row[l][c] = (d[l].off + (((xs ^ ys ^ zs) & hmask) | ((xs + ys + zs) & dmask))) << 3;
             }
         }
     }
@@ -892,7 +899,24 @@ constexpr int final_waves() { return (S_ == 1 && PLAIN_) ? SAMNERF_DIAG_FINAL_WA
 template <int S_, bool PLAIN_, int AD_>
 constexpr int final_waves_of() { return AD_ ? 1 : final_waves<S_, PLAIN_>(); }
 
-template <int T, int S, bool EXACT, bool EXIT = false, bool GEO = false, bool SA = false, int AD = 0>
+// LAY: the main grid's level layout as the kernel sees it.
+//   0  run time: slot classes from the kernel arguments (kdense / khashed),
+//      the grid scale's division / multiplication picked per call;
+//   1  the reference architecture's grid (network.py:82-86: L16 C2, 2^19
+//      rows per level, base resolution 16 -> levels 0-4 dense, 5-15 hashed)
+//      with a power-of-two grid scale: k-block 0's slots are dense, dense,
+//      mixed, hashed, k-block 1's all hashed -- compile-time constants, so the
+//      sample loop is straight-line code (no per-slot uniform branches for the
+//      scheduler to stop at, no per-slot selects) and the grid scale is one
+//      multiply.  The host picks 1 when the model's descriptors match
+//      (final_layout), else 0; both give the same bits.
+// TAP: the parity-tap stores (sigma of every sample, the corner rows) are
+// compiled in.  Product renders run TAP = false: the tap address arithmetic
+// and its branches are not in their sample loop at all.
+constexpr uint32_t kLay1Dense[2] = {0x3u, 0x0u}, kLay1Hashed[2] = {0x8u, 0xFu};
+
+template <int T, int S, bool EXACT, bool EXIT = false, bool GEO = false, bool SA = false, int AD = 0,
+          int LAY = 0, bool TAP = true>
 __global__ void __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(final_waves_of<S, !EXIT && !GEO && !SA, AD>(),
                                    final_waves_of<S, !EXIT && !GEO && !SA, AD>())))
@@ -991,7 +1015,12 @@ k_final(FinalArgs a) {
         for (int q = 0; q < 4; ++q) dl[q] = sLv[final_level(kb, hh, q)];
     };
     // wave-uniform slot classes (kernel arguments)
-    auto kinds = [&](int kb) { return SlotKinds{a.kdense[kb], a.khashed[kb]}; };
+    auto kinds = [&](int kb) {
+        if constexpr (LAY == 1) return SlotKinds{kLay1Dense[kb], kLay1Hashed[kb]};
+        else return SlotKinds{a.kdense[kb], a.khashed[kb]};
+    };
+    // grid-space coordinate (LAY 1: the host checked inv_b2 != 0)
+    auto gscale = [&](float x) { return LAY == 1 ? (x + a.gs.bound) * a.gs.inv_b2 : a.gs(x); };
     // rb_prev of sample i is rb_next of sample i - 1 when S == 1 (same bits;
     // saves a division), recomputed from the bins otherwise
     // the sample's position from its two raw bins (b0 read only when S > 1:
@@ -1004,9 +1033,15 @@ k_final(FinalArgs a) {
         const float t = (rbn + rbp) / 2.0f;
         float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
         contract3(x, y, z);
-        ux = a.gs(x);
-        uy = a.gs(y);
-        uz = a.gs(z);
+        ux = gscale(x);
+        uy = gscale(y);
+        uz = gscale(z);
+    };
+    // the sample's positions for k_sgrid (stored after its first gathers are
+    // issued: the stores share vmcnt with the loads, so stores issued first
+    // would hold up the first gather's consumption by their write latency)
+    auto store_position = [&](int i, float ux, float uy, float uz) {
+        const int k = i * S + seg;
         if (sample_writer) {
             a.u_out[((size_t)k * 3 + 0) * N + r] = ux;
             a.u_out[((size_t)k * 3 + 1) * N + r] = uy;
@@ -1074,9 +1109,12 @@ k_final(FinalArgs a) {
                 levels(kb, dl);
                 // parity taps: this half-wave's levels 8 kb + hh + 2 q of the sample
                 uint32_t* rt = nullptr;
-                if (a.rows_tap && live && r % a.tap_stride == 0u)
+                if (TAP && a.rows_tap && live && r % a.tap_stride == 0u)
                     rt = a.rows_tap + ((size_t)(r / a.tap_stride) * T + k) * 128u + (8 * kb + hh) * 8;
-                gather_levels_c2<4, S == 1>(emb, dl, ux, uy, uz, f, kinds(kb), rt, 16);
+                GatherC2<4> g;
+                gather_issue_c2<4>(emb, dl, ux, uy, uz, g, kinds(kb), rt, 16);
+                if (kbi == 0) store_position(i, ux, uy, uz);
+                gather_finish_c2<4, S == 1>(g, f);
             }
             if constexpr (AD > 0) {
 #pragma unroll
@@ -1092,7 +1130,7 @@ k_final(FinalArgs a) {
                 float m = 0.0f;
 #pragma unroll
                 for (int e = 0; e < 8; e += 2) m = max_abs3(m, f[e], f[e + 1]);
-                m = fmaxf(m, __shfl_xor(m, 32));
+                m = max_halves(m);
                 const int kk = scale_exp_of_max(m);
                 if (kbi == 0) {
                     k1 = kk;
@@ -1118,7 +1156,7 @@ k_final(FinalArgs a) {
             int mb = 0;                                  // max of relu(h1) on the float bits
 #pragma unroll
             for (int i = 0; i < 16; ++i) mb = max_relu3(mb, h1a[i], h1b[i]);
-            const float m = fmaxf(__builtin_bit_cast(float, mb), __shfl_xor(__builtin_bit_cast(float, mb), 32));
+            const float m = max_halves(__builtin_bit_cast(float, mb));
             const int k2 = scale_exp_of_max(m);
             s2 = exp2i(k2);
             e_h2 = e_h1 + k2 + ke1;
@@ -1159,7 +1197,7 @@ k_final(FinalArgs a) {
             int mb = 0;
 #pragma unroll
             for (int i = 0; i < 16; ++i) mb = max_relu3(mb, h2a[i], h2b[i]);
-            const float m = fmaxf(__builtin_bit_cast(float, mb), __shfl_xor(__builtin_bit_cast(float, mb), 32));
+            const float m = max_halves(__builtin_bit_cast(float, mb));
             const int k3 = scale_exp_of_max(m);
             s3 = exp2i(k3);
             e_o3 = e_h2 + k3 + ke2;
@@ -1195,14 +1233,14 @@ k_final(FinalArgs a) {
         }
 
         // sigma pre-activation = row 0, held by the lower half-wave
-        const float s_lo = o3[0];
-        const float s_hi = __shfl_xor(s_lo, 32);
+        float s_lo, s_hi;
+        halves(o3[0], s_lo, s_hi);                       // s_lo: row 0 of this column in both halves
 #ifdef SAMNERF_AB_FASTEXP   // timing A/B only
 #define KF_EXP __expf
 #else
 #define KF_EXP expf
 #endif
-        const float sigma = KF_EXP(hh == 0 ? s_lo : s_hi);
+        const float sigma = KF_EXP(s_lo);
         // composite (renderer.py:300-307): w_k = alpha_k * exp(-sum_{j<k} ds_j),
         // the sum in double and in sample order across the ray's S slots
         const float ds = k == T - 1 ? INFINITY : (rb_next - rb_prev) * sigma;
@@ -1215,7 +1253,7 @@ k_final(FinalArgs a) {
         }
         const float w = nan_to_num((1.0f - KF_EXP(-ds)) * KF_EXP(-(float)before));
         if (sample_writer) a.w_out[(size_t)k * N + r] = w;
-        if (a.sigma_tap && sample_writer) a.sigma_tap[(size_t)k * N + r] = sigma;
+        if (TAP && a.sigma_tap && sample_writer) a.sigma_tap[(size_t)k * N + r] = sigma;
         wsum += (double)w;
         depth += (double)(w * t);
 #pragma unroll
@@ -1379,10 +1417,10 @@ k_final(FinalArgs a) {
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) sacc += E[160 + rho(q) + 4 * hh] * fg[q];
-            sacc += __shfl_xor(sacc, 32);
+            sacc = sum_halves(sacc);
             if (live && hh == 0) a.mlog[(size_t)a.tiles(r) * K + c] = sacc;
         }
-        if (live) {                                      // this lane's components of X
+        if (live && a.xsum) {                            // this lane's components of X (training)
             float* X = a.xsum + (size_t)a.tiles(r) * kAeff;
 #pragma unroll
             for (int m = 0; m < 16; ++m) X[2 * final_level(m >> 3, hh, (m & 7) >> 1) + (m & 1)] = gacc[m];
@@ -2004,6 +2042,17 @@ uint32_t final_classes() {
     return (v && atoi(v) == 0) ? 0u : 1u;
 }
 
+// k_final's LAY (1: the reference grid's slot classes and a power-of-two
+// grid scale, compile-time; 0: run time).  SAMNERF_FINAL_LAY=0 (diagnostic
+// build) forces the run-time form, for the bit-identity test.
+int final_layout(const FinalArgs& fa) {
+    const char* v = diag_env("SAMNERF_FINAL_LAY");
+    if (v && atoi(v) == 0) return 0;
+    for (int kb = 0; kb < 2; ++kb)
+        if (fa.kdense[kb] != kLay1Dense[kb] || fa.khashed[kb] != kLay1Hashed[kb]) return 0;
+    return fa.gs.inv_b2 != 0.0f ? 1 : 0;
+}
+
 // k_sgrid_box4 packs cell indices and extents into 10 bits
 bool box4_ok(const GridDesc<16>& g) {
     for (int l = 0; l < 16; ++l)
@@ -2186,9 +2235,24 @@ void launch_final(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa, bool 
         }
         return;
     }
-    if (seg == 1) k_final<32, 1, EXACT><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
-    else if (seg == 2) k_final<32, 2, EXACT><<<xcd_blocks(div_up(N, 64)), 256, 0, s>>>(fa);
-    else k_final<32, 4, EXACT><<<xcd_blocks(div_up(N, 32)), 256, 0, s>>>(fa);
+    // the plain forms: LAY 1 when the grid matches it, TAP only while taps are
+    // set (S = 1 only: the taps' renders are whole views; S > 1 tapped renders
+    // take the run-time layout)
+    const bool tap = fa.sigma_tap || fa.rows_tap;
+    const bool lay1 = final_layout(fa) == 1;
+    const uint32_t nb1 = xcd_blocks(div_up(N, 128)), nb2 = xcd_blocks(div_up(N, 64)),
+                   nb4 = xcd_blocks(div_up(N, 32));
+    if (seg == 1) {
+        if (lay1 && !tap) k_final<32, 1, EXACT, false, false, false, 0, 1, false><<<nb1, 256, 0, s>>>(fa);
+        else if (lay1) k_final<32, 1, EXACT, false, false, false, 0, 1, true><<<nb1, 256, 0, s>>>(fa);
+        else k_final<32, 1, EXACT><<<nb1, 256, 0, s>>>(fa);
+    } else if (seg == 2) {
+        if (lay1 && !tap) k_final<32, 2, EXACT, false, false, false, 0, 1, false><<<nb2, 256, 0, s>>>(fa);
+        else k_final<32, 2, EXACT><<<nb2, 256, 0, s>>>(fa);
+    } else {
+        if (lay1 && !tap) k_final<32, 4, EXACT, false, false, false, 0, 1, false><<<nb4, 256, 0, s>>>(fa);
+        else k_final<32, 4, EXACT><<<nb4, 256, 0, s>>>(fa);
+    }
 }
 
 Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
@@ -2216,7 +2280,7 @@ Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
     w.mpacked = take(mdef ? mask_head_packed_floats() : 0);
     w.aeff = take(madapt ? (size_t)32 * kAeff : 0);
     w.mlog = take(madapt ? (size_t)m->mask_out * n : 0);
-    w.xsum = take(madapt ? (size_t)kAeff * n : 0);
+    w.xsum = take(madapt && m->with_mask == 2 ? (size_t)kAeff * n : 0);   // training renders only
     const bool n1 = m->t_thresh > 0.0f;
     w.n1_list = reinterpret_cast<uint32_t*>(take(n1 ? 2 * n : 0));
     w.n1_cnt = reinterpret_cast<uint32_t*>(take(n1 ? 2 : 0));
@@ -2443,9 +2507,10 @@ int render_impl(const samnerf_model* m, const float* rays_o, const float* rays_d
     if (m->with_sam && (rc = make_grid_desc(m->s_grid, 8, 16, gs, "s_grid"))) return rc;
 
     const uint32_t nb = div_up(N, 256);
-    // parity taps expose slot-ordered intermediates as ray-major views: the
-    // identity map while they are set
-    const RayTiles tiles = g_taps_on ? RayTiles{0u, 0u} : make_ray_tiles(N, m->view_width);
+    // (parity taps: the tapped intermediates stay in slot order, the caller
+    // maps slots to rays -- fused.py ray_of_slots -- so the taps see the
+    // product's tiled launch)
+    const RayTiles tiles = make_ray_tiles(N, m->view_width);
     PropArgs pa{};
     pa.rays_o = rays_o;
     pa.rays_d = rays_d;
@@ -2591,7 +2656,7 @@ int render_impl(const samnerf_model* m, const float* rays_o, const float* rays_d
             k_mask_eff<<<1, 256, 0, s>>>(ea);
             fa.aeff = w.aeff;
             fa.mlog = w.mlog;
-            fa.xsum = w.xsum;
+            fa.xsum = m->with_mask == 2 ? w.xsum : nullptr;   // training render: the head's inputs
             fa.mask_out = m->mask_out;
             ad = m->mask_kind;
         }
@@ -2729,12 +2794,17 @@ int samnerf_mask_forward(const samnerf_model* m, uint32_t N, float* logits, cons
     GridDesc<16> gm;
     int rc = make_grid_desc(m->m_grid, 8, 16, gm, "m_grid");
     if (rc) return rc;
-    const RayTiles tiles = g_taps_on ? RayTiles{0u, 0u} : make_ray_tiles(N, m->view_width);
+    const RayTiles tiles = make_ray_tiles(N, m->view_width);
     return mask_head_forward(m, gm, w.u_f, w.w_f, w.geo_f, N, logits, tiles, w.mpacked,
                              reinterpret_cast<hipStream_t>(stream));
 }
 
 size_t samnerf_mask_train_workspace_size(uint32_t N) { return mask_train_workspace_bytes(N); }
+
+size_t samnerf_mask_train_workspace_size_model(const samnerf_model* m, uint32_t N) {
+    if (!m || !m->with_mask || m->mask_kind < 0 || m->mask_kind > 2) return mask_train_workspace_bytes(N);
+    return mask_train_workspace_bytes(m->mask_kind, N);
+}
 
 // the render workspace's final samples of a 'default' mask model, checked
 static int mask_train_inputs(const samnerf_model* m, uint32_t N, const void* render_ws, size_t render_bytes,
@@ -2750,6 +2820,9 @@ static int mask_train_inputs(const samnerf_model* m, uint32_t N, const void* ren
     if (render_bytes < w.bytes)
         return fail(SAMNERF_EWORKSPACE, "%s: render workspace needs %zu bytes, got %zu", what, w.bytes,
                     render_bytes);
+    if (m->mask_kind != 0 && m->with_mask != 2)
+        return fail(SAMNERF_EINVAL, "%s: the adaptive heads train on a render with with_mask = 2 (it keeps "
+                    "the per-ray input sums)", what);
     return m->mask_kind == 0 ? make_grid_desc(m->m_grid, 8, 16, gm, "m_grid") : SAMNERF_OK;
 }
 
@@ -2765,7 +2838,7 @@ int samnerf_mask_train_forward(const samnerf_model* m, uint32_t N, float* logits
     if (m->mask_kind != 0)                               // adaptive: the chain on the per-ray sums
         return adaptive_train_forward(m, w.xsum, N, logits, workspace, workspace_bytes,
                                       reinterpret_cast<hipStream_t>(stream));
-    const RayTiles tiles = g_taps_on ? RayTiles{0u, 0u} : make_ray_tiles(N, m->view_width);
+    const RayTiles tiles = make_ray_tiles(N, m->view_width);
     return mask_train_forward(m, gm, w.u_f, w.w_f, w.geo_f, N, tiles, logits, workspace, workspace_bytes,
                               reinterpret_cast<hipStream_t>(stream));
 }
@@ -2787,7 +2860,7 @@ int samnerf_mask_train_backward(const samnerf_model* m, uint32_t N, const float*
     if (!grad_m_grid) return fail(SAMNERF_EINVAL, "mask_train_backward: null m_grid gradient");
     for (int i = 0; i < 3; ++i)
         if (!grad_mask_w[i]) return fail(SAMNERF_EINVAL, "mask_train_backward: null gradient");
-    const RayTiles tiles = g_taps_on ? RayTiles{0u, 0u} : make_ray_tiles(N, m->view_width);
+    const RayTiles tiles = make_ray_tiles(N, m->view_width);
     return mask_train_backward(m, gm, w.u_f, w.w_f, w.geo_f, N, tiles, grad_logits, grad_mask_w, grad_m_grid,
                                workspace, workspace_bytes, reinterpret_cast<hipStream_t>(stream));
 }

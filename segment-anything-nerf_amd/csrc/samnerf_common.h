@@ -142,6 +142,36 @@ __device__ __forceinline__ uint32_t dense_or_hash_row(uint32_t x, uint32_t y, ui
     return x + y * d.res + z * (d.res * d.res);
 }
 
+// Cross-half-wave exchange (lane i <-> lane i ^ 32) as one
+// v_permlane32_swap_b32, a VALU op on gfx950, instead of __shfl_xor(v, 32)'s
+// ds_bpermute_b32 (an LDS round trip and an lgkmcnt wait in the middle of the
+// MLP chains).  With vdst = vsrc = v the swap leaves lo = v[i & 31] and
+// hi = v[i | 32] in every lane i.
+__device__ __forceinline__ void halves(float v, float& lo, float& hi) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    lo = __uint_as_float(r[0]);
+    hi = __uint_as_float(r[1]);
+}
+// fmaxf(v, __shfl_xor(v, 32)) (operands in lane order; only ever fed to
+// scale_exp_of_max, which ignores the sign of a zero)
+__device__ __forceinline__ float max_halves(float v) {
+    float lo, hi;
+    halves(v, lo, hi);
+    return fmaxf(lo, hi);
+}
+// v + __shfl_xor(v, 32), the same bits in both halves (IEEE + commutes)
+__device__ __forceinline__ float sum_halves(float v) {
+    float lo, hi;
+    halves(v, lo, hi);
+    return lo + hi;
+}
+// __shfl_xor(v, 32)
+__device__ __forceinline__ float xor_half(float v) {
+    float lo, hi;
+    halves(v, lo, hi);
+    return (threadIdx.x & 32u) ? lo : hi;
+}
+
 template <int N>
 struct alignas(16) VecF {
     float v[N];

@@ -93,6 +93,7 @@ _SIGS = {
                                      ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp, _vp, _sz,
                                      _vp], _int),
     "samnerf_mask_train_workspace_size": ([_u32], _sz),
+    "samnerf_mask_train_workspace_size_model": ([ctypes.POINTER(SamnerfModel), _u32], _sz),
     "samnerf_mask_train_forward": ([ctypes.POINTER(SamnerfModel), _u32, _vp, _vp, _sz, _vp, _sz, _vp], _int),
     "samnerf_mask_train_backward": ([ctypes.POINTER(SamnerfModel), _u32, _vp, ctypes.POINTER(_vp), _vp, _vp,
                                      _sz, _vp, _sz, _vp], _int),

@@ -173,7 +173,12 @@ class ShardedViewPipeline:
         tensors and pack them (any render_fn)."""
         if codec not in ("fp32", "q16"):
             raise ValueError(f"codec must be 'fp32' or 'q16', got {codec!r}")
-        if tile_cols is not None and (codec != "fp32" or tuple(keys) != KEYS_ALL[:len(keys)]
+        # samnerf_render_forward_tile always writes columns 0-4 (and 5-260 when
+        # the model has SAM features and feats=True): only the 3- and 4-key
+        # prefixes describe a tile it fills (ADVICE r4); tile_cols = 5 needs a
+        # render_fn with feats=False on a with_sam model
+        if tile_cols is not None and (codec != "fp32" or len(keys) not in (3, 4)
+                                      or tuple(keys) != KEYS_ALL[:len(keys)]
                                       or tile_cols != sum(KEY_WIDTHS[:len(keys)])):
             raise ValueError("tile_cols: fp32 transport of (image, depth, weights_sum[, samvit]) only")
         self.render_fn, self.H, self.W = render_fn, H, W

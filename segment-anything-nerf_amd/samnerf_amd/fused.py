@@ -61,6 +61,20 @@ def perturbed_positions(N, num_steps, device):
     return tuple(out)
 
 
+def ray_of_slots(N, view_width):
+    """The kernels' slot -> ray map (samnerf_common.h RayTiles / make_ray_tiles):
+    with a view width W (a multiple of 8, N a multiple of 4 W rows) slot s is
+    pixel (x, y) of 8 x 4 tile s // 32 in row-major tile order, pixel s % 32
+    row-major inside it; the identity otherwise.  int64 [N] (CPU)."""
+    s = torch.arange(N, dtype=torch.int64)
+    W = int(view_width)
+    if W < 8 or W % 8 or N % (4 * W):
+        return s
+    tile, inn = s >> 5, s & 31
+    trow, tcol = tile // (W // 8), tile % (W // 8)
+    return (trow * 4 + (inn >> 3)) * W + tcol * 8 + (inn & 7)
+
+
 class FusedRenderer:
     """head_mode: 0 = f16x3 (each fp32 product of grid_mlp, the SAM head and
     the mask head as three fp16 MFMA products on power-of-two scaled operands:
@@ -234,10 +248,11 @@ class FusedRenderer:
         N = rays_o.shape[0]
         dev = rays_o.device
         m = self.model()
-        m.view_width = 0 if taps else int(view_width or 0)
+        m.view_width = int(view_width or 0)
         if mask and not self.fused_mask_ok():
             raise NotImplementedError("fused render: this mask head runs on the unfused path")
-        m.with_mask = 1 if mask else 0
+        # 2: a training render (mask_logits=False): the adaptive heads keep their per-ray input sums
+        m.with_mask = (2 if not mask_logits else 1) if mask else 0
         pert = None
         if isinstance(perturb, (tuple, list)) or perturb:      # the GUI passes spp (an int) as perturb
             pert = tuple(perturb) if isinstance(perturb, (tuple, list)) else \
@@ -329,11 +344,19 @@ class FusedRenderer:
         if mask and mask_logits:
             out["instance_mask_logits"] = logits
         if tap is not None:
+            # the kernels keep per-sample intermediates in slot order (ray
+            # tiling, samnerf_model.view_width): back to ray order here
+            ray_of = ray_of_slots(N, int(m.view_width)).to(dev)
             u2 = tap.pop("u2")
-            out.update({k: v.t() for k, v in tap.items()})
-            out["u2"] = u2.permute(2, 0, 1)
+            for k, v in tap.items():
+                r = torch.empty_like(v.t())
+                r[ray_of] = v.t()
+                out[k] = r
+            r = torch.empty_like(u2.permute(2, 0, 1))
+            r[ray_of] = u2.permute(2, 0, 1)
+            out["u2"] = r
             out.update(rows_tap)
-            out["tap_rays"] = torch.arange(0, N, stride)
+            out["tap_rays"] = ray_of[torch.arange(0, N, stride, device=dev)].cpu()
         if samvit is not None:
             out["samvit"] = samvit
         if keep_workspace:
@@ -479,10 +502,11 @@ class _FusedMaskTrain(torch.autograd.Function):
         out = renderer.render(rays_o, rays_d, cnf, bg, keep_workspace=True, feats=False,
                               own_workspace=True, mask=True, mask_logits=False)
         ws, need, m, vw = out.pop("_workspace")
-        tneed = lib().samnerf_mask_train_workspace_size(N)
+        m.with_mask = 2
+        tneed = lib().samnerf_mask_train_workspace_size_model(ctypes.byref(m), N)
         tws = torch.empty(max(tneed, 1), dtype=torch.uint8, device=dev)
         logits = torch.empty(N, int(m.mask_out), device=dev)
-        m.with_mask, m.view_width = 1, vw
+        m.with_mask, m.view_width = 2, vw
         check(lib().samnerf_mask_train_forward(ctypes.byref(m), N, _ptr(logits), _ptr(ws), need, _ptr(tws),
                                                tneed, _stream(rays_o)), "mask_train_forward")
         ctx.state = (m, vw, ws, need, tws, tneed, list(renderer._keep))
@@ -500,7 +524,7 @@ class _FusedMaskTrain(torch.autograd.Function):
         g_emb = None if adaptive else torch.zeros(ctx.shapes[0], device=dev)
         gw = [torch.empty(sh, device=dev) for sh in (ctx.shapes if adaptive else ctx.shapes[1:])]
         arr = (ctypes.c_void_p * 8)(*[t.data_ptr() for t in gw])
-        m.with_mask, m.view_width = 1, vw
+        m.with_mask, m.view_width = 2, vw
         check(lib().samnerf_mask_train_backward(ctypes.byref(m), g.shape[0], _ptr(g), arr, _ptr(g_emb),
                                                 _ptr(ws), need, _ptr(tws), tneed, _stream(g)),
               "mask_train_backward")

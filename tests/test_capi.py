@@ -97,3 +97,19 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(L.SamnerfUnavailable, match="no CPU fallback"):
         L.lib()
+
+
+def test_mask_train_workspace_size_is_model_aware(hip_lib):
+    """the adaptive heads (mask_kind 1 / 2) need 2 x 7 x 96 floats
+    per ray, not the 'default' head's ~157 KB activation carve."""
+    from samnerf_amd._lib import SamnerfModel
+    m = SamnerfModel()
+    m.with_mask = 1
+    n = 4096
+    m.mask_kind = 0
+    dflt = hip_lib.samnerf_mask_train_workspace_size_model(ctypes.byref(m), n)
+    assert dflt == hip_lib.samnerf_mask_train_workspace_size(n)
+    assert dflt > 150_000 * n
+    for kind in (1, 2):
+        m.mask_kind = kind
+        assert hip_lib.samnerf_mask_train_workspace_size_model(ctypes.byref(m), n) == 2 * 7 * 96 * 4 * n

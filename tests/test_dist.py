@@ -110,3 +110,16 @@ def test_render_sharded_gloo_world2(n):
     for rank, ok, shapes in res:
         assert ok, f"rank {rank} gathered wrong rows"
         assert shapes["image"] == (n, 3) and shapes["samvit"] == (n, 256)
+
+
+def test_tile_cols_only_for_whole_tile_layouts():
+    """samnerf_render_forward_tile always writes columns 0-4, so only
+    the 3- and 4-key prefixes of (image, depth, weights_sum, samvit) describe a
+    tile it fills; a 2-key prefix is refused at construction, not at the
+    first submit."""
+    import pytest
+    from samnerf_amd.dist import ShardedViewPipeline
+    with pytest.raises(ValueError, match="tile_cols"):
+        ShardedViewPipeline(None, 8, 8, keys=("image", "depth"), tile_cols=4)
+    with pytest.raises(ValueError, match="tile_cols"):
+        ShardedViewPipeline(None, 8, 8, keys=("image", "depth", "weights_sum", "samvit"), tile_cols=260)

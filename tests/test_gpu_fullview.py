@@ -57,7 +57,9 @@ def view(request, hip_lib, cuda):
     net = make_net(spec, params, cuda)
     pose, intr = synth.gui_camera(W, H, rot=synth.random_rotation(2 if with_sam else 3))
     ro, rd = ops.get_rays(pose, intr, H, W, device=cuda)
-    out = FusedRenderer(net).render(ro, rd, taps=True)
+    # tiled, as the bench renders (view_width = W: 8 x 4 pixel tiles per wave);
+    # the taps come back in ray order (fused.ray_of_slots)
+    out = FusedRenderer(net).render(ro, rd, taps=True, view_width=W)
     torch.cuda.synchronize()
     assert ("samvit" in out) == with_sam
     return {"spec": spec, "params": params, "ro": ro.cpu(), "rd": rd.cpu(), "with_sam": with_sam,
@@ -229,10 +231,16 @@ def test_corner_rows_bit_exact(view):
 
 
 def test_taps_leave_outputs_unchanged(view, cuda):
-    """The tapped render (the taps' stores, k_sgrid_box4's TAP instantiation)
-    gives the product render's outputs bit for bit."""
+    """The tapped render (the taps' stores: k_final's and k_sgrid_box4's TAP
+    instantiations) gives the product render's outputs bit for bit, and the
+    tiled product render (the bench's launch, view_width = W) equals the
+    untiled one on the whole 512x512 view."""
     from samnerf_amd.fused import FusedRenderer
     net = make_net(view["spec"], view["params"], cuda)
-    out = FusedRenderer(net).render(view["ro"].to(cuda), view["rd"].to(cuda))
+    fr = FusedRenderer(net)
+    ro, rd = view["ro"].to(cuda), view["rd"].to(cuda)
+    tiled = fr.render(ro, rd, view_width=W)
+    untiled = fr.render(ro, rd)
     for k in ("image", "depth", "weights_sum") + (("samvit",) if view["with_sam"] else ()):
-        assert torch.equal(out[k].cpu(), view["out"][k]), k
+        assert torch.equal(tiled[k].cpu(), view["out"][k]), k
+        assert torch.equal(untiled[k].cpu(), view["out"][k]), k

@@ -418,13 +418,15 @@ def test_fused_ragged_ray_counts(hip_lib, cuda, n):
     _check_outputs(out, ref)
 
 
-@pytest.mark.parametrize("n", [70000, 9000])
+@pytest.mark.parametrize("n", [70000, 40000, 9000])
 def test_final_slot_classes_bit_identical(hip_lib, cuda, monkeypatch, n, diag):
     """k_final's wave-uniform slot paths -- one 16-B load per x-adjacent corner
     pair on dense levels (with the top-cell weight swap) and select-free
-    hashed rows -- against the lane-varying form (SAMNERF_FINAL_CLASSES=0):
+    hashed rows -- against the lane-varying form (SAMNERF_FINAL_CLASSES=0),
+    and the compile-time layout of the reference grid (LAY 1, the product's
+    form) against the same classes taken at run time (SAMNERF_FINAL_LAY=0):
     identical bits, on a view whose far samples reach the top cells of the
-    coarse levels."""
+    coarse levels, at S = 1 / 2 / 4 segments (n = 70000 / 40000 / 9000)."""
     from samnerf_amd import ops
     from samnerf_amd.fused import FusedRenderer, ROW
     spec = synth.ModelSpec(with_sam=True)
@@ -433,14 +435,16 @@ def test_final_slot_classes_bit_identical(hip_lib, cuda, monkeypatch, n, diag):
     ro, rd = ops.get_rays(pose, intr, 160, 512, device=cuda)
     fr = FusedRenderer(net)
     outs = []
-    for cl in ("0", "1"):
+    for cl, lay in (("0", "0"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("SAMNERF_FINAL_CLASSES", cl)
+        monkeypatch.setenv("SAMNERF_FINAL_LAY", lay)
         rows = torch.empty(n, ROW, device=cuda)
         o = fr.render(ro[:n], rd[:n], rows=rows)
         o["rows"] = rows
         outs.append(o)
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
+        assert torch.equal(outs[0][k], outs[2][k]), k
 
 
 def test_fused_render_from_reference_layout_checkpoint(hip_lib, cuda, tmp_path):
@@ -538,26 +542,22 @@ def _twice_equal(render, times=2):
 
 @pytest.mark.parametrize("seg", ["1", "2", "4"])
 @pytest.mark.parametrize("head_mode", [0, 1])
-def test_final_forms_deterministic(hip_lib, cuda, monkeypatch, seg, head_mode, diag):
-    """Every k_final form renders the same bits three times (a
-    forward whose output varies run to run has a hazard; the removed
-    prefetch form differed on the first render of a process): S = 1 / 2 / 4,
-    both precisions, feature rows on."""
-    from samnerf_amd import ops
-    from samnerf_amd.fused import FusedRenderer, ROW
-    monkeypatch.setenv("SAMNERF_FINAL_S", seg)
-    spec = synth.ModelSpec(with_sam=True)
-    net = make_net(spec, synth.make_params(spec, seed=23, emb_scale=0.5, ln_jitter=0.1), cuda)
-    pose, intr = synth.gui_camera(512, 80, rot=synth.random_rotation(11))
-    ro, rd = ops.get_rays(pose, intr, 80, 512, device=cuda)
-    fr = FusedRenderer(net, head_mode=head_mode)
-    rows = torch.empty(ro.shape[0], ROW, device=cuda)
-
-    def render():
-        o = fr.render(ro, rd, rows=rows, view_width=512)
-        o["rows"] = rows.clone()
-        return o
-    _twice_equal(render, times=3)
+def test_final_forms_deterministic(hip_lib, cuda, seg, head_mode):
+    """Every k_final form renders the same bits three times in a FRESHLY
+    SPAWNED process (tests/final_forms_child.py: the removed round-4 prefetch
+    form differed on the first render of a process, so the first render must
+    be one of those compared), and the child's digest equals this process's:
+    S = 1 / 2 / 4, both precisions, feature rows on, the bench's ray tiling."""
+    import subprocess
+    import sys
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "final_forms_child.py")
+    r = subprocess.run([sys.executable, child, seg, str(head_mode)], capture_output=True, text=True,
+                       timeout=100)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    digests = [ln.split()[1] for ln in r.stdout.splitlines() if ln.startswith("digest")]
+    assert len(digests) == 3 and len(set(digests)) == 1, r.stdout
+    from final_forms_child import render_digest
+    assert render_digest(seg, head_mode, cuda) == digests[0]
 
 
 @pytest.mark.parametrize("form", ["exit", "mask_default", "sum_after", "adaptive_density", "adaptive_rgb"])

@@ -89,3 +89,20 @@ def test_surface_scene_is_an_opaque_sphere():
         s_in = net.density(inside, proposal=p)["sigma"]
         s_out = net.density(outside, proposal=p)["sigma"]
         assert bool((s_in > 20).all()) and bool((s_out < 0.05).all()), (p, s_in, s_out)
+
+
+def test_ray_of_slots_matches_ray_tiles():
+    """fused.ray_of_slots restates RayTiles (samnerf_common.h): a permutation
+    of the view's pixels, 8 x 4 tiles in row-major tile order; the identity
+    where the tiling does not apply."""
+    import torch
+    from samnerf_amd.fused import ray_of_slots
+    W, H = 64, 16
+    m = ray_of_slots(W * H, W)
+    assert torch.equal(torch.sort(m).values, torch.arange(W * H))
+    for s in (0, 1, 7, 8, 31, 32, 33, 255, 256, W * H - 1):
+        tile, inn = s // 32, s % 32
+        trow, tcol = tile // (W // 8), tile % (W // 8)
+        assert int(m[s]) == (trow * 4 + inn // 8) * W + tcol * 8 + inn % 8
+    assert torch.equal(ray_of_slots(W * H - W, W), torch.arange(W * H - W))   # not 4 whole rows
+    assert torch.equal(ray_of_slots(100, 0), torch.arange(100))

@@ -5,7 +5,7 @@
 # stage ms.  usage (GPU box): bash tools/ab_libs.sh ROUNDS lib1 lib2 ...
 set -o pipefail
 ROUNDS=$1; shift
-OUT="$GRAFT_REPO_ROOT/gpurun_out/ab"
+OUT="${AB_DIR:-$GRAFT_REPO_ROOT/gpurun_out/ab}"
 mkdir -p "$OUT"
 for r in $(seq 1 $ROUNDS); do
   for L in "$@"; do
