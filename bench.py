@@ -333,7 +333,7 @@ def mask_view(dev, steps, warmup, head_mode=0, ref_rays=32768):
                     "weighted sum): fused render + k_mask_head vs run_torch(return_mask=1), 512x512 view"}
 
 
-def train_steps(dev, steps, warmup, torch_adam=False, head="hip"):
+def train_steps(dev, steps, warmup, torch_adam=False, head="hip", deterministic=False):
     """BASELINE config 5: one step = fused forward of 4096 rays
     (64x64, fovy 60) with grad, MSE vs a N(0,1) [1,256,64,64] target (seed 1)
     after the reference's bilinear resize, backward (HIP s_grid scatter +
@@ -351,7 +351,7 @@ def train_steps(dev, steps, warmup, torch_adam=False, head="hip"):
     params_ = [p for p in net.parameters() if p.requires_grad]
     opt = (torch.optim.Adam(params_, lr=1e-2, eps=1e-15) if torch_adam
            else FusedAdam(params_, lr=1e-2, eps=1e-15))
-    renderer = FusedRenderer(net)
+    renderer = FusedRenderer(net, deterministic=deterministic)
     h = w = 64
     pose, intr = synth.gui_camera(w, h)
     ro, rd = ops.get_rays(pose, intr, h, w, device=dev)
@@ -680,6 +680,60 @@ class ViewRunner:
         return dt, last, stage_avg, stage_src
 
 
+def explain_gather(runner, views=5):
+    """N > 1: what one view costs each rank, measured apart so the driver's
+    scaling run explains itself.  Per view: the band's
+    render (HIP events on the render stream around samnerf_render_forward_tile
+    into this rank's slice of the gather buffer) and then the all-gather alone
+    (RCCL: all_gather_into_tensor, the current stream waiting on the
+    collective's stream; events on the current stream around it), not
+    overlapped, so gather_ms / render_ms says which of the two the pipelined
+    timing is bound by.  Bytes: what each rank receives per view.  Returns
+    rank 0's record (all ranks take part)."""
+    from samnerf_amd.dist import _all_gather
+    args, dev, H, W = runner.args, runner.dev, runner.H, runner.W
+    from samnerf_amd import ops
+    ro, rd = ops.get_rays(runner.pose, runner.intr, H, W, device=dev, row0=runner.r0, rows=runner.r1 - runner.r0)
+    n = ro.shape[0]
+    cols = 5 if args.no_sam else 261
+    buf = torch.empty(runner.world * n, cols, device=dev)
+    own = buf[dist.get_rank() * n:(dist.get_rank() + 1) * n]
+    rms, gms = [], []
+    for i in range(views + 1):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        torch.cuda.synchronize()
+        e0.record()
+        runner.renderer.render(ro, rd, view_width=W if args.tiles else 0, out_tile=own)
+        e1.record()
+        _all_gather(buf, own, None, async_op=False)
+        e2.record()
+        torch.cuda.synchronize()
+        if i:                                            # the first view warms the collective
+            rms.append(e0.elapsed_time(e1))
+            gms.append(e1.elapsed_time(e2))
+    mine = torch.tensor([float(np.mean(rms)), float(np.mean(gms))], dtype=torch.float64)
+    allr = [torch.zeros(2, dtype=torch.float64) for _ in range(runner.world)]
+    if args.dist_backend == "nccl":
+        g = [t.to(dev) for t in allr]
+        dist.all_gather(g, mine.to(dev))
+        allr = [t.cpu() for t in g]
+    else:
+        dist.all_gather(allr, mine)
+    render = [float(t[0]) for t in allr]
+    gather = [float(t[1]) for t in allr]
+    recv = (runner.world - 1) * n * cols * 4
+    return {"per_rank_render_ms": render, "per_rank_gather_ms": gather,
+            "bytes_received_per_rank_per_view": recv,
+            "gather_GBps_per_rank": recv / (max(gather) * 1e-3) / 1e9,
+            "gather_over_render": max(gather) / (sum(render) / len(render)),
+            "views": views, "backend": args.dist_backend,
+            "what": "each rank renders its band into its slice of the gather buffer, then the all-gather "
+                    "runs alone (not overlapped): render_ms = HIP events on the render stream, gather_ms = "
+                    "events on the current stream around all_gather_into_tensor (waits for RCCL's stream); "
+                    "the timed headline overlaps view i's gather with view i+1's render, so a view costs "
+                    "about max(render, gather) when gather_over_render < 1"}
+
+
 VALU_RATE = os.path.join(REPO, "profiles", "r4_valu_rate.json")
 
 
@@ -840,6 +894,8 @@ def main():
     roof, stage_roof = rooflines(stage_avg, band_rays, args.head_mode, pmc_rates(), stage_clocks())
 
     side = {}
+    if world > 1 and args.chunks == 0 and codec == "fp32":
+        side["gather_explained"] = explain_gather(runner)
     if not args.no_alt and world > 1 and with_sam and args.chunks == 0:
         # the other transport, same views, after the headline
         other = "q16" if codec == "fp32" else "fp32"
@@ -963,9 +1019,15 @@ def main():
     if not args.no_alt and world == 1 and args.rank_share <= 1 and with_sam:
         # BASELINE config 5 beside the headline (`--mode train` runs it alone)
         ms5, loss5 = train_steps(dev, 20, 5)
+        ms5d, loss5d = train_steps(dev, 20, 5, deterministic=True)
         side["cfg5_train"] = {"ms_per_step": ms5, "steps_per_s": 1e3 / ms5,
                               "rays_per_s": 4096 * 1e3 / ms5, "steps": 20, "warmup": 5,
-                              "final_loss": loss5, **TRAIN_WHAT}
+                              "final_loss": loss5, **TRAIN_WHAT,
+                              "deterministic_mode": {
+                                  "ms_per_step": ms5d, "final_loss": loss5d,
+                                  "what": "the same steps with the s_grid scatter in 64-bit fixed point "
+                                          "(samnerf_sgrid_backward_det, SURVEY H5): gradients repeat bit for "
+                                          "bit (tests/test_gpu_train.py::test_distillation_steps_repeat_bit_for_bit)"}}
 
     if not args.no_alt and world == 1 and args.rank_share <= 1:
         # the reference's RGB training stage on the HIP training

@@ -331,6 +331,22 @@ int samnerf_sgrid_backward(const samnerf_model* model, const float* grad_fsam, u
                            float* grad_embeddings, const void* workspace,
                            size_t workspace_bytes, samnerf_stream_t stream);
 
+/* Deterministic form of samnerf_sgrid_backward (an optional mode
+ * whose gradients repeat bit for bit run to run).  The reference scatters
+ * with unordered fp32 atomics (gridencoder.cu:334-347), as the default form
+ * does, so two identical steps differ in the last bits.  Here every
+ * contribution is added to a 64-bit fixed-point accumulator instead (integer
+ * atomics are associative: the totals do not depend on the order the waves
+ * reach a row in), at the scale 2^(61 - ceil(log2 N) - e) with max |grad_fsam|
+ * < 2^e, so no total can overflow and each is resolved to max|g| 2^-(61 -
+ * ceil(log2 N)); then the totals are added to grad_embeddings as fp32.
+ * accum: samnerf_sgrid_accum_size(model) bytes of device memory, all zero on
+ * the first call (hipMemset) and left zero by every call. */
+size_t samnerf_sgrid_accum_size(const samnerf_model* model);
+int samnerf_sgrid_backward_det(const samnerf_model* model, const float* grad_fsam, uint32_t N,
+                               float* grad_embeddings, int64_t* accum, const void* workspace,
+                               size_t workspace_bytes, samnerf_stream_t stream);
+
 /* ------------------------------------------------------------- training --
  * One Adam step (torch.optim.Adam semantics, amsgrad off, maximize off) over
  * every tensor of the table in one launch: param -= lr / (1 - beta1^step) *

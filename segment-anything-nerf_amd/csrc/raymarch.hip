@@ -218,7 +218,20 @@ constexpr uint32_t prop_sigma_blocks(uint32_t N) {
 // identical bits.
 constexpr uint32_t kPropBoxSlots = 128;      // rows per level slice (8 B each)
 
-template <int T, bool FIRST, int LOOK>
+// KD / KH (round 5): the proposal grid's level classes as compile-time
+// masks (bit l: level l dense / hashed; the reference's proposal grids,
+// network.py:96-104 at the default sizes, are DDDHH and DDHHH), with a
+// power-of-two grid scale.  The run-time form (KD = KH = 0) takes each
+// level's dense / hashed branch on a uniform flag, and the branches split the
+// levels into separate blocks: each level's loads were issued and waited for
+// before the next level's (5 memory round trips per sample).  With the
+// classes known the 5 levels' 28 loads issue together, then the weighted
+// corner sums (gather_issue_c2 / gather_finish_c2, the k_final lookups: the
+// same rows, weights and FMA order as lookup_level3, so the same bits).
+template <uint32_t KD, uint32_t KH>
+__device__ __forceinline__ void prop_lookup_lay(const PropArgs& a, float x, float y, float z, float* feat);
+
+template <int T, bool FIRST, int LOOK, uint32_t KD = 0, uint32_t KH = 0>
 __global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
     static_assert(T % 4 == 0, "T must be a multiple of 4");
     constexpr uint32_t Q = T / 4;
@@ -283,6 +296,8 @@ __global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
             else
                 lookup_level3_pbox<2, true>(a.grid.emb, a.grid.lv[l], bx[l], sl, ux, uy, uz, feat + 2 * l);
         }
+    } else if constexpr ((KD | KH) == 0x1Fu && LOOK == kLookPacked) {
+        prop_lookup_lay<KD, KH>(a, x, y, z, feat);
     } else {
         grid_features<5, 2, LOOK == kLookRef>(a.grid, a.gs(x), a.gs(y), a.gs(z), feat);
     }
@@ -855,6 +870,17 @@ __device__ __forceinline__ void gather_levels_c2(const float2* __restrict__ emb,
     gather_finish_c2<NL, PK>(g, f);
 }
 
+// k_prop_sigma's lookup with compile-time level classes (KD / KH): the 5
+// levels' loads issued together, then the packed corner sums
+template <uint32_t KD, uint32_t KH>
+__device__ __forceinline__ void prop_lookup_lay(const PropArgs& a, float x, float y, float z, float* feat) {
+    const float ux = (x + a.gs.bound) * a.gs.inv_b2, uy = (y + a.gs.bound) * a.gs.inv_b2,
+                uz = (z + a.gs.bound) * a.gs.inv_b2;
+    GatherC2<5> g;
+    gather_issue_c2<5>(reinterpret_cast<const float2*>(a.grid.emb), a.grid.lv, ux, uy, uz, g, SlotKinds{KD, KH});
+    gather_finish_c2<5, true>(g, feat);
+}
+
 __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const LevelDesc& q, bool hi) {
     return LevelDesc{hi ? q.off : p.off, hi ? q.size : p.size, hi ? q.res : p.res, hi ? q.flags : p.flags,
                      hi ? q.fres : p.fres, hi ? q.ftop : p.ftop};
@@ -880,6 +906,12 @@ __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const Leve
 // spill 20+ registers at 3 waves and stay at 2 (0.139 vs 0.158 ms at 32K rays).
 #ifndef SAMNERF_DIAG_FINAL_WAVES
 #define SAMNERF_DIAG_FINAL_WAVES 3
+#endif
+#ifndef SAMNERF_FINAL_JOINT
+#define SAMNERF_FINAL_JOINT 1
+#endif
+#ifndef SAMNERF_FINAL_VG
+#define SAMNERF_FINAL_VG 0
 #endif
 template <int S_, bool PLAIN_ = true>
 constexpr int final_waves() { return (S_ == 1 && PLAIN_) ? SAMNERF_DIAG_FINAL_WAVES : 2; }
@@ -927,7 +959,12 @@ k_final(FinalArgs a) {
     static_assert(kXSteps * 64 == 2 * kFSlots * 64 * 4, "exact weights reuse the f16x3 slots");
     constexpr int R = 32 / S, TS = T / S;
     __shared__ uint4 Fbuf[2 * kFSlots * 64];          // f16x3: hi | lo fragments; exact: fp32 steps
-    __shared__ float Vl[kVTotal];
+    // VG: the view MLP's weights read from global memory (L2) at the end of
+    // the ray instead of staged in LDS -- it runs once per ray (not per
+    // sample) outside the SA forms, and without its 12 KiB a block's LDS
+    // (33 KiB) lets 4 blocks share a CU
+    constexpr bool VG = SAMNERF_FINAL_VG && !SA;
+    __shared__ float Vl[VG ? 1 : kVTotal];
     __shared__ LevelDesc sLv[16];
     if (threadIdx.x < 16) sLv[threadIdx.x] = a.grid.lv[threadIdx.x];
     uint4* const Fh = Fbuf;
@@ -939,7 +976,9 @@ k_final(FinalArgs a) {
     } else {
         for (int idx = threadIdx.x; idx < 2 * kFSlots * 64; idx += 256) Fbuf[idx] = a.gpack[idx];
     }
-    for (int idx = threadIdx.x; idx < kVTotal; idx += 256) Vl[idx] = view_weight(a, idx);
+    if constexpr (!VG)
+        for (int idx = threadIdx.x; idx < kVTotal; idx += 256) Vl[idx] = view_weight(a, idx);
+    auto VW = [&](int idx) { return VG ? view_weight(a, idx) : Vl[idx]; };
     // f16x3: log2 scales of the three weight tensors' fragments
     const int ke0 = EXACT ? 0 : a.gexp[0], ke1 = EXACT ? 0 : a.gexp[1], ke2 = EXACT ? 0 : a.gexp[2];
     __syncthreads();
@@ -1098,24 +1137,63 @@ k_final(FinalArgs a) {
         // a scale two or more binades lower (up to one binade it still fits
         // fp16 at the first block's scale, f16x3.h).
         int k1 = 0, e_h1 = 0, e_h2 = 0;
+        // this half-wave's 8 features of k-block kb (levels 8 kb + hh + 2 q)
+        auto gather_kb = [&](int kb, float* f, bool first) {
+            LevelDesc dl[4];
+            levels(kb, dl);
+            uint32_t* rt = nullptr;                      // parity taps only
+            if (TAP && a.rows_tap && live && r % a.tap_stride == 0u)
+                rt = a.rows_tap + ((size_t)(r / a.tap_stride) * T + k) * 128u + (8 * kb + hh) * 8;
+            GatherC2<4> g;
+            gather_issue_c2<4>(emb, dl, ux, uy, uz, g, kinds(kb), rt, 16);
+            if (first) store_position(i, ux, uy, uz);
+            gather_finish_c2<4, S == 1>(g, f);
+        };
+#if SAMNERF_FINAL_JOINT
+        // f16x3, layer 1 in one piece (round 5): both k-blocks gathered first
+        // -- k-block 0 (the dense pair loads, 24 loads) before k-block 1 (32),
+        // so only its 8 features wait through the second gather, where the
+        // one-block-at-a-time form held layer 1's 32 accumulators there --
+        // then ONE scale from the column's max over all 32 inputs, and the 12
+        // MFMAs in the k-block 1, 0 order of every round.  (No rescale of the
+        // accumulators between the blocks any more: the same f16x3 products
+        // at one power-of-two scale, fp32-equivalent as before; the bits are
+        // those of this form.)
+        constexpr bool kJoint = !EXACT;
+#else
+        constexpr bool kJoint = false;
+#endif
+        if constexpr (kJoint) {
+            float f0[8], f1[8];
+            gather_kb(0, f0, true);
+            gather_kb(1, f1, false);
+            if constexpr (AD > 0) {
 #pragma unroll
-        for (int kbi = 0; kbi < 2; ++kbi) {
+                for (int m = 0; m < 8; ++m) {
+                    fk[m] = f0[m];
+                    fk[8 + m] = f1[m];
+                }
+            }
+            float m = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) m = max_abs3(max_abs3(m, f0[e], f0[e + 1]), f1[e], f1[e + 1]);
+            k1 = scale_exp_of_max(max_halves(m));
+            const float sc = exp2i(k1);
+            uint4 bh, bl;
+            split8_f16(f1, sc, bh, bl);
+            h1a = mfma_f16x3(FH[(kF1 + 2) * 64], FL[(kF1 + 2) * 64], bh, bl, h1a);
+            h1b = mfma_f16x3(FH[(kF1 + 3) * 64], FL[(kF1 + 3) * 64], bh, bl, h1b);
+            split8_f16(f0, sc, bh, bl);
+            h1a = mfma_f16x3(FH[kF1 * 64], FL[kF1 * 64], bh, bl, h1a);
+            h1b = mfma_f16x3(FH[(kF1 + 1) * 64], FL[(kF1 + 1) * 64], bh, bl, h1b);
+        }
+#pragma unroll
+        for (int kbi = 0; kbi < (kJoint ? 0 : 2); ++kbi) {
             // k-block 1 (levels 8-15) first, then 0: the accumulation order
             // of every round (a cross-sample prefetch of k-block 1 set it)
             const int kb = 1 - kbi;
             float f[8];
-            {
-                LevelDesc dl[4];
-                levels(kb, dl);
-                // parity taps: this half-wave's levels 8 kb + hh + 2 q of the sample
-                uint32_t* rt = nullptr;
-                if (TAP && a.rows_tap && live && r % a.tap_stride == 0u)
-                    rt = a.rows_tap + ((size_t)(r / a.tap_stride) * T + k) * 128u + (8 * kb + hh) * 8;
-                GatherC2<4> g;
-                gather_issue_c2<4>(emb, dl, ux, uy, uz, g, kinds(kb), rt, 16);
-                if (kbi == 0) store_position(i, ux, uy, uz);
-                gather_finish_c2<4, S == 1>(g, f);
-            }
+            gather_kb(kb, f, kbi == 0);
             if constexpr (AD > 0) {
 #pragma unroll
                 for (int m = 0; m < 8; ++m) fk[kb * 8 + m] = f[m];
@@ -1384,18 +1462,18 @@ k_final(FinalArgs a) {
     if constexpr (!SA) {
         floatx16 v1 = {};
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v1 = MFMA32(Vl[kV1 + q * 64 + lane], fg[q], v1);
+        for (int q = 0; q < 8; ++q) v1 = MFMA32(VW(kV1 + q * 64 + lane), fg[q], v1);
 #pragma unroll
-        for (int s = 0; s < 8; ++s) v1 = MFMA32(Vl[kV1 + (8 + s) * 64 + lane], sh[2 * s + hh] * ws, v1);
+        for (int s = 0; s < 8; ++s) v1 = MFMA32(VW(kV1 + (8 + s) * 64 + lane), sh[2 * s + hh] * ws, v1);
 #pragma unroll
         for (int i = 0; i < 16; ++i) v1[i] = relu_bits(v1[i]);
         floatx16 v2 = {};
 #pragma unroll
-        for (int q = 0; q < 16; ++q) v2 = MFMA32(Vl[kV2 + q * 64 + lane], v1[q], v2);
+        for (int q = 0; q < 16; ++q) v2 = MFMA32(VW(kV2 + q * 64 + lane), v1[q], v2);
 #pragma unroll
         for (int i = 0; i < 16; ++i) v2[i] = relu_bits(v2[i]);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) v3 = MFMA32(Vl[kV3 + q * 64 + lane], v2[q], v3);
+        for (int q = 0; q < 16; ++q) v3 = MFMA32(VW(kV3 + q * 64 + lane), v2[q], v3);
     }
 
     if constexpr (AD > 0) {
@@ -1720,11 +1798,32 @@ k_sgrid_box4(SgridArgs a) {
 // is kept selectable (SAMNERF_SGRID_BWD=box) and tested against it.
 constexpr uint32_t kBwdBoxCells = 64;
 
-template <int T>
+// DET (samnerf_sgrid_backward_det): the per-corner form's adds go
+// to a 64-bit fixed-point accumulator instead of the fp32 table -- integer
+// atomics are associative, so every total is the same whatever order the
+// waves reach it in -- at the scale 2^det_shift (sgrid_det_shift: |any row's
+// total| * 2^shift < 2^61); k_sgrid_det_finish adds the totals to the fp32
+// gradient.  The per-wave butterfly merge is a fixed order, so it stays.
+struct DetAcc {
+    unsigned long long* acc;   // [rows][8] int64 (two's complement), null: the fp32 atomics
+    const uint32_t* hdr;       // hdr[0]: max |grad_fsam| (float bits), k_sgrid_det_max
+    int log2n;                 // ceil(log2 N)
+};
+
+// 2^shift of the fixed point: max |g| < 2^e and at most N rays of weights
+// summing to <= 1 reach a row, so |total| < 2^(log2n + e) and |total| 2^shift
+// < 2^61 (two bits of margin)
+__device__ __forceinline__ int sgrid_det_shift(const DetAcc& d) {
+    int e = 0;
+    frexpf(__uint_as_float(d.hdr[0]), &e);
+    return 61 - d.log2n - e;
+}
+
+template <int T, bool DET = false>
 __global__ void __launch_bounds__(256)
 k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __restrict__ u_in,
                  const float* __restrict__ w_in, const float* __restrict__ grad, uint32_t gstride,
-                 float* __restrict__ gemb, uint32_t max_cells, uint32_t run_res) {
+                 float* __restrict__ gemb, uint32_t max_cells, uint32_t run_res, DetAcc det = {}) {
     __shared__ float box[4][kBwdBoxCells * 8];           // per wave: cell x channel sums
     __shared__ uint32_t list[4][kBwdBoxCells];           // per wave: rows of the non-zero cells
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1751,7 +1850,9 @@ k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __rest
     // previous sample's 8 corner rows stay pending in registers -- a new corner
     // on a pending row absorbs its sum, only rows the ray has left are added to
     // memory (consecutive samples of a ray share cells at the coarse levels)
-    const bool run = max_cells == 0u && d.res <= run_res;     // block-uniform
+    const bool run = !DET && max_cells == 0u && d.res <= run_res;     // block-uniform
+    const double dscale = DET ? ldexp(1.0, sgrid_det_shift(det)) : 0.0;
+    unsigned long long* const dbase = DET ? det.acc + (size_t)d.off * 8u + ch : nullptr;
     uint32_t prow[8];
     float pval[8];
 #pragma unroll
@@ -1778,7 +1879,7 @@ k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __rest
         const uint32_t z0 = (uint32_t)wave_imin((int)cz), z1 = (uint32_t)wave_imax((int)nz);
         const uint32_t ex = x1 - x0 + 1u, ey = y1 - y0 + 1u, ez = z1 - z0 + 1u;
         const uint32_t cells = ex * ey * ez;                 // wave-uniform
-        if (cells <= max_cells) {
+        if (!DET && cells <= max_cells) {
             // 1. zero the slice (lane = cell), 2. LDS-add the corners
             reinterpret_cast<float4*>(slice + lane * 8u)[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             reinterpret_cast<float4*>(slice + lane * 8u)[1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1869,7 +1970,13 @@ k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __rest
                         else val += oval;
                     }
                 }
-                if (alive) atomicAdd(base + (size_t)row * 8u, val);
+                if (alive) {
+                    if constexpr (DET)
+                        atomicAdd(dbase + (size_t)row * 8u,
+                                  (unsigned long long)__double2ll_rn((double)val * dscale));
+                    else
+                        atomicAdd(base + (size_t)row * 8u, val);
+                }
             }
         }
     }
@@ -1877,6 +1984,35 @@ k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __rest
 #pragma unroll
         for (int c = 0; c < 8; ++c)
             if (prow[c] != 0xFFFFFFFFu) atomicAdd(base + (size_t)prow[c] * 8u, pval[c]);
+}
+
+// max |grad_fsam[ray, 0:128]| into hdr[0] (zeroed by the host): float bits of
+// non-negative values order as unsigned integers, so the atomic max is exact
+__global__ void __launch_bounds__(256)
+k_sgrid_det_max(const float* __restrict__ grad, uint32_t N, uint32_t gstride, uint32_t* hdr) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float m = 0.0f;
+    if (t < (uint64_t)N * 32u) {                     // 4 features per thread
+        const float4 v = *reinterpret_cast<const float4*>(grad + (size_t)(t >> 5) * gstride + (t & 31u) * 4u);
+        m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+    }
+    m = wave_max64(m);
+    if ((threadIdx.x & 63u) == 0u && m > 0.0f) atomicMax(hdr, __float_as_uint(m));
+}
+
+// the fixed-point totals into the fp32 gradient (accumulated into, as the
+// atomic form), the accumulator left zero for the next call
+__global__ void __launch_bounds__(256)
+k_sgrid_det_finish(DetAcc det, float* __restrict__ gemb, uint64_t n) {
+    const double inv = ldexp(1.0, -sgrid_det_shift(det));
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const long long v = (long long)det.acc[i];
+        if (v != 0) {
+            gemb[i] = gemb[i] + (float)((double)v * inv);
+            det.acc[i] = 0ull;
+        }
+    }
 }
 
 // ------------------------------------------------------- step kernels ----
@@ -2068,6 +2204,24 @@ bool box4_ok(const GridDesc<16>& g) {
 template <int T, bool FIRST>
 void launch_prop_sigma(int look, uint32_t N, hipStream_t s, const PropArgs& pa) {
     const uint32_t nb = prop_sigma_blocks<T>(N);
+    // the reference's proposal grids with a power-of-two grid scale: the
+    // compile-time level classes (SAMNERF_PROP_LAY=0, diagnostic build: the
+    // run-time form, for the bit-identity test)
+    uint32_t kd = 0, kh = 0;
+    for (int l = 0; l < 5; ++l) {
+        kd |= (pa.grid.lv[l].flags & kHashed) ? 0u : 1u << l;
+        kh |= (pa.grid.lv[l].flags & kHashed) ? 1u << l : 0u;
+    }
+    const char* pl = diag_env("SAMNERF_PROP_LAY");
+    const bool lay = look == kLookPacked && pa.gs.inv_b2 != 0.0f && !(pl && atoi(pl) == 0);
+    if (lay && kd == 0x07u && kh == 0x18u) {
+        k_prop_sigma<T, FIRST, kLookPacked, 0x07u, 0x18u><<<nb, 256, 0, s>>>(pa);
+        return;
+    }
+    if (lay && kd == 0x03u && kh == 0x1Cu) {
+        k_prop_sigma<T, FIRST, kLookPacked, 0x03u, 0x1Cu><<<nb, 256, 0, s>>>(pa);
+        return;
+    }
     if (look == kLookRef) k_prop_sigma<T, FIRST, kLookRef><<<nb, 256, 0, s>>>(pa);
     else if (look == kLookBox4 && box4_ok(pa.grid))
         k_prop_sigma<T, FIRST, kLookBox4><<<nb, 256, 0, s>>>(pa);
@@ -2863,6 +3017,48 @@ int samnerf_mask_train_backward(const samnerf_model* m, uint32_t N, const float*
     const RayTiles tiles = make_ray_tiles(N, m->view_width);
     return mask_train_backward(m, gm, w.u_f, w.w_f, w.geo_f, N, tiles, grad_logits, grad_mask_w, grad_m_grid,
                                workspace, workspace_bytes, reinterpret_cast<hipStream_t>(stream));
+}
+
+// rows of the s_grid table (the deterministic backward's accumulator holds 8
+// int64 per row, then an 8-entry header)
+static uint64_t sgrid_rows(const samnerf_model* m) {
+    return m && m->with_sam && m->s_grid.offsets_host ? (uint64_t)m->s_grid.offsets_host[m->s_grid.num_levels]
+                                                      : 0u;
+}
+
+size_t samnerf_sgrid_accum_size(const samnerf_model* m) {
+    const uint64_t rows = sgrid_rows(m);
+    return rows ? (size_t)(rows * 8u + 8u) * sizeof(int64_t) : 0u;
+}
+
+int samnerf_sgrid_backward_det(const samnerf_model* m, const float* grad_fsam, uint32_t N,
+                               float* grad_embeddings, int64_t* accum, const void* workspace,
+                               size_t workspace_bytes, samnerf_stream_t stream) {
+    if (!m || !grad_fsam || !grad_embeddings || !workspace || !accum)
+        return fail(SAMNERF_EINVAL, "sgrid_backward_det: null pointer");
+    if (!m->with_sam) return fail(SAMNERF_EINVAL, "sgrid_backward_det: model has no s_grid");
+    Workspace w = carve(m, N, const_cast<void*>(workspace));
+    if (workspace_bytes < w.bytes)
+        return fail(SAMNERF_EWORKSPACE, "sgrid_backward_det: workspace too small");
+    if (N == 0) return SAMNERF_OK;
+    GridDesc<16> gs;
+    int rc = make_grid_desc(m->s_grid, 8, 16, gs, "s_grid");
+    if (rc) return rc;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const uint64_t n = sgrid_rows(m) * 8u;
+    DetAcc det;
+    det.acc = reinterpret_cast<unsigned long long*>(accum);
+    uint32_t* hdr = reinterpret_cast<uint32_t*>(accum + n);
+    det.hdr = hdr;
+    det.log2n = 0;
+    while ((1ull << det.log2n) < (uint64_t)N) ++det.log2n;
+    if (hipMemsetAsync(hdr, 0, sizeof(uint32_t), s) != hipSuccess)
+        return fail(SAMNERF_ELAUNCH, "sgrid_backward_det: header reset failed");
+    k_sgrid_det_max<<<div_up((uint64_t)N * 32u, 256), 256, 0, s>>>(grad_fsam, N, kRow, hdr);
+    k_sgrid_backward<32, true><<<dim3(div_up((uint64_t)N * 8, 256), 16, 1), 256, 0, s>>>(
+        N, make_ray_tiles(N, m->view_width), gs, w.u_f, w.w_f, grad_fsam, kRow, grad_embeddings, 0u, 0u, det);
+    k_sgrid_det_finish<<<2048, 256, 0, s>>>(det, grad_embeddings, n);
+    return check_launch("sgrid_backward_det");
 }
 
 int samnerf_sgrid_backward(const samnerf_model* m, const float* grad_fsam, uint32_t N,

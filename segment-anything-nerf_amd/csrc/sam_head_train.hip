@@ -337,6 +337,8 @@ struct DwArgs {
     const float* lnpart;    // [blocks][512] from k_ht_bwd
     uint32_t N, Np, chunks; // chunks of 256 rays
     uint32_t blocks;        // k_ht_bwd workgroups
+    uint32_t parts;         // partial sums per output: min(chunks, kDwParts)
+    float* slab;            // [parts][kDwTiles][32 x 32] | [parts][5][256] bias | [parts][512] LN
     float* gw[5];           // weight gradients [256][K_l] (accumulated)
     float* gb[5];           // bias gradients (accumulated)
     float* gln_w;
@@ -351,73 +353,125 @@ __host__ __device__ constexpr int dw_items_before(int l) {
 }
 constexpr int kDwTiles = dw_items_before(5);              // 352 output tiles of 32 x 32
 
-// dW_l[u][k] += sum over a chunk of 256 rays of G_l[u][r] X_l[k][r]; one wave
-// per (output tile, chunk).  The sum runs over rays, so the rays of an
-// MFMA's k pair can be any two: lane half h of group m takes rays
+// dW_l[u][k] = sum over the rays of G_l[u][r] X_l[k][r], in a FIXED order
+// (round 5: the gradients of a step repeat bit for bit -- the round-2..4 form
+// added each 256-ray chunk's tile with float atomics, in whatever order the
+// waves finished).  One wave per (output tile, part): part p sums chunks p,
+// p + parts, .. in order into its accumulators and stores the tile to the
+// slab; k_ht_dw_sum adds the parts in order.  The sum runs over rays, so the
+// rays of an MFMA's k pair can be any two: lane half h of group m takes rays
 // c0 + 8m + 4h .. +3 over four MFMAs, one 16-B load per operand.  The waves
 // of the first column tile (kt 0) also sum their G rows: the bias gradient.
-// After the tiles, 8 waves per chunk add the chunk's 16 LN partials.
+// After the tiles, 8 waves per part sum the part's LN partials.
+constexpr uint32_t kDwParts = 16;
+constexpr size_t kDwSlabTile = (size_t)kDwTiles * 1024;   // floats per part: the weight tiles
+__host__ __device__ constexpr size_t dw_slab_floats(uint32_t parts) {
+    return (size_t)parts * (kDwSlabTile + 5 * 256 + 512);
+}
+
 __global__ void __launch_bounds__(256) k_ht_dw(DwArgs a) {
     const uint32_t item = blockIdx.x * 4u + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
-    if (item >= (uint32_t)kDwTiles * a.chunks) {
-        const uint32_t e = item - (uint32_t)kDwTiles * a.chunks;
-        if (e >= 8u * a.chunks) return;
-        const uint32_t chunk = e >> 3, v = ((e & 7u) << 6) + (uint32_t)lane;       // v: 0..511
-        const uint32_t b0 = chunk * (256u / kRays), b1 = min(b0 + 256u / kRays, a.blocks);
+    float* const sbias = a.slab + (size_t)a.parts * kDwSlabTile;       // [parts][5][256]
+    float* const sln = sbias + (size_t)a.parts * 5 * 256;              // [parts][512]
+    if (item >= (uint32_t)kDwTiles * a.parts) {
+        const uint32_t e = item - (uint32_t)kDwTiles * a.parts;
+        if (e >= 8u * a.parts) return;
+        const uint32_t part = e >> 3, v = ((e & 7u) << 6) + (uint32_t)lane;       // v: 0..511
         float sum = 0.0f;
-        for (uint32_t b = b0; b < b1; ++b) sum += a.lnpart[(size_t)b * 512 + v];
-        atomicAdd(v < 256u ? a.gln_w + v : a.gln_b + (v - 256u), sum);
+        for (uint32_t chunk = part; chunk < a.chunks; chunk += a.parts) {
+            const uint32_t b0 = chunk * (256u / kRays), b1 = min(b0 + 256u / kRays, a.blocks);
+            for (uint32_t b = b0; b < b1; ++b) sum += a.lnpart[(size_t)b * 512 + v];
+        }
+        sln[(size_t)part * 512 + v] = sum;
         return;
     }
-    const uint32_t tile = item % kDwTiles, chunk = item / kDwTiles;
+    const uint32_t tile = item % kDwTiles, part = item / kDwTiles;
     int l = 0;
     while (l < 4 && (int)tile >= dw_items_before(l + 1)) ++l;
     const int lt = (int)tile - dw_items_before(l);
     const int ut = lt / kDwTilesK[l], kt = lt % kDwTilesK[l];
-    const uint32_t c0 = chunk * 256u;
     const int u = 32 * ut + i, kk = 32 * kt + i;           // A row (unit) / B column (input) of this lane
-    const float* Ga = a.G + ((size_t)l * 256 + u) * a.Np + c0 + 4 * h;
     // B source: saved activations (unit-major, ray-contiguous) or the rows
     const bool from_x = (l == 0) || (l == 2 && kk >= 256);
     const int xc = l == 0 ? kk : kk - 256;                  // x column for from_x
     const bool xok = xc < kIn;
-    const float* Hb = (l == 0 || from_x) ? nullptr
-                                         : a.hsave + ((size_t)(l - 1) * 256 + kk) * a.Np + c0 + 4 * h;
     f32x16 acc = {};
     float bsum = 0.0f;
-    for (int m = 0; m < 32; ++m) {
-        const float4 ga = *reinterpret_cast<const float4*>(Ga + 8 * m);
-        if (kt == 0) bsum += (ga.x + ga.y) + (ga.z + ga.w);
-        float xb[4];
-        if (from_x) {
+    for (uint32_t chunk = part; chunk < a.chunks; chunk += a.parts) {
+        const uint32_t c0 = chunk * 256u;
+        const float* Ga = a.G + ((size_t)l * 256 + u) * a.Np + c0 + 4 * h;
+        const float* Hb = (l == 0 || from_x) ? nullptr
+                                             : a.hsave + ((size_t)(l - 1) * 256 + kk) * a.Np + c0 + 4 * h;
+        for (int m = 0; m < 32; ++m) {
+            const float4 ga = *reinterpret_cast<const float4*>(Ga + 8 * m);
+            if (kt == 0) bsum += (ga.x + ga.y) + (ga.z + ga.w);
+            float xb[4];
+            if (from_x) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t ray = c0 + 8u * m + 4u * h + e;
-                xb[e] = (xok && ray < a.N) ? a.rows[(size_t)ray * kRowIn + xc] : 0.0f;
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t ray = c0 + 8u * m + 4u * h + e;
+                    xb[e] = (xok && ray < a.N) ? a.rows[(size_t)ray * kRowIn + xc] : 0.0f;
+                }
+            } else {
+                const float4 hb = *reinterpret_cast<const float4*>(Hb + 8 * m);
+                xb[0] = hb.x; xb[1] = hb.y; xb[2] = hb.z; xb[3] = hb.w;
             }
-        } else {
-            const float4 hb = *reinterpret_cast<const float4*>(Hb + 8 * m);
-            xb[0] = hb.x; xb[1] = hb.y; xb[2] = hb.z; xb[3] = hb.w;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.x, xb[0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.y, xb[1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.z, xb[2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.w, xb[3], acc, 0, 0, 0);
         }
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.x, xb[0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.y, xb[1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.z, xb[2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ga.w, xb[3], acc, 0, 0, 0);
     }
     if (kt == 0) {
-        bsum += __shfl_xor(bsum, 32);
-        if (h == 0) atomicAdd(a.gb[l] + u, bsum);
+        bsum = sum_halves(bsum);
+        if (h == 0) sbias[((size_t)part * 5 + l) * 256 + u] = bsum;
     }
     // acc register q of lane (col i, half h) = dW[32ut + (q & 3) + 8 (q >> 2) + 4h][32kt + i]
-    const int col = 32 * kt + i;
-    if (kcol(l, col) < 0) return;
+    float* const st = a.slab + ((size_t)part * kDwTiles + tile) * 1024;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int row = 32 * ut + (q & 3) + 8 * (q >> 2) + 4 * h;
-        atomicAdd(a.gw[l] + (size_t)row * kKl[l] + col, acc[q]);
+    for (int q = 0; q < 16; ++q) st[((q & 3) + 8 * (q >> 2) + 4 * h) * 32 + i] = acc[q];
+}
+
+// the parts of every weight / bias / LN gradient added in part order into
+// the (zeroed) gradients: one thread per output value
+__global__ void __launch_bounds__(256) k_ht_dw_sum(DwArgs a) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t base = 0;
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        const uint32_t n = 256u * (uint32_t)kKl[l];
+        if (t >= base && t < base + n) {
+            const uint32_t row = (t - base) / (uint32_t)kKl[l], col = (t - base) % (uint32_t)kKl[l];
+            // padded input column of logical column col (layer 0: the same; layer 2: the same)
+            const uint32_t tile = (uint32_t)dw_items_before(l) + (row >> 5) * kDwTilesK[l] + (col >> 5);
+            const size_t off = (size_t)tile * 1024 + (row & 31u) * 32 + (col & 31u);
+            float sum = 0.0f;
+            for (uint32_t p = 0; p < a.parts; ++p) sum += a.slab[(size_t)p * kDwSlabTile + off];
+            a.gw[l][t - base] += sum;
+            return;
+        }
+        base += n;
+    }
+    const float* sbias = a.slab + (size_t)a.parts * kDwSlabTile;
+    if (t < base + 5u * 256u) {
+        const uint32_t l = (t - base) >> 8, u = (t - base) & 255u;
+        float sum = 0.0f;
+        for (uint32_t p = 0; p < a.parts; ++p) sum += sbias[((size_t)p * 5 + l) * 256 + u];
+        a.gb[l][u] += sum;
+        return;
+    }
+    base += 5u * 256u;
+    if (t < base + 512u) {
+        const uint32_t v = t - base;
+        const float* sln = sbias + (size_t)a.parts * 5 * 256;
+        float sum = 0.0f;
+        for (uint32_t p = 0; p < a.parts; ++p) sum += sln[(size_t)p * 512 + v];
+        if (v < 256u) a.gln_w[v] += sum;
+        else a.gln_b[v - 256u] += sum;
     }
 }
+constexpr uint32_t kDwOutputs = 256u * (163u + 256u + 419u + 256u + 256u) + 5u * 256u + 512u;
 
 struct Layout {
     float* wf;
@@ -426,6 +480,7 @@ struct Layout {
     float* stats;
     float* G;
     float* lnpart;
+    float* slab;            // k_ht_dw's partial sums (dw_slab_floats)
     uint32_t Np;
     size_t bytes;
 };
@@ -448,6 +503,7 @@ Layout carve(uint32_t N, void* base) {
     L.stats = take((size_t)2 * L.Np);
     L.G = take((size_t)5 * 256 * L.Np);
     L.lnpart = take((size_t)512 * div_up(N, kRays));
+    L.slab = take(dw_slab_floats(std::min<uint32_t>(L.Np / 256u, kDwParts)));
     L.bytes = off;
     return L;
 }
@@ -551,7 +607,10 @@ int samnerf_head_train_backward(const samnerf_model* m, const float* rows, const
     }
     d.gln_w = grad_ln_w;
     d.gln_b = grad_ln_b;
-    k_ht_dw<<<div_up((uint64_t)(kDwTiles + 8) * d.chunks, 4), 256, 0, s>>>(d);
+    d.parts = std::min<uint32_t>(d.chunks, kDwParts);
+    d.slab = L.slab;
+    k_ht_dw<<<div_up((uint64_t)(kDwTiles + 8) * d.parts, 4), 256, 0, s>>>(d);
+    k_ht_dw_sum<<<div_up(kDwOutputs, 256), 256, 0, s>>>(d);
     return check_launch("head_train_backward (dW)");
 }
 

@@ -71,6 +71,9 @@ _SIGS = {
                                      _vp, _u32, _int, _vp, _vp, _sz, _vp], _int),
     "samnerf_sgrid_backward": ([ctypes.POINTER(SamnerfModel), _vp, _u32, _vp, _vp, _sz, _vp],
                                _int),
+    "samnerf_sgrid_accum_size": ([ctypes.POINTER(SamnerfModel)], _sz),
+    "samnerf_sgrid_backward_det": ([ctypes.POINTER(SamnerfModel), _vp, _u32, _vp, _vp, _vp, _sz, _vp],
+                                   _int),
     "samnerf_mask_forward": ([ctypes.POINTER(SamnerfModel), _u32, _vp, _vp, _sz, _vp], _int),
     "samnerf_tile_words": ([], _u32),
     "samnerf_tile_encode": ([_vp, _vp, _vp, _vp, _u32, _vp, _vp], _int),

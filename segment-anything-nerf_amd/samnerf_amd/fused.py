@@ -84,8 +84,14 @@ class FusedRenderer:
     samnerf_hip.h).  Unset, both follow the network's head_mode / t_thresh
     attributes (NeRFRenderer, defaults 0)."""
 
-    def __init__(self, net, head_mode=None, t_thresh=None):
+    def __init__(self, net, head_mode=None, t_thresh=None, deterministic=False):
+        """deterministic=True: the s_grid gradient of the distillation step
+        (sgrid_backward) sums in 64-bit fixed point (samnerf_sgrid_backward_det,
+        SURVEY H5) so identical steps give identical bits; the default is the
+        reference's unordered fp32 atomics."""
         self.net = net
+        self.deterministic = bool(deterministic)
+        self._accum = None
         self._ws = None
         self._keep = []
         self._model = None
@@ -385,6 +391,14 @@ class FusedRenderer:
         N = grad_rows.shape[0]
         grad_rows = grad_rows.contiguous()
         assert grad_rows.shape[1] == ROW
+        if self.deterministic:
+            size = lib().samnerf_sgrid_accum_size(ctypes.byref(m))
+            if self._accum is None or self._accum.numel() < size or self._accum.device != grad_rows.device:
+                self._accum = torch.zeros(max(size, 1), dtype=torch.uint8, device=grad_rows.device)
+            check(lib().samnerf_sgrid_backward_det(ctypes.byref(m), _ptr(grad_rows), N,
+                                                   _ptr(grad_embeddings), _ptr(self._accum), _ptr(ws), need,
+                                                   _stream(grad_rows)), "sgrid_backward_det")
+            return
         check(lib().samnerf_sgrid_backward(ctypes.byref(m), _ptr(grad_rows), N,
                                            _ptr(grad_embeddings), _ptr(ws), need,
                                            _stream(grad_rows)), "sgrid_backward")

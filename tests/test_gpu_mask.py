@@ -51,7 +51,7 @@ def test_mask_training_reduces_loss(hip_lib, cuda):
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
     assert losses[-1] < 0.5 * losses[0], losses
 
 

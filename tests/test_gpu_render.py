@@ -447,6 +447,31 @@ def test_final_slot_classes_bit_identical(hip_lib, cuda, monkeypatch, n, diag):
         assert torch.equal(outs[0][k], outs[2][k]), k
 
 
+@pytest.mark.parametrize("n", [70000, 9000])
+def test_prop_level_classes_bit_identical(hip_lib, cuda, monkeypatch, n, diag):
+    """k_prop_sigma with the reference proposal grids' level classes as
+    compile-time constants (DDDHH / DDHHH: the 5 levels' loads issued
+    together) against the run-time form (SAMNERF_PROP_LAY=0: one level's
+    loads at a time): every output and the proposal stages' tapped optical
+    depths, weights, bins and searchsorted indices, bit for bit."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer, ROW
+    spec = synth.ModelSpec(with_sam=True)
+    net = make_net(spec, synth.make_params(spec, seed=41, emb_scale=0.5, ln_jitter=0.1), cuda)
+    pose, intr = synth.gui_camera(512, 160, rot=synth.random_rotation(19))
+    ro, rd = ops.get_rays(pose, intr, 160, 512, device=cuda)
+    fr = FusedRenderer(net)
+    outs = []
+    for lay in ("0", "1"):
+        monkeypatch.setenv("SAMNERF_PROP_LAY", lay)
+        rows = torch.empty(n, ROW, device=cuda)
+        o = fr.render(ro[:n], rd[:n], rows=rows, taps=True)
+        o["rows"] = rows
+        outs.append({k: v.cpu() for k, v in o.items()})
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+
+
 def test_fused_render_from_reference_layout_checkpoint(hip_lib, cuda, tmp_path):
     """SURVEY 8f-1 on the device: a model-only checkpoint in the reference's
     layout (utils.py:2046-2074; save_checkpoint writes {epoch, global_step,

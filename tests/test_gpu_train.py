@@ -52,7 +52,8 @@ def test_fused_sgrid_backward_matches_autograd(hip_lib, cuda):
         assert err <= 2e-3 * max(scale, 1e-3), f"{k}: {err} vs scale {scale}"
 
 
-def test_distillation_step_matches_cpu_twin_full_tables(hip_lib, cuda):
+@pytest.mark.parametrize("det", [False, True])
+def test_distillation_step_matches_cpu_twin_full_tables(hip_lib, cuda, det):
     """BASELINE config 5 at the reference's table sizes (s_grid 2^19 rows per
     hashed level, 5,258,512 rows x 8; 4096 rays of a 64x64 camera): the fused
     forward + HIP s_grid scatter + head backward on the GPU against the
@@ -62,7 +63,8 @@ def test_distillation_step_matches_cpu_twin_full_tables(hip_lib, cuda):
     Loss to fp32 rounding; at the same resampled bins, gradients of
     s_grid.embeddings and every samvit_mlp tensor within 1e-4 relative (norm):
     float atomics, GPU vs CPU GEMM order, f16x3 grid_mlp forward
-    (fp32-equivalent)."""
+    (fp32-equivalent).  det: the s_grid scatter in the deterministic mode
+    (samnerf_sgrid_backward_det, 64-bit fixed point)."""
     from oracle import renderer as orc
     from oracle_backend import injected_bins, oracle_encoders
     from samnerf_amd.fused import FusedRenderer
@@ -77,7 +79,8 @@ def test_distillation_step_matches_cpu_twin_full_tables(hip_lib, cuda):
     pose, intr = synth.gui_camera(64, 64, rot=synth.random_rotation(10))
     ro, rd = orc.get_rays(pose, intr, 64, 64)
     gt = torch.randn(1, 256, 64, 64, generator=torch.Generator().manual_seed(1))
-    _, lg = sam_train_step(FusedRenderer(nets["gpu"]), ro.to(cuda), rd.to(cuda), 64, 64, gt.to(cuda))
+    _, lg = sam_train_step(FusedRenderer(nets["gpu"], deterministic=det), ro.to(cuda), rd.to(cuda), 64, 64,
+                           gt.to(cuda))
     lg.backward()
     # the twin samples at the fused path's resampled bins (an ulp of a sample
     # position moves the fine levels' gradients: tests/test_gpu_rgb_train.py)
@@ -142,6 +145,76 @@ def test_sgrid_backward_box_matches_per_corner(hip_lib, cuda, monkeypatch, diag)
         mx = ((a - b).abs().max() / b.abs().max()).item()
         print(mode, "vs per-corner scatter:", rel, mx)
         assert rel < 1e-5 and mx < 1e-5, (mode, rel, mx)
+
+
+def test_sgrid_backward_deterministic_mode(hip_lib, cuda):
+    """the deterministic s_grid scatter (samnerf_sgrid_backward_det:
+    64-bit fixed-point integer atomics, associative) gives the same bits on
+    every call, and the fp32-atomic scatter's values to 1e-5 of the tensor
+    (norm and max), on the full-size table with a 64x64 view plus 1000
+    scattered rays; its accumulator is left zero."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer, ROW
+    spec = synth.ModelSpec(with_sam=True)
+    net = make_net(spec, synth.make_params(spec, seed=9, emb_scale=0.5, ln_jitter=0.1), cuda)
+    pose, intr = synth.gui_camera(64, 64, rot=synth.random_rotation(14))
+    ro, rd = ops.get_rays(pose, intr, 64, 64, device=cuda)
+    perm = torch.randperm(4096, generator=torch.Generator().manual_seed(1)).to(cuda)
+    ro = torch.cat([ro, ro[perm[:1000]]]).contiguous()
+    rd = torch.cat([rd, rd[perm[:1000]]]).contiguous()
+    N = ro.shape[0]
+    fr = FusedRenderer(net, deterministic=True)
+    rows = torch.empty(N, ROW, device=cuda)
+    ws = fr.render(ro, rd, rows=rows, keep_workspace=True, feats=False, own_workspace=True)["_workspace"]
+    g = torch.randn(N, ROW, device=cuda, generator=torch.Generator(device=cuda).manual_seed(2))
+    dets = []
+    for _ in range(3):
+        ge = torch.zeros_like(net.s_grid.embeddings)
+        fr.sgrid_backward(g, ws, ge)
+        dets.append(ge)
+    n = net.s_grid.embeddings.numel() * 8
+    assert not fr._accum[:n].any()                          # left zero for the next call
+    fr.deterministic = False
+    ref = torch.zeros_like(net.s_grid.embeddings)
+    fr.sgrid_backward(g, ws, ref)
+    for d in dets[1:]:
+        assert torch.equal(d, dets[0])
+    rel = ((dets[0] - ref).norm() / ref.norm()).item()
+    mx = ((dets[0] - ref).abs().max() / ref.abs().max()).item()
+    print("deterministic vs fp32-atomic scatter:", rel, mx, int((ref != 0).sum()))
+    # the fp32 atomics round every add in whatever order the waves reach a
+    # row; the fixed-point totals are exact sums rounded once: they differ
+    # at the atomic form's own order noise (measured 6.9e-7 / 1.6e-6)
+    assert (ref != 0).sum() > 10000 and rel < 1e-5 and mx < 1e-5, (rel, mx)
+
+
+def test_distillation_steps_repeat_bit_for_bit(hip_lib, cuda):
+    """Two identical config-5 steps (fused render, HIP head forward /
+    backward, deterministic s_grid scatter) give identical gradients, bit
+    for bit, for all 13 trained tensors: the head's dW sums its 256-ray
+    chunks in a fixed order (k_ht_dw + k_ht_dw_sum) and the s_grid scatter
+    runs in the deterministic mode."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer
+    from samnerf_amd.train import sam_train_step
+    spec = synth.ModelSpec(with_sam=True)
+    net = make_net(spec, synth.make_params(spec, seed=7, emb_scale=0.5, ln_jitter=0.1), cuda)
+    net.train()
+    for k, p in net.named_parameters():
+        p.requires_grad = k.startswith("s_grid") or k.startswith("samvit_mlp")
+    pose, intr = synth.gui_camera(64, 64, rot=synth.random_rotation(10))
+    ro, rd = ops.get_rays(pose, intr, 64, 64, device=cuda)
+    gt = torch.randn(1, 256, 64, 64, device=cuda, generator=torch.Generator(device=cuda).manual_seed(1))
+    fr = FusedRenderer(net, deterministic=True)
+    grads = []
+    for _ in range(2):
+        net.zero_grad(set_to_none=True)
+        _, loss = sam_train_step(fr, ro, rd, 64, 64, gt)
+        loss.backward()
+        grads.append({k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None})
+    assert len(grads[0]) == 13
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k
 
 
 @pytest.mark.parametrize("n", [4096, 1000, 37])
