@@ -1654,6 +1654,16 @@ constexpr uint32_t kBoxSlots = 256;          // 32 B slots per wave (8 KiB)
 // the corner-row stores, its own instantiation because the tap code raised the
 // product form's spills (20 -> 60 bytes of scratch at 4 waves per SIMD); the
 // tapped render's outputs are checked bit-identical to the product's.
+// SGRID_UNI (round 5): a level whose box is one cell for the whole wave
+// reads that cell's 8 corner rows through the scalar cache
+// (lookup_level3_uniform) -- the coarse levels, where a wave's 64 neighbouring
+// rays at one sample share a cell most of the time; the box path's LDS reads
+// (8 corners x 32 B per lane) bound the kernel
+#ifndef SAMNERF_SGRID_UNI
+#define SAMNERF_SGRID_UNI 1
+#endif
+constexpr bool SGRID_UNI = SAMNERF_SGRID_UNI;
+
 template <int T, bool TAP = false>
 __global__ void __launch_bounds__(256)
 #if SAMNERF_DIAG_SGRID_WAVES
@@ -1729,7 +1739,21 @@ k_sgrid_box4(SgridArgs a) {
                 uint32_t* rt = nullptr;                     // parity taps only
                 if (TAP && live && r % a.tap_stride == 0u)
                     rt = a.rows_tap + ((size_t)(r / a.tap_stride) * T + k) * 128u + (4 * g + l) * 8;
-                if (b.slots <= kBoxSlots) {
+                if (SGRID_UNI && b.uni && ordered) {
+                    // one cell for the whole wave: its 8 corner rows through the
+                    // scalar cache, no box staging, no LDS reads (round 5)
+                    const uint32_t dx = b.ex - 1u, dy = b.ey - 1u, dz = b.ez - 1u;
+                    uint32_t rows[8];
+#pragma unroll
+                    for (int c = 0; c < 8; ++c)
+                        rows[c] = dense_or_hash_row(b.x0 + (c & 1) * dx, b.y0 + ((c >> 1) & 1) * dy,
+                                                    b.z0 + (c >> 2) * dz, L[l]);
+                    if (rt) {
+#pragma unroll
+                        for (int c = 0; c < 8; ++c) rt[c] = rows[c];
+                    }
+                    lookup_level3_uniform<8>(a.grid.emb, L[l], rows, ux, uy, uz, f);
+                } else if (b.slots <= kBoxSlots) {
                     wave_lds_sync();                        // previous level's reads done
                     stage_pbox<8>(base, L[l], b, slice, lane);
                     wave_lds_sync();

@@ -161,6 +161,7 @@ __device__ __forceinline__ uint32_t log2_ceil(uint32_t v) { return v <= 1u ? 0u 
 
 struct PBox {
     uint32_t x0, y0, z0, ex, ey, ez, lx, ly, slots;
+    uint32_t uni;          // every lane's position in the one cell (x0, y0, z0): the box is its corners
 };
 
 // Packed per-lane form: p0 = x0 | y0 << 10 | z0 << 20, p1 = ex | ey << 10 |
@@ -170,13 +171,14 @@ __device__ __forceinline__ void pbox_lane(const LevelDesc& d, const URange& u, u
                                           uint32_t& p1, uint32_t& p2) {
     const uint32_t top = d.res - 1u;
     const uint32_t x0 = cell_of(u.lo[0], d), y0 = cell_of(u.lo[1], d), z0 = cell_of(u.lo[2], d);
-    const uint32_t x1 = min(cell_of(u.hi[0], d) + 1u, top);
-    const uint32_t y1 = min(cell_of(u.hi[1], d) + 1u, top);
-    const uint32_t z1 = min(cell_of(u.hi[2], d) + 1u, top);
+    const uint32_t hx = cell_of(u.hi[0], d), hy = cell_of(u.hi[1], d), hz = cell_of(u.hi[2], d);
+    const uint32_t x1 = min(hx + 1u, top);
+    const uint32_t y1 = min(hy + 1u, top);
+    const uint32_t z1 = min(hz + 1u, top);
     const uint32_t ex = x1 - x0 + 1u, ey = y1 - y0 + 1u, ez = z1 - z0 + 1u;
     p0 = x0 | (y0 << 10) | (z0 << 20);
     p1 = ex | (ey << 10) | (ez << 20);
-    p2 = log2_ceil(ex) | (log2_ceil(ey) << 8);
+    p2 = log2_ceil(ex) | (log2_ceil(ey) << 8) | ((hx == x0 && hy == y0 && hz == z0) ? 1u << 16 : 0u);
 }
 
 __device__ __forceinline__ PBox pbox_read(uint32_t p0, uint32_t p1, uint32_t p2, int lane) {
@@ -191,7 +193,8 @@ __device__ __forceinline__ PBox pbox_read(uint32_t p0, uint32_t p1, uint32_t p2,
     r.ey = (b >> 10) & 1023u;
     r.ez = b >> 20;
     r.lx = c & 255u;
-    r.ly = c >> 8;
+    r.ly = (c >> 8) & 255u;
+    r.uni = c >> 16;
     r.slots = r.ez << (r.lx + r.ly);
     return r;
 }
@@ -244,6 +247,45 @@ __device__ __forceinline__ void tap_direct_rows(const LevelDesc& d, float ux, fl
     corner_rows<C>(d, ux, uy, uz, off, w);
 #pragma unroll
     for (int c = 0; c < 8; ++c) tap[c] = off[c] / (uint32_t)(C * 4) - d.off;
+}
+
+// lookup_level3 when every lane of the wave is in one cell (PBox::uni, no NaN
+// lane): the 8 corner rows are wave-uniform, so they are read once through
+// the scalar cache (s_load, no vector-memory or LDS traffic) and each lane
+// weights them with its own fractions -- the same rows (the top-clamped
+// corners of the cell), weights and FMA order as lookup_level3 (same bits).
+// row[c]: the level-relative row of corner c (wave-uniform).
+template <int C>
+__device__ __forceinline__ void lookup_level3_uniform(const float* __restrict__ emb, const LevelDesc& d,
+                                                      const uint32_t* row, float ux, float uy, float uz,
+                                                      float* acc) {
+    static_assert(C == 8, "uniform-cell lookup: C = 8 rows (32 B)");
+    uint32_t cx, cy, cz;
+    float fx, fy, fz;
+    locate_axis(ux, d, cx, fx);
+    locate_axis(uy, d, cy, fy);
+    locate_axis(uz, d, cz, fz);
+    f2v wc[4];
+    corner_weights_pk(fx, fy, fz, wc);
+    f2v a[C / 2];
+#pragma unroll
+    for (int i = 0; i < C / 2; ++i) a[i] = f2v{0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const float4* p = reinterpret_cast<const float4*>(emb + (size_t)(d.off + row[c]) * C);
+        const float4 v0 = p[0], v1 = p[1];
+        const float w = corner_w(wc, c);
+        const f2v wv = {w, w};
+        a[0] = __builtin_elementwise_fma(wv, f2v{v0.x, v0.y}, a[0]);
+        a[1] = __builtin_elementwise_fma(wv, f2v{v0.z, v0.w}, a[1]);
+        a[2] = __builtin_elementwise_fma(wv, f2v{v1.x, v1.y}, a[2]);
+        a[3] = __builtin_elementwise_fma(wv, f2v{v1.z, v1.w}, a[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < C / 2; ++i) {
+        acc[2 * i] = a[i].x;
+        acc[2 * i + 1] = a[i].y;
+    }
 }
 
 // lookup_level3 from a staged padded box (same rows, weights, FMA order);
