@@ -519,6 +519,15 @@ int samnerf_set_taps(const samnerf_taps* taps, uint32_t N);
  * events = NULL disables it.  Thread-local; costs one hipEventRecord per stage. */
 int samnerf_set_stage_events(void* const* events, uint32_t n);
 
+/* Test hook: the compiled kernel forms the last samnerf_render_forward(_tile)
+ * of this thread launched, so the tests can tell which specialisation ran.
+ * out[0] / out[1]: the proposal stages' level classes (dense-level mask |
+ * hashed-level mask << 8) when k_prop_sigma ran with them as compile-time
+ * constants, 0 for the run-time form; out[2]: k_final's layout (1 = the
+ * reference grid's compile-time slot layout, 0 = run-time); out[3] reserved.
+ * Writes min(n, 4) entries, returns 4.  Thread-local, no GPU work. */
+int samnerf_last_forms(uint32_t* out, uint32_t n);
+
 #ifdef __cplusplus
 }
 #endif

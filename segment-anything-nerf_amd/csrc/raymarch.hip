@@ -231,8 +231,15 @@ constexpr uint32_t kPropBoxSlots = 128;      // rows per level slice (8 B each)
 template <uint32_t KD, uint32_t KH>
 __device__ __forceinline__ void prop_lookup_lay(const PropArgs& a, float x, float y, float z, float* feat);
 
+#ifndef SAMNERF_PROP_WAVES
+#define SAMNERF_PROP_WAVES 0
+#endif
 template <int T, bool FIRST, int LOOK, uint32_t KD = 0, uint32_t KH = 0>
-__global__ void __launch_bounds__(256) k_prop_sigma(PropArgs a) {
+__global__ void __launch_bounds__(256)
+#if SAMNERF_PROP_WAVES
+__attribute__((amdgpu_waves_per_eu(SAMNERF_PROP_WAVES, SAMNERF_PROP_WAVES)))
+#endif
+k_prop_sigma(PropArgs a) {
     static_assert(T % 4 == 0, "T must be a multiple of 4");
     constexpr uint32_t Q = T / 4;
     const uint32_t b = blockIdx.x, i = b >> 3;
@@ -872,12 +879,87 @@ __device__ __forceinline__ void gather_levels_c2(const float2* __restrict__ emb,
 
 // k_prop_sigma's lookup with compile-time level classes (KD / KH): the 5
 // levels' loads issued together, then the packed corner sums
+// PROP_UNI (round 5): a dense level whose cell is the same for all the
+// wave's lanes (the coarse proposal levels: 64 neighbouring rays at one
+// sample) reads its 4 corner pairs once through the scalar cache instead of
+// 4 vector gathers -- the proposal stages are bound by the vector-memory
+// address path.  Same rows, weights and FMA order (same bits).
+#ifndef SAMNERF_PROP_UNI
+#define SAMNERF_PROP_UNI 1
+#endif
+
 template <uint32_t KD, uint32_t KH>
 __device__ __forceinline__ void prop_lookup_lay(const PropArgs& a, float x, float y, float z, float* feat) {
     const float ux = (x + a.gs.bound) * a.gs.inv_b2, uy = (y + a.gs.bound) * a.gs.inv_b2,
                 uz = (z + a.gs.bound) * a.gs.inv_b2;
+    if constexpr (!SAMNERF_PROP_UNI) {
+        GatherC2<5> g;
+        gather_issue_c2<5>(reinterpret_cast<const float2*>(a.grid.emb), a.grid.lv, ux, uy, uz, g,
+                           SlotKinds{KD, KH});
+        gather_finish_c2<5, true>(g, feat);
+        return;
+    }
+    const char* base = reinterpret_cast<const char*>(a.grid.emb);
+    const uint64_t live = __builtin_amdgcn_read_exec();
     GatherC2<5> g;
-    gather_issue_c2<5>(reinterpret_cast<const float2*>(a.grid.emb), a.grid.lv, ux, uy, uz, g, SlotKinds{KD, KH});
+    uint32_t row[5][8];
+    bool uni[5];
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        const LevelDesc& d = a.grid.lv[l];
+        uint32_t cx, cy, cz;
+        locate_axis(ux, d, cx, g.fx[l]);
+        locate_axis(uy, d, cy, g.fy[l]);
+        locate_axis(uz, d, cz, g.fz[l]);
+        const uint32_t top = d.res - 1u;
+        const uint32_t ny = min(cy + 1u, top), nz = min(cz + 1u, top);
+        uni[l] = false;
+        if ((KD >> l) & 1u) {
+            // one cell for every live lane (wave-uniform: a ballot)
+            const uint32_t c0 = __builtin_amdgcn_readfirstlane(cx), c1 = __builtin_amdgcn_readfirstlane(cy),
+                           c2 = __builtin_amdgcn_readfirstlane(cz);
+            uni[l] = __builtin_amdgcn_ballot_w64(cx == c0 && cy == c1 && cz == c2) == live;
+            const bool edge = cx == top;                   // gather_issue_c2's top-cell pair
+            g.fx[l] = edge ? 1.0f : g.fx[l];
+            const uint32_t bx = d.off + (edge ? cx - 1u : cx);
+            const uint32_t r2 = d.res * d.res;
+            const uint32_t Y[2] = {(uint32_t)__umul24(cy, d.res), (uint32_t)__umul24(ny, d.res)};
+            const uint32_t Z[2] = {(uint32_t)__umul24(cz, r2), (uint32_t)__umul24(nz, r2)};
+#pragma unroll
+            for (int p = 0; p < 4; ++p) row[l][p] = (bx + Y[p & 1] + Z[p >> 1]) << 3;
+        } else {
+            const uint32_t mask = d.size - 1u;
+            const uint32_t X[2] = {cx, min(cx + 1u, top)};
+            const uint32_t Y[2] = {cy * kPrime1, ny * kPrime1};
+            const uint32_t Z[2] = {cz * kPrime2, nz * kPrime2};
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                row[l][c] = (d.off + ((X[c & 1] ^ Y[(c >> 1) & 1] ^ Z[c >> 2]) & mask)) << 3;
+        }
+    }
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        if ((KD >> l) & 1u) {
+            if (uni[l]) {                                  // the scalar cache: wave-uniform rows
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const f4a8 v = *reinterpret_cast<const f4a8*>(base + __builtin_amdgcn_readfirstlane(row[l][p]));
+                    g.e[l][2 * p] = make_float2(v.x, v.y);
+                    g.e[l][2 * p + 1] = make_float2(v.z, v.w);
+                }
+            } else {
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const f4a8 v = *reinterpret_cast<const f4a8*>(base + row[l][p]);
+                    g.e[l][2 * p] = make_float2(v.x, v.y);
+                    g.e[l][2 * p + 1] = make_float2(v.z, v.w);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) g.e[l][c] = *reinterpret_cast<const float2*>(base + row[l][c]);
+        }
+    }
     gather_finish_c2<5, true>(g, feat);
 }
 
@@ -2173,6 +2255,10 @@ thread_local uint32_t g_n_stage_events = 0;
 thread_local samnerf_taps g_taps = {};
 thread_local uint32_t g_taps_n = 0;
 thread_local bool g_taps_on = false;
+// the compiled forms the last render of this thread launched
+// (samnerf_last_forms): [0] / [1] the proposal stages' level classes (KD |
+// KH << 8, 0 for the run-time form), [2] k_final's layout (final_layout)
+thread_local uint32_t g_last_forms[4] = {};
 
 void mark_stage(uint32_t i, hipStream_t s) {
     if (i < g_n_stage_events && g_stage_events[i]) (void)hipEventRecord(g_stage_events[i], s);
@@ -2237,7 +2323,9 @@ void launch_prop_sigma(int look, uint32_t N, hipStream_t s, const PropArgs& pa) 
         kh |= (pa.grid.lv[l].flags & kHashed) ? 1u << l : 0u;
     }
     const char* pl = diag_env("SAMNERF_PROP_LAY");
-    const bool lay = look == kLookPacked && pa.gs.inv_b2 != 0.0f && !(pl && atoi(pl) == 0);
+    const bool lay = (look == kLookPacked || look == kLookAuto) && pa.gs.inv_b2 != 0.0f && !(pl && atoi(pl) == 0);
+    const bool lay_ok = lay && ((kd == 0x07u && kh == 0x18u) || (kd == 0x03u && kh == 0x1Cu));
+    g_last_forms[T == 128 ? 0 : 1] = lay_ok ? kd | kh << 8 : 0u;
     if (lay && kd == 0x07u && kh == 0x18u) {
         k_prop_sigma<T, FIRST, kLookPacked, 0x07u, 0x18u><<<nb, 256, 0, s>>>(pa);
         return;
@@ -2375,6 +2463,7 @@ void launch_final_np(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa) {
 
 template <bool EXACT>
 void launch_final(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa, bool sa, int ad) {
+    g_last_forms[2] = 0u;
     if (ad) {                                            // adaptive mask heads: S = 1
         const uint32_t nb = xcd_blocks(div_up(N, 128));
         if (ad == 2) k_final<32, 1, EXACT, false, false, true, 2><<<nb, 256, 0, s>>>(fa);
@@ -2418,6 +2507,7 @@ void launch_final(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa, bool 
     // take the run-time layout)
     const bool tap = fa.sigma_tap || fa.rows_tap;
     const bool lay1 = final_layout(fa) == 1;
+    g_last_forms[2] = lay1 && (seg == 1 || !tap) ? 1u : 0u;
     const uint32_t nb1 = xcd_blocks(div_up(N, 128)), nb2 = xcd_blocks(div_up(N, 64)),
                    nb4 = xcd_blocks(div_up(N, 32));
     if (seg == 1) {
@@ -2939,6 +3029,11 @@ int samnerf_set_stage_events(void* const* events, uint32_t n) {
     for (uint32_t i = 0; i < g_n_stage_events; ++i)
         g_stage_events[i] = reinterpret_cast<hipEvent_t>(events[i]);
     return SAMNERF_OK;
+}
+
+int samnerf_last_forms(uint32_t* out, uint32_t n) {
+    for (uint32_t i = 0; out && i < n && i < 4; ++i) out[i] = g_last_forms[i];
+    return 4;
 }
 
 int samnerf_set_taps(const samnerf_taps* taps, uint32_t N) {

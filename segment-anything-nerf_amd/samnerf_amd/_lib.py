@@ -80,6 +80,7 @@ _SIGS = {
     "samnerf_tile_decode": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp], _int),
     "samnerf_set_stage_events": ([ctypes.POINTER(_vp), _u32], _int),
     "samnerf_set_taps": ([ctypes.c_void_p, _u32], _int),
+    "samnerf_last_forms": ([ctypes.c_void_p, _u32], _int),
     "samnerf_adam_step": ([ctypes.c_void_p, _u32, _f64, _f64, _f64, _f64, _f64, _u32, _vp], _int),
     "samnerf_rgb_train_workspace_size": ([ctypes.POINTER(SamnerfModel), _u32], _sz),
     "samnerf_rgb_train_step": ([ctypes.POINTER(SamnerfModel), _vp, _vp, _u32, _vp, _u32, _vp,

@@ -75,6 +75,15 @@ def ray_of_slots(N, view_width):
     return (trow * 4 + (inn >> 3)) * W + tcol * 8 + (inn & 7)
 
 
+def last_forms():
+    """The compiled kernel forms the calling thread's last render launched
+    (samnerf_last_forms): [prop0 level classes, prop1 level classes, k_final
+    layout, 0]; level classes = dense mask | hashed mask << 8, 0 = run-time."""
+    out = (ctypes.c_uint32 * 4)()
+    lib().samnerf_last_forms(out, 4)
+    return list(out)
+
+
 class FusedRenderer:
     """head_mode: 0 = f16x3 (each fp32 product of grid_mlp, the SAM head and
     the mask head as three fp16 MFMA products on power-of-two scaled operands:

@@ -428,7 +428,7 @@ def test_final_slot_classes_bit_identical(hip_lib, cuda, monkeypatch, n, diag):
     identical bits, on a view whose far samples reach the top cells of the
     coarse levels, at S = 1 / 2 / 4 segments (n = 70000 / 40000 / 9000)."""
     from samnerf_amd import ops
-    from samnerf_amd.fused import FusedRenderer, ROW
+    from samnerf_amd.fused import FusedRenderer, ROW, last_forms
     spec = synth.ModelSpec(with_sam=True)
     net = make_net(spec, synth.make_params(spec, seed=29, emb_scale=0.5, ln_jitter=0.1), cuda)
     pose, intr = synth.gui_camera(512, 160, rot=synth.random_rotation(17))
@@ -440,6 +440,7 @@ def test_final_slot_classes_bit_identical(hip_lib, cuda, monkeypatch, n, diag):
         monkeypatch.setenv("SAMNERF_FINAL_LAY", lay)
         rows = torch.empty(n, ROW, device=cuda)
         o = fr.render(ro[:n], rd[:n], rows=rows)
+        assert last_forms()[2] == int(lay)          # the form under test is the one that ran
         o["rows"] = rows
         outs.append(o)
     for k in outs[0]:
@@ -451,11 +452,12 @@ def test_final_slot_classes_bit_identical(hip_lib, cuda, monkeypatch, n, diag):
 def test_prop_level_classes_bit_identical(hip_lib, cuda, monkeypatch, n, diag):
     """k_prop_sigma with the reference proposal grids' level classes as
     compile-time constants (DDDHH / DDHHH: the 5 levels' loads issued
-    together) against the run-time form (SAMNERF_PROP_LAY=0: one level's
+    together; a dense level whose cell is wave-uniform read through the
+    scalar cache) against the run-time form (SAMNERF_PROP_LAY=0: one level's
     loads at a time): every output and the proposal stages' tapped optical
     depths, weights, bins and searchsorted indices, bit for bit."""
     from samnerf_amd import ops
-    from samnerf_amd.fused import FusedRenderer, ROW
+    from samnerf_amd.fused import FusedRenderer, ROW, last_forms
     spec = synth.ModelSpec(with_sam=True)
     net = make_net(spec, synth.make_params(spec, seed=41, emb_scale=0.5, ln_jitter=0.1), cuda)
     pose, intr = synth.gui_camera(512, 160, rot=synth.random_rotation(19))
@@ -466,6 +468,9 @@ def test_prop_level_classes_bit_identical(hip_lib, cuda, monkeypatch, n, diag):
         monkeypatch.setenv("SAMNERF_PROP_LAY", lay)
         rows = torch.empty(n, ROW, device=cuda)
         o = fr.render(ro[:n], rd[:n], rows=rows, taps=True)
+        # the form under test is the one that ran (round 5 found the
+        # specialisation unreachable from the render path)
+        assert last_forms()[:2] == ([0x1807, 0x1C03] if lay == "1" else [0, 0])
         o["rows"] = rows
         outs.append({k: v.cpu() for k, v in o.items()})
     for k in outs[0]:
@@ -609,3 +614,20 @@ def test_final_mode_forms_deterministic(hip_lib, cuda, form):
     ro, rd = ops.get_rays(pose, intr, 128, 256, device=cuda)
     fr = FusedRenderer(net, t_thresh=t)
     _twice_equal(lambda: fr.render(ro, rd, mask=mask, view_width=256))
+
+
+def test_product_runs_the_specialised_forms(hip_lib, cuda):
+    """The product library, on the headline configuration's grids (cfg 3:
+    proposal grids DDDHH / DDHHH, power-of-two grid scale, the reference's
+    16-level grid), launches the compile-time forms: k_prop_sigma with the
+    level classes as constants and k_final's LAY 1 -- at S = 1 and S = 2."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer, last_forms
+    spec = synth.ModelSpec(with_sam=True)
+    net = make_net(spec, synth.make_params(spec, seed=7), cuda)
+    pose, intr = synth.gui_camera(512, 160, rot=synth.random_rotation(3))
+    ro, rd = ops.get_rays(pose, intr, 160, 512, device=cuda)
+    fr = FusedRenderer(net)
+    for n in (81920, 40000):
+        fr.render(ro[:n], rd[:n])
+        assert last_forms() == [0x1807, 0x1C03, 1, 0], n

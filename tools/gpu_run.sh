@@ -7,6 +7,8 @@
 #   tests   pytest -m gpu (PYTEST_FILES, PYTEST_K narrow it)
 #   ab      tools/ab_libs.sh $AB_ROUNDS $AB_LIBS (interleaved library A/B on the headline view)
 #   bench   python bench.py $BENCH_ARGS (the driver's default line unless set)
+#   share   bench.py --rank-share $SHARE_N (8) at $SHARE_STREAMS (1 2 3) streams
+#   surface bench.py --scene surface (the opaque-sphere headline)
 #   prof    rocprofv3 --kernel-trace --stats of the headline (bench.py --no-alt --streams 1)
 #   pmc     tools/pmc_passes.sh (PASSES selects counter groups)
 # Logs go to gpurun_out/$TAG/.  Every GPU step runs under its own time limit;
@@ -44,6 +46,17 @@ fi
 if has bench; then
   step bench 400 python bench.py ${BENCH_ARGS:-} || exit 1
   tail -1 "$OUT/bench.log" | python -c "import json,sys; r=json.loads(sys.stdin.read()); print(r['value'], r['ms_per_step'], {k: round(v, 4) for k, v in r['stage_ms'].items()})"
+fi
+if has share; then   # one rank's band of the N = 8 split on this GPU, 1-3 streams
+  for s in ${SHARE_STREAMS:-1 2 3}; do
+    step share_s$s 200 python bench.py --rank-share ${SHARE_N:-8} --streams $s --no-alt --steps 60 --warmup 5 \
+      --cpu-rays 0 --ref-gpu-rays 0 || exit 1
+    tail -1 "$OUT/share_s$s.log" | python -c "import json,sys; r=json.loads(sys.stdin.read()); print('streams $s', r['ms_per_step'], {k: round(v, 4) for k, v in r['stage_ms'].items()})"
+  done
+fi
+if has surface; then
+  step surface 200 python bench.py --scene surface --no-alt --cpu-rays 0 --ref-gpu-rays 0 || exit 1
+  tail -1 "$OUT/surface.log" | python -c "import json,sys; r=json.loads(sys.stdin.read()); print('surface', r['ms_per_step'], {k: round(v, 4) for k, v in r['stage_ms'].items()})"
 fi
 if has prof; then
   cd /tmp && export TMPDIR=/tmp
