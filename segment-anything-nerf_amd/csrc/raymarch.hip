@@ -2464,11 +2464,22 @@ void launch_final_np(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa) {
 template <bool EXACT>
 void launch_final(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa, bool sa, int ad) {
     g_last_forms[2] = 0u;
+    // LAY 1 (the reference grid's compile-time slot layout) wherever the grid
+    // matches it and no taps are set; the taps' forms keep the run-time layout
+    const bool lay1 = final_layout(fa) == 1 && !fa.sigma_tap && !fa.rows_tap;
     if (ad) {                                            // adaptive mask heads: S = 1
         const uint32_t nb = xcd_blocks(div_up(N, 128));
-        if (ad == 2) k_final<32, 1, EXACT, false, false, true, 2><<<nb, 256, 0, s>>>(fa);
-        else if (sa) k_final<32, 1, EXACT, false, false, true, 1><<<nb, 256, 0, s>>>(fa);
-        else k_final<32, 1, EXACT, false, false, false, 1><<<nb, 256, 0, s>>>(fa);
+        g_last_forms[2] = lay1 ? 1u : 0u;
+        if (ad == 2) {
+            if (lay1) k_final<32, 1, EXACT, false, false, true, 2, 1, false><<<nb, 256, 0, s>>>(fa);
+            else k_final<32, 1, EXACT, false, false, true, 2><<<nb, 256, 0, s>>>(fa);
+        } else if (sa) {
+            if (lay1) k_final<32, 1, EXACT, false, false, true, 1, 1, false><<<nb, 256, 0, s>>>(fa);
+            else k_final<32, 1, EXACT, false, false, true, 1><<<nb, 256, 0, s>>>(fa);
+        } else {
+            if (lay1) k_final<32, 1, EXACT, false, false, false, 1, 1, false><<<nb, 256, 0, s>>>(fa);
+            else k_final<32, 1, EXACT, false, false, false, 1><<<nb, 256, 0, s>>>(fa);
+        }
         return;
     }
     if (sa) {                                            // --sum_after_mlp (RGB / mask models)
@@ -2477,7 +2488,12 @@ void launch_final(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa, bool 
         return;
     }
     if (fa.geo_out) {                                    // mask model: geo_feat per sample
-        launch_final_np<EXACT, false, true, false>(seg, N, s, fa);
+        if (seg == 1 && lay1) {
+            g_last_forms[2] = 1u;
+            k_final<32, 1, EXACT, false, true, false, 0, 1, false><<<xcd_blocks(div_up(N, 128)), 256, 0, s>>>(fa);
+        } else {
+            launch_final_np<EXACT, false, true, false>(seg, N, s, fa);
+        }
         return;
     }
     if (fa.exit_depth < INFINITY) {                      // N1 (no prefetch form)
@@ -2506,19 +2522,19 @@ void launch_final(int seg, uint32_t N, hipStream_t s, const FinalArgs& fa, bool 
     // set (S = 1 only: the taps' renders are whole views; S > 1 tapped renders
     // take the run-time layout)
     const bool tap = fa.sigma_tap || fa.rows_tap;
-    const bool lay1 = final_layout(fa) == 1;
-    g_last_forms[2] = lay1 && (seg == 1 || !tap) ? 1u : 0u;
+    const bool lay = final_layout(fa) == 1;
+    g_last_forms[2] = lay && (seg == 1 || !tap) ? 1u : 0u;
     const uint32_t nb1 = xcd_blocks(div_up(N, 128)), nb2 = xcd_blocks(div_up(N, 64)),
                    nb4 = xcd_blocks(div_up(N, 32));
     if (seg == 1) {
-        if (lay1 && !tap) k_final<32, 1, EXACT, false, false, false, 0, 1, false><<<nb1, 256, 0, s>>>(fa);
-        else if (lay1) k_final<32, 1, EXACT, false, false, false, 0, 1, true><<<nb1, 256, 0, s>>>(fa);
+        if (lay && !tap) k_final<32, 1, EXACT, false, false, false, 0, 1, false><<<nb1, 256, 0, s>>>(fa);
+        else if (lay) k_final<32, 1, EXACT, false, false, false, 0, 1, true><<<nb1, 256, 0, s>>>(fa);
         else k_final<32, 1, EXACT><<<nb1, 256, 0, s>>>(fa);
     } else if (seg == 2) {
-        if (lay1 && !tap) k_final<32, 2, EXACT, false, false, false, 0, 1, false><<<nb2, 256, 0, s>>>(fa);
+        if (lay && !tap) k_final<32, 2, EXACT, false, false, false, 0, 1, false><<<nb2, 256, 0, s>>>(fa);
         else k_final<32, 2, EXACT><<<nb2, 256, 0, s>>>(fa);
     } else {
-        if (lay1 && !tap) k_final<32, 4, EXACT, false, false, false, 0, 1, false><<<nb4, 256, 0, s>>>(fa);
+        if (lay && !tap) k_final<32, 4, EXACT, false, false, false, 0, 1, false><<<nb4, 256, 0, s>>>(fa);
         else k_final<32, 4, EXACT><<<nb4, 256, 0, s>>>(fa);
     }
 }

@@ -169,3 +169,37 @@ def test_fused_adaptive_density_matches_unfused_path(hip_lib, cuda, sum_after):
         scale = ref[k].abs().max().item()
         print("adaptive density", sum_after, k, err, scale)
         assert err < 1e-3 * max(1.0, scale), (k, err, scale)
+
+
+@pytest.mark.parametrize("kind", ["default", "adaptive_density", "adaptive_rgb_sum"])
+def test_mask_models_final_layout_bit_identical(hip_lib, cuda, monkeypatch, diag, kind):
+    """Mask models on k_final's compile-time layout of the reference grid (LAY 1:
+    the 'default' head's geo_feat form at S = 1, the adaptive heads' weighted-sum
+    forms) against the run-time layout (SAMNERF_FINAL_LAY=0): image, depth,
+    weights_sum and the instance logits bit for bit, on 70,000 rays of a
+    512-wide view (S = 1), the form under test asserted by samnerf_last_forms."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer, last_forms
+    if kind == "default":
+        spec = synth.ModelSpec(with_sam=False, with_mask=True, mask_type="default", n_inst=2,
+                               sum_after_mlp=False)
+    elif kind == "adaptive_density":
+        spec = synth.ModelSpec(with_sam=False, with_mask=True, mask_type="adaptive",
+                               adaptive_type="density", n_inst=4, sum_after_mlp=False)
+    else:
+        spec = synth.ModelSpec(with_sam=False, with_mask=True, mask_type="adaptive",
+                               adaptive_type="rgb", n_inst=4, sum_after_mlp=True)
+    net = make_net(spec, synth.make_params(spec, seed=17, emb_scale=0.5), cuda)
+    pose, intr = synth.gui_camera(512, 160, rot=synth.random_rotation(21))
+    ro, rd = ops.get_rays(pose, intr, 160, 512, device=cuda)
+    n = 70000
+    fr = FusedRenderer(net)
+    outs = []
+    for lay in ("0", "1"):
+        monkeypatch.setenv("SAMNERF_FINAL_LAY", lay)
+        with torch.no_grad():
+            o = fr.render(ro[:n], rd[:n], mask=True)
+        assert last_forms()[2] == int(lay)
+        outs.append({k: v.cpu() for k, v in o.items() if torch.is_tensor(v)})
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
