@@ -998,6 +998,432 @@ k_sam_head_h16q(HeadArgsH a, uint32_t ntiles) {
     }                                             // the DMA past the last tile drained
 }
 
+#ifndef SAMNERF_HEAD_W8
+#define SAMNERF_HEAD_W8 0
+#endif
+#if defined(SAMNERF_DIAG_VARIANTS) || SAMNERF_HEAD_W8
+// ============================================ f16x3, 16-ray waves, 2 per SIMD
+// The head at two waves per SIMD: one wave per SIMD
+// (k_sam_head_h16q) leaves the matrix pipe idle while the wave does its
+// layer-boundary VALU (bias, leaky_relu, column max, hi / lo split of 128
+// values per lane), its LDS reads and its step barrier, so the head sat at
+// ~0.4 of its MFMA issue rate.  Here a 128-ray tile is 8 waves of 16 rays on
+// v_mfma_f32_16x16x32_f16 (4 accumulator registers per 16 x 16 tile, 16 tiles
+// = the 256 units: 64 registers where the 32-ray form holds 128), so two
+// waves fit a SIMD's 512 registers and one wave's boundary work runs beside
+// the other wave's MFMAs.  The waves are independent (own rays, all 256
+// units): no exchange between them, only the shared weight stream.
+//
+// Orientation: out^T[16 units x 16 rays] per tile; A = weights (lane (i, g)
+// = unit 16 t + i, inputs 8 g .. 8 g + 7 of the 32-deep k-block), B =
+// activations (lane (j, g) = ray j, the same 8 inputs), D lane (j, g) =
+// units 16 t + 4 g + r (r = 0..3) of ray j.  A hidden layer's k-block b takes
+// D registers of tiles 2 b and 2 b + 1 -- input position 8 g + m of k-block b
+// is unit 32 b + 4 g + m (m < 4) or 32 b + 16 + 4 g + m - 4 -- so the weights
+// are packed permuted to match (w8_unit) and a layer's accumulators ARE the
+// next layer's B operands, as in the 32-ray form.
+//
+// Weight stream: a step = one 32-deep k-block x 8 of the 16 output tiles
+// (16 KiB of hi / lo fragments, [hi/lo][tile][lane]); 88 steps per tile (x
+// layers 6 k-blocks: 163 inputs padded to 192).  4-buffer ring by LDS DMA, two
+// 1-KiB pieces per wave and step, issued between the step's MFMAs; the tile's
+// rows come into LDS by DMA during steps 30 .. 40 of the previous tile (11
+// pieces per wave; the pieces past the 84-KiB x region go to a 1-KiB sink so
+// that every wave issues the same count -- the hand-counted vmcnt waits rely on
+// it).  The waves dispatched second take s_setprio 1 for the whole kernel
+// (MI355X_MICROARCH.md "Two waves per SIMD", item 4).
+//
+// Arithmetic: the same f16x3 products (power-of-two scaled operands, per-ray
+// column scales, per-tensor weight scales) over 32-deep instead of 16-deep
+// k-blocks: fp32-equivalent like the 32-ray form, not bit-identical to it (the
+// accumulation order differs; tests/test_gpu_render.py::
+// test_sam_head_w8_form_is_fp32_equivalent).
+//
+// Measured (round 5, profiles/r5l_head_forms.txt): the head alone, back to
+// back, 0.608 ms against 0.697 for k_sam_head_h16q (-13 %; the two
+// 4-wave-workgroups form 0.676); inside the view 0.54 against 0.565 ms, but
+// the view is not faster (2.856-2.890 against 2.851-2.866 ms): the stages
+// after the head run 2-4 % slower -- the chip is at its power limit through
+// the view (2.1-2.2 GHz), so a head that finishes sooner at the same MFMA and
+// more LDS work moves the clock, not the view.  The per-step barrier also
+// keeps the 8 waves in lockstep, so their layer boundaries coincide.  Kept for
+// the diagnostic build (forms 30 / 31) and SAMNERF_HEAD_W8 timing builds.
+namespace w8 {
+constexpr int kXkb = 6;                               // 163 inputs -> 6 k-blocks of 32
+constexpr int kHkb = 8;                               // 256 -> 8
+constexpr int kSegKb[6] = {kXkb, kHkb, kXkb, kHkb, kHkb, kHkb};
+constexpr int kSegLayer[6] = {0, 1, 2, 2, 3, 4};
+constexpr int segBase(int seg) {
+    int b = 0;
+    for (int i = 0; i < seg; ++i) b += kSegKb[i];
+    return b;
+}
+constexpr int kKb = segBase(6);                       // 44 k-blocks
+constexpr int kSteps = 2 * kKb;                       // 88: (k-block, half of the tiles)
+constexpr int kStepVec = 2 * 8 * 64;                  // uint4 per step
+constexpr int kPackedVec = kSteps * kStepVec;
+constexpr int kRays = 16;                             // per wave
+constexpr int kWaves = 8;
+constexpr int kXPieces = 11;                          // per wave and tile: 88 >= 82 KiB of rows
+constexpr int kXRegion = 84;                          // KiB of the x region
+constexpr int kXFirst = 30;                           // x pieces in steps 30 .. 40 (x last read before step 28)
+static_assert(kXPieces * kWaves * 1024 >= kTileBytes, "x pieces cover a tile");
+static_assert(kXRegion * 1024 >= kTileBytes && kXRegion * 1024 <= kXVec * 16, "x region");
+static_assert(kXFirst > 2 * (kXkb + kHkb) + 1 && kXFirst + kXPieces + 3 < kSteps, "x stream window");
+
+// the input of a hidden layer's k-block b at position 8 g + m (accumulator order)
+__host__ __device__ constexpr int hunit(int b, int g, int m) { return 32 * b + (m < 4 ? 4 * g + m : 16 + 4 * g + m - 4); }
+
+__device__ __forceinline__ float weight(const float* const* W, int kb, int unit, int g, int m) {
+    int seg = 0;
+    while (seg < 5 && kb >= segBase(seg + 1)) ++seg;
+    const int b = kb - segBase(seg);
+    const int kx = 32 * b + 8 * g + m;
+    switch (seg) {
+        case 0: return kx < kIn ? W[0][unit * kIn + kx] : 0.0f;
+        case 1: return W[1][unit * 256 + hunit(b, g, m)];
+        case 2: return kx < kIn ? W[2][unit * (256 + kIn) + 256 + kx] : 0.0f;
+        case 3: return W[2][unit * (256 + kIn) + hunit(b, g, m)];
+        case 4: return W[3][unit * 256 + hunit(b, g, m)];
+        default: return W[4][unit * 256 + hunit(b, g, m)];
+    }
+}
+}  // namespace w8
+
+// packed[step 88][hi/lo][tile 8][lane 64], then kexp[5]; a workgroup's 256
+// fragments are half a step (one layer), as k_pack_h16
+__global__ void __launch_bounds__(256) k_pack_w8(PackArgs a) {
+    __shared__ int kx;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int bstep = (int)((blockIdx.x * blockDim.x) >> 9);
+    int bseg = 0;
+    while (bseg < 5 && (bstep >> 1) >= w8::segBase(bseg + 1)) ++bseg;
+    const int layer = w8::kSegLayer[bseg];
+    if (threadIdx.x < 64) {
+        float m = threadIdx.x < kWmaxParts ? a.part[layer * kWmaxParts + threadIdx.x] : 0.0f;
+        m = wave_max64(m);
+        if (threadIdx.x == 0) {
+            kx = scale_exp_of_max(m);
+            a.kexp[layer] = kx;
+        }
+    }
+    __syncthreads();
+    if (t >= (uint32_t)w8::kSteps * 8u * 64u) return;
+    const int lane = (int)(t & 63u), tile = (int)((t >> 6) & 7u), step = (int)(t >> 9);
+    const int kb = step >> 1, unit = 16 * (8 * (step & 1) + tile) + (lane & 15), g = lane >> 4;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = w8::weight(a.W, kb, unit, g, e);
+    uint4 hi, lo;
+    split8_f16(v, exp2i(kx), hi, lo);
+    a.packed[(size_t)step * w8::kStepVec + tile * 64 + lane] = hi;
+    a.packed[(size_t)step * w8::kStepVec + 512 + tile * 64 + lane] = lo;
+}
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// C += A.B in f16x3 on the 16 x 16 x 32 form (small terms first)
+__device__ __forceinline__ floatx4 mfma16_f16x3(uint4 ah, uint4 al, uint4 bh, uint4 bl, floatx4 c) {
+    const f16x8 Ah = __builtin_bit_cast(f16x8, ah), Al = __builtin_bit_cast(f16x8, al);
+    const f16x8 Bh = __builtin_bit_cast(f16x8, bh), Bl = __builtin_bit_cast(f16x8, bl);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(Al, Bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, Bl, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, Bh, c, 0, 0, 0);
+}
+
+template <int NBUF, int WAVES>
+struct HeadStreamW8 {
+    static constexpr int kPieces = 16 / WAVES;          // 1-KiB weight pieces per wave and step
+    const uint4* packed;
+    uint4* Wb;                 // LDS ring [NBUF][kStepVec]
+    const char* rows;
+    const char* rows_end;      // their last 16 B
+    uint32_t xs;               // LDS byte address of the x region
+    uint32_t sink;             // LDS byte address of the 1-KiB sink
+    uint32_t next_tile;
+    int wave, lane;
+    int rot;
+    int step;
+
+    __device__ __forceinline__ int buf(int s) const {
+        const int b = rot + s % NBUF;
+        return b >= NBUF ? b - NBUF : b;
+    }
+    // piece c (0..1) of in-tile step s (s >= kSteps: the next tile's)
+    __device__ __forceinline__ void wpiece(int s, int c) {
+        const int o = wave * 64 * kPieces + c * 64;
+        const uint4* base = packed + (size_t)(s % w8::kSteps) * w8::kStepVec + (size_t)o;
+        lds_dma16(base + lane, (uint32_t)reinterpret_cast<uintptr_t>(Wb + buf(s) * w8::kStepVec + o));
+    }
+    __device__ __forceinline__ void xpiece(int q) {
+        const uint32_t p = (uint32_t)(wave * w8::kXPieces + q);
+        const char* src = rows + (size_t)next_tile * kTileBytes + (size_t)p * 1024u + (size_t)lane * 16u;
+        src = src > rows_end ? rows_end : src;
+        lds_dma16(src, p < (uint32_t)w8::kXRegion ? xs + p * 1024u : sink);
+    }
+    // the rows stream into LDS only in the 8-wave form (WAVES 4: read from global)
+    static __device__ __forceinline__ constexpr bool xstep(int s) {
+        return WAVES == 8 && s >= w8::kXFirst && s < w8::kXFirst + w8::kXPieces;
+    }
+
+    // k-block step s: tiles 8 HALF .. 8 HALF + 7 of the current layer
+    template <int HALF>
+    __device__ __forceinline__ void run(floatx4 (&acc)[16], const uint4& bh, const uint4& bl) {
+        const int s = step;
+        const uint4* cur = Wb + buf(s) * w8::kStepVec + lane;
+        uint4 fh[8], fl[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            fh[t] = cur[t * 64];
+            fl[t] = cur[512 + t * 64];
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            acc[8 * HALF + t] = mfma16_f16x3(fh[t], fl[t], bh, bl, acc[8 * HALF + t]);
+            if (t % (8 / kPieces) == 8 / kPieces - 1) {
+                __builtin_amdgcn_sched_barrier(0);
+                wpiece(s + NBUF - 1, t / (8 / kPieces));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (xstep(s)) {
+            __builtin_amdgcn_sched_barrier(0);
+            xpiece(s - w8::kXFirst);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // step s + 1 landed: younger than its pieces (issued in step s + 2 -
+        // NBUF) are the x pieces of steps s + 2 - NBUF .. s and the weight
+        // pieces of the steps after it
+        int n = kPieces * (NBUF - 2);
+#pragma unroll
+        for (int k = s + 2 - NBUF; k <= s; ++k) n += xstep(k) ? 1 : 0;
+        wait_vmn(n);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        ++step;
+    }
+};
+
+// a layer's accumulators back to fp32 values in place (times `inv`, + bias,
+// leaky_relu when `act`); returns the lane's max |value|
+__device__ __forceinline__ float finish_w8(floatx4 (&acc)[16], const float* Bs, float inv, int g, bool act) {
+    float m = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const float4 bb = *reinterpret_cast<const float4*>(Bs + 16 * t + 4 * g);
+        const float b4[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[t][r] = leaky(__builtin_fmaf(acc[t][r], inv, b4[r]), act);
+        m = max_abs3(m, acc[t][0], acc[t][1]);
+        m = max_abs3(m, acc[t][2], acc[t][3]);
+    }
+    return m;
+}
+
+// the values (times s) as the next layer's B operands: k-block b <- tiles 2 b, 2 b + 1
+__device__ __forceinline__ void split_w8(const floatx4 (&acc)[16], float s, uint4 (&ah)[w8::kHkb],
+                                         uint4 (&al)[w8::kHkb]) {
+#pragma unroll
+    for (int b = 0; b < w8::kHkb; ++b) {
+        const float v[8] = {acc[2 * b][0], acc[2 * b][1], acc[2 * b][2], acc[2 * b][3],
+                            acc[2 * b + 1][0], acc[2 * b + 1][1], acc[2 * b + 1][2], acc[2 * b + 1][3]};
+        split8_f16(v, s, ah[b], al[b]);
+    }
+}
+
+// max over the 4 lanes of a ray (j, j + 16, j + 32, j + 48)
+__device__ __forceinline__ float ray_max4(float m) {
+    m = fmaxf(m, __shfl_xor(m, 16));
+    return fmaxf(m, __shfl_xor(m, 32));
+}
+__device__ __forceinline__ double ray_sum4(double v) {
+    v += __shfl_xor(v, 16);
+    return v + __shfl_xor(v, 32);
+}
+
+constexpr int kW8SinkVec = 64;                        // uint4 of the 1-KiB sink
+
+// WAVES 8: one 512-thread workgroup per CU, 128-ray tiles, the rows by LDS
+// DMA.  WAVES 4: two independent 256-thread workgroups per CU (64-ray tiles,
+// LDS 71 KiB each, the rows read from global at the tile's start and at layer
+// 2): the two waves of a SIMD belong to different workgroups and drift out of
+// phase, so one's layer boundary can run under the other's MFMAs; the
+// weight stream is read twice per CU.
+template <int NBUF, int WAVES, bool VEC = true>
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_sam_head_w8(HeadArgsH a, uint32_t ntiles) {
+    constexpr bool XLDS = WAVES == 8;
+    constexpr int kTileRays = WAVES * w8::kRays;
+    constexpr int kX = XLDS ? kXVec + kW8SinkVec : 0;
+    __shared__ uint4 smem[NBUF * w8::kStepVec + kX + (7 * 256 + 8) / 4];
+    uint4* const Wb = smem;
+    float* const Xs = reinterpret_cast<float*>(smem + NBUF * w8::kStepVec);
+    float* const Bs = reinterpret_cast<float*>(smem + NBUF * w8::kStepVec + kX);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int j = lane & 15, g = lane >> 4;
+    if (XLDS && wave >= 4) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half, static
+
+    for (int i = tid; i < 5 * 256; i += 64 * WAVES) Bs[i] = a.b[i >> 8][i & 255];
+    float* const Wi = Bs + 7 * 256;                       // 2^-kexp[l]
+    if (tid < 5) Wi[tid] = exp2i(-a.kexp[tid]);
+    if (tid < 256) {
+        Bs[5 * 256 + tid] = a.ln_w[tid];
+        Bs[6 * 256 + tid] = a.ln_b[tid];
+    }
+
+    HeadStreamW8<NBUF, WAVES> st;
+    st.packed = a.packed;
+    st.Wb = Wb;
+    st.rows = reinterpret_cast<const char*>(a.rows);
+    st.rows_end = st.rows + (size_t)a.N * kRowIn * 4 - 16;
+    st.xs = (uint32_t)reinterpret_cast<uintptr_t>(Xs);
+    st.sink = (uint32_t)reinterpret_cast<uintptr_t>(smem + NBUF * w8::kStepVec + kXVec);
+    st.next_tile = blockIdx.x;
+    st.wave = __builtin_amdgcn_readfirstlane(wave);
+    st.lane = lane;
+    st.rot = 0;
+    st.step = 0;
+    if constexpr (XLDS) {
+#pragma unroll
+        for (int q = 0; q < w8::kXPieces; ++q) st.xpiece(q);
+    }
+#pragma unroll
+    for (int q = 0; q + 1 < NBUF; ++q)
+#pragma unroll
+        for (int c = 0; c < st.kPieces; ++c) st.wpiece(q, c);
+    wait_vmn(st.kPieces * (NBUF - 2));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        st.next_tile = tile + gridDim.x;
+        st.step = 0;
+        asm volatile("" : "+s"(st.packed), "+s"(st.rows));
+        const uint32_t ray = tile * kTileRays + wave * w8::kRays + j;
+        const bool live = ray < a.N;
+        // this lane's row: in LDS (WAVES 8) or global (a dead lane reads row 0)
+        const float* xr = XLDS ? Xs + (wave * w8::kRays + j) * kRowIn : a.rows + (size_t)(live ? ray : 0u) * kRowIn;
+        auto x8 = [&](int kb, float (&v)[8]) {
+            const int c0 = 32 * kb + 8 * g;
+            if (c0 + 8 <= kRowIn) {
+                const float4 p = *reinterpret_cast<const float4*>(xr + c0);
+                const float4 q = *reinterpret_cast<const float4*>(xr + c0 + 4);
+                v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w;
+                v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
+            } else {
+#pragma unroll
+                for (int m = 0; m < 8; ++m) v[m] = c0 + m < kRowIn ? xr[c0 + m] : 0.0f;
+            }
+#pragma unroll
+            for (int m = 0; m < 8; ++m)
+                if (!live || c0 + m >= kIn) v[m] = 0.0f;      // column 163 of a row is padding
+        };
+        float xmax = 0.0f;
+#pragma unroll
+        for (int kb = 0; kb < w8::kXkb; ++kb) {
+            float v[8];
+            x8(kb, v);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) xmax = fmaxf(xmax, fabsf(v[m]));
+        }
+        xmax = ray_max4(xmax);
+        uint4 xh[w8::kXkb], xl[w8::kXkb];
+        auto load_x = [&](float sc_s) {
+#pragma unroll
+            for (int kb = 0; kb < w8::kXkb; ++kb) {
+                float v[8];
+                x8(kb, v);
+                split8_f16(v, sc_s, xh[kb], xl[kb]);
+            }
+        };
+        Scale2 sc = scale_of_max(xmax);
+        load_x(sc.s);
+
+        floatx4 acc[16];
+        uint4 ah[w8::kHkb], al[w8::kHkb];
+        auto zero = [&]() {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) acc[t] = floatx4{};
+        };
+        auto next = [&](int layer, float extra) {
+            float m = finish_w8(acc, Bs + layer * 256, sc.inv * Wi[layer], g, true);
+            m = fmaxf(ray_max4(m), extra);
+            sc = scale_of_max(m);
+            split_w8(acc, sc.s, ah, al);
+        };
+        auto x_segment = [&]() {
+#pragma unroll
+            for (int kb = 0; kb < w8::kXkb; ++kb) {
+                st.template run<0>(acc, xh[kb], xl[kb]);
+                st.template run<1>(acc, xh[kb], xl[kb]);
+            }
+        };
+        auto h_segment = [&]() {
+#pragma unroll
+            for (int kb = 0; kb < w8::kHkb; ++kb) {
+                st.template run<0>(acc, ah[kb], al[kb]);
+                st.template run<1>(acc, ah[kb], al[kb]);
+            }
+        };
+
+        zero();                                               // layer 0: W0 . x
+        x_segment();
+        next(0, 0.0f);
+        zero();                                               // layer 1
+        h_segment();
+        next(1, xmax);                                        // layer 2 reads cat(h, x): one scale
+        zero();                                               // layer 2: W2 . cat(h, x)
+        load_x(sc.s);
+        x_segment();
+        h_segment();
+        next(2, 0.0f);
+        zero();                                               // layer 3
+        h_segment();
+        next(3, 0.0f);
+        zero();                                               // layer 4 (no activation)
+        h_segment();
+        finish_w8(acc, Bs + 4 * 256, sc.inv * Wi[4], g, false);
+
+        // LayerNorm(256, eps=1e-5)
+        double s = 0.0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s += (double)acc[t][r];
+        s = ray_sum4(s);
+        const double mean = s / 256.0;
+        double var = 0.0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double dlt = (double)acc[t][r] - mean;
+                var += dlt * dlt;
+            }
+        var = ray_sum4(var);
+        const float rstd = (float)(1.0 / sqrt(var / 256.0 + 1e-5));
+        const float mf = (float)mean;
+        if (live) {
+            float* o = a.out + (size_t)ray * a.ld;
+            const float* lw = Bs + 5 * 256;
+            const float* lb = Bs + 6 * 256;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const int u = 16 * t + 4 * g;
+                float4 y;
+                y.x = ((acc[t][0] - mf) * rstd) * lw[u + 0] + lb[u + 0];
+                y.y = ((acc[t][1] - mf) * rstd) * lw[u + 1] + lb[u + 1];
+                y.z = ((acc[t][2] - mf) * rstd) * lw[u + 2] + lb[u + 2];
+                y.w = ((acc[t][3] - mf) * rstd) * lw[u + 3] + lb[u + 3];
+                store_out4(o + u, y, VEC);
+            }
+        }
+        st.rot = (st.rot + w8::kSteps) % NBUF;
+    }
+    wait_vmn(0);                                          // the DMA past the last tile drained
+}
+#endif  // SAMNERF_DIAG_VARIANTS || SAMNERF_HEAD_W8
+
 #ifdef SAMNERF_DIAG_VARIANTS
 // ============================================================ f16x3, paired
 // The same arithmetic as k_sam_head_h16 (every accumulator tile sees the same
@@ -1291,15 +1717,61 @@ static int device_cus() {
     return cus[dev];
 }
 
+// the 16-ray two-waves-per-SIMD head (k_sam_head_w8): SAMNERF_HEAD_W8=1 / 2
+// at build time (timing builds), or diagnostic forms 30 / 31
+[[maybe_unused]] static int head_w8() {      // 0: k_sam_head_h16q, 1: 8-wave workgroups, 2: two 4-wave workgroups per CU
+#ifdef SAMNERF_DIAG_VARIANTS
+    const char* v = diag_env("SAMNERF_HEAD_V");
+    if (v) return atoi(v) == 30 ? 1 : atoi(v) == 31 ? 2 : 0;
+#endif
+    return SAMNERF_HEAD_W8;
+}
+
 size_t sam_head_packed_floats() {
     const size_t f32 = (size_t)8 * kTotalGroups * 64 * 4;
     const size_t h16 = (size_t)kPackedVec * 4 * kHeadCopies + 8 + 5 * kWmaxParts;   // fragment copies, log2 scales, partial maxima
-    return f32 > h16 ? f32 : h16;
+    const size_t hw8 = (size_t)88 * 1024 * 4 + 8 + 5 * kWmaxParts;   // k_sam_head_w8's 88 steps (diagnostic forms)
+    const size_t m = f32 > h16 ? f32 : h16;
+    return m > hw8 ? m : hw8;
 }
 
 int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, float* samvit,
                      float* packed, hipStream_t s, uint32_t ld) {
     const bool vec = ld % 4u == 0u && reinterpret_cast<uintptr_t>(samvit) % 16u == 0u;
+#if defined(SAMNERF_DIAG_VARIANTS) || SAMNERF_HEAD_W8
+    if (m->head_mode == 0 && head_w8()) {                        // f16x3, 16-ray waves
+        PackArgs p;
+        for (int i = 0; i < 5; ++i) p.W[i] = m->sam_w[i];
+        p.packed = reinterpret_cast<uint4*>(packed);
+        p.kexp = reinterpret_cast<int*>(packed + (size_t)w8::kPackedVec * 4);
+        p.part = packed + (size_t)w8::kPackedVec * 4 + 8;
+        k_head_wmax<<<dim3(kWmaxParts, 5), 256, 0, s>>>(p);
+        k_pack_w8<<<div_up((uint32_t)w8::kSteps * 8u * 64u, 256), 256, 0, s>>>(p);
+        HeadArgsH a{};
+        a.rows = rows;
+        a.N = N;
+        a.packed = p.packed;
+        a.kexp = p.kexp;
+        for (int i = 0; i < 5; ++i) a.b[i] = m->sam_b[i];
+        a.ln_w = m->ln_w;
+        a.ln_b = m->ln_b;
+        a.out = samvit;
+        a.ld = ld;
+        a.vec_out = vec;
+        if (head_w8() == 2) {                                    // two 64-ray workgroups per CU
+            const uint32_t blocks = div_up(N, 64u);
+            const uint32_t grid = blocks < 2u * (uint32_t)device_cus() ? blocks : 2u * (uint32_t)device_cus();
+            if (vec) k_sam_head_w8<4, 4><<<grid, 256, 0, s>>>(a, blocks);
+            else k_sam_head_w8<4, 4, false><<<grid, 256, 0, s>>>(a, blocks);
+        } else {
+            const uint32_t blocks = div_up(N, (uint32_t)kRaysV5);
+            const uint32_t grid = blocks < (uint32_t)device_cus() ? blocks : (uint32_t)device_cus();
+            if (vec) k_sam_head_w8<4, 8><<<grid, 512, 0, s>>>(a, blocks);
+            else k_sam_head_w8<4, 8, false><<<grid, 512, 0, s>>>(a, blocks);
+        }
+        return check_launch("sam_head_w8");
+    }
+#endif
     if (m->head_mode == 0) {                                     // f16x3 (default)
         PackArgs p;
         for (int i = 0; i < 5; ++i) p.W[i] = m->sam_w[i];

@@ -277,6 +277,48 @@ def test_sam_head_persistent_form_bit_identical(hip_lib, cuda, n):
     assert torch.equal(prod, tile)
 
 
+
+@pytest.mark.parametrize("form", ["30", "31"])
+@pytest.mark.parametrize("n", [1000, 128 * 300 + 37, 128 * 1024])
+def test_sam_head_w8_form_is_fp32_equivalent(hip_lib, cuda, n, form):
+    """The 16-ray two-waves-per-SIMD head (k_sam_head_w8, diagnostic forms 30:
+    one 8-wave workgroup per CU, 128-ray tiles; 31: two 4-wave workgroups per
+    CU, 64-ray tiles; v_mfma_f32_16x16x32_f16, 32-deep k-blocks) on
+    rows spanning 1e-4 .. 1e4 per ray: as close to the float64 head as the
+    exact fp32 MFMA head (within 2x), within 1e-6 of the product f16x3 head
+    relative to the output scale; ragged tails and several tiles per
+    workgroup (the rows streamed into LDS, the weight ring across tiles)."""
+    import copy
+    from samnerf_amd import _lib
+    from samnerf_amd.fused import FusedRenderer
+    spec = synth.ModelSpec(with_sam=True, grid_log2=12, s_grid_log2=11, prop_log2=10)
+    params = synth.make_params(spec, seed=6, emb_scale=0.5, ln_jitter=0.1)
+    net = make_net(spec, params, cuda)
+    g = torch.Generator().manual_seed(n)
+    rows = torch.randn(n, 164, generator=g)
+    rows *= 10.0 ** (torch.rand(n, 1, generator=g) * 8 - 4)
+    rows[:5] = 0.0
+    rows[:, 163] = 0.0
+    rows = rows.to(cuda)
+    prod = FusedRenderer(net).sam_head(rows).cpu().double()
+    ex = FusedRenderer(net, head_mode=1).sam_head(rows).cpu().double()
+    os.environ["SAMNERF_HEAD_V"] = form
+    try:
+        with _lib.diag_library():
+            w8 = FusedRenderer(net).sam_head(rows).cpu().double()
+    finally:
+        os.environ.pop("SAMNERF_HEAD_V", None)
+    head = copy.deepcopy(net.samvit_mlp).cpu()
+    with torch.no_grad():
+        ref = head.double()(rows[:, :163].cpu().double())
+    assert torch.isfinite(w8).all()
+    e_w8 = (w8 - ref).abs().max().item()
+    e_ex = (ex - ref).abs().max().item()
+    rel = ((w8 - prod).abs().max() / ref.abs().max()).item()
+    print("w8 head vs float64", e_w8, "exact", e_ex, "vs product rel", rel)
+    assert e_w8 <= 2.0 * e_ex + 1e-7, (e_w8, e_ex)
+    assert rel < 1e-6, rel
+
 def test_exact_fp32_mode_vs_oracle(hip_lib, cuda):
     """head_mode 1 runs grid_mlp on v_mfma_f32_32x32x2_f32 (an fma chain per
     k pair) as well as the SAM head: against the oracle (torch CPU GEMMs in
