@@ -97,11 +97,14 @@ int proposal_forward(const samnerf_model* m, const TrainGeometry& g, const float
 
 // pos = clamp(fma(u, res, -0.5), 0, res-1); cell = floor; frac = pos - cell.
 // nvcc contracts `u*res - 0.5` (gridencoder.cu:148), so the fma is explicit.
+// p >= 0 after the clamp, so the truncating conversion is the floor and
+// v_fract_f32 (p - floor(p), clamped below 1) is p - cell exactly: one VALU
+// less per axis than floor, convert and subtract, the same bits.
 __device__ __forceinline__ void locate_axis(float u, uint32_t res, uint32_t& cell, float& frac) {
     float p = __builtin_fmaf(u, (float)res, -0.5f);
     p = fminf(fmaxf(p, 0.0f), (float)(res - 1u));
-    cell = (uint32_t)floorf(p);
-    frac = p - (float)cell;
+    cell = (uint32_t)p;
+    frac = __builtin_amdgcn_fractf(p);
 }
 
 // fminf(fmaxf(p, 0), top) for top >= 0 as one v_med3_f32 (fminf / fmaxf
@@ -123,13 +126,14 @@ __device__ __forceinline__ float relu_bits(float x) {
 }
 
 // The same with the level's float resolution precomputed: frac = p -
-// floorf(p) is p - (float)cell exactly (p in [0, res - 1], res < 2^24).
+// floorf(p) is p - (float)cell exactly (p in [0, res - 1], res < 2^24), and
+// for p >= 0 that is v_fract_f32 (no floor instruction; the conversion
+// truncates, which is the floor).
 __device__ __forceinline__ void locate_axis(float u, const LevelDesc& d, uint32_t& cell, float& frac) {
     float p = __builtin_fmaf(u, d.fres, -0.5f);
     p = clamp_med3(p, d.ftop);
-    const float fl = floorf(p);
-    cell = (uint32_t)fl;
-    frac = p - fl;
+    cell = (uint32_t)p;
+    frac = __builtin_amdgcn_fractf(p);
 }
 
 // Fused-path row index.  The host (make_grid_desc) only admits levels that

@@ -144,7 +144,7 @@ __device__ __forceinline__ URange wave_urange(float ux, float uy, float uz) {
 __device__ __forceinline__ uint32_t cell_of(float u, const LevelDesc& d) {
     float p = __builtin_fmaf(u, d.fres, -0.5f);
     p = clamp_med3(p, d.ftop);
-    return (uint32_t)floorf(p);
+    return (uint32_t)p;                       // p >= 0: truncation is the floor
 }
 
 }  // namespace samnerf
