@@ -172,6 +172,19 @@ __device__ __forceinline__ floatx16 mfma_f16x3(uint4 ah, uint4 al, uint4 bh, uin
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(Ah, Bh, c, 0, 0, 0);
 }
 
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// C += A.B in f16x3 on the 16 x 16 x 32 form (small terms first): lane
+// (i, g) holds A[row i][k = 8 g .. 8 g + 7] and B[k = 8 g ..][column i], D
+// lane (j, g) column j, rows 4 g .. 4 g + 3
+__device__ __forceinline__ floatx4 mfma16_f16x3(uint4 ah, uint4 al, uint4 bh, uint4 bl, floatx4 c) {
+    const f16x8 Ah = __builtin_bit_cast(f16x8, ah), Al = __builtin_bit_cast(f16x8, al);
+    const f16x8 Bh = __builtin_bit_cast(f16x8, bh), Bl = __builtin_bit_cast(f16x8, bl);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(Al, Bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, Bl, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, Bh, c, 0, 0, 0);
+}
+
 // max |x| of a wave-wide reduction over the 64 lanes (for weight rows)
 __device__ __forceinline__ float wave_max64(float m) {
 #pragma unroll

@@ -27,10 +27,16 @@
 //                32x32 output tile x 1,024 rows per wave, float atomics.
 // Rows are sample-major (row = k * N + slot), the order in which the render
 // (k_final, GEO form) leaves positions, weights and geo_feat in its workspace.
-// Every product is an fp32 MFMA (exact fma chains), so the gradients match
-// torch's fp32 autograd up to summation order.
+// head_mode 1: every product is an fp32 MFMA (exact fma chains), so the
+// gradients match torch's fp32 autograd up to summation order.  head_mode 0
+// (the default, as the inference heads; round 5): the forward's GEMMs in
+// f16x3 (k_mt_fwd16 below: fp32-equivalent products on the fp16 matrix
+// cores); the backward and dW stay exact fp32 in both modes (measured: the
+// f16x3 forms of those are bound by the scatter and the row loads, not the
+// matrix cores, and were not faster).
 #include <algorithm>
 
+#include "f16x3.h"
 #include "fp32_chain.h"
 #include "samnerf_common.h"
 
@@ -262,48 +268,12 @@ __device__ __forceinline__ void bwd_layer(const float* __restrict__ wb, const fl
     }
 }
 
-__global__ void __launch_bounds__(256) k_mt_bwd(BwdArgs a) {
-    __shared__ float P[256 * kRows];
-    __shared__ float Q[256 * kRows];
-    __shared__ LevelDesc sLv[16];
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const uint32_t r0 = blockIdx.x * kRows;
+// the trilinear scatter of dx's m_grid part (Q [128][16] of the block's rows)
+// into the embedding gradient (k_mt_bwd)
+__device__ __forceinline__ void mt_scatter(const BwdArgs& a, const LevelDesc* sLv, const float* Q, uint32_t r0,
+                                           int w, int lane) {
     const Saved& sv = a.sv;
     const uint32_t N = a.in.N;
-    if (tid < 16) sLv[tid] = a.in.grid.lv[tid];
-    // g_o[u][j] = w_row * dL/dlogits[ray][u] (u < K), into P (32 x 16)
-    for (int idx = tid; idx < 32 * kRows; idx += 256) {
-        const int u = idx / kRows, j = idx % kRows;
-        const uint32_t r = r0 + (uint32_t)j;
-        float g = 0.0f;
-        if (r < sv.R && (uint32_t)u < a.K) {
-            const uint32_t k = r / N, s = r % N;
-            g = a.in.w[(size_t)k * N + s] * a.glog[(size_t)a.tiles(s) * a.K + u];
-        }
-        P[idx] = g;
-        sv.go[(size_t)u * sv.Rp + r] = g;
-    }
-    __syncthreads();
-    // torch's leaky_relu backward: grad * (result > 0 ? 1 : slope)
-    bwd_layer<2, 16>(a.wb, P, w, lane, [&](int v, int j, float d) {
-        const uint32_t r = r0 + (uint32_t)j;
-        const float h = sv.h2[(size_t)v * sv.Rp + r];
-        const float gz = r < sv.R ? (h > 0.0f ? d : d * 0.01f) : 0.0f;
-        Q[v * kRows + j] = gz;
-        sv.g2[(size_t)v * sv.Rp + r] = gz;
-    });
-    __syncthreads();
-    bwd_layer<1, 16>(a.wb, Q, w, lane, [&](int v, int j, float d) {
-        const uint32_t r = r0 + (uint32_t)j;
-        const float h = sv.h1[(size_t)v * sv.Rp + r];
-        const float gz = r < sv.R ? (h > 0.0f ? d : d * 0.01f) : 0.0f;
-        P[v * kRows + j] = gz;
-        sv.g1[(size_t)v * sv.Rp + r] = gz;
-    });
-    __syncthreads();
-    // dx of the m_grid part (tiles 0..7 of 9; geo_feat is detached) into Q
-    bwd_layer<0, 8>(a.wb, P, w, lane, [&](int v, int j, float d) { Q[v * kRows + j] = d; });
-    __syncthreads();
     // trilinear scatter: wave w takes levels w, w + 4, .., lane = (corner c,
     // channel ch), the block's 16 rows in order: each float atomic instruction
     // adds to 8 corner rows of 32 contiguous bytes (a thread per (row, level)
@@ -350,6 +320,233 @@ __global__ void __launch_bounds__(256) k_mt_bwd(BwdArgs a) {
         if (run != 0xffffffffu) atomicAdd(tgt + run / 4u + ch, acc);
     }
 }
+
+__global__ void __launch_bounds__(256) k_mt_bwd(BwdArgs a) {
+    __shared__ float P[256 * kRows];
+    __shared__ float Q[256 * kRows];
+    __shared__ LevelDesc sLv[16];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t r0 = blockIdx.x * kRows;
+    const Saved& sv = a.sv;
+    const uint32_t N = a.in.N;
+    if (tid < 16) sLv[tid] = a.in.grid.lv[tid];
+    // g_o[u][j] = w_row * dL/dlogits[ray][u] (u < K), into P (32 x 16)
+    for (int idx = tid; idx < 32 * kRows; idx += 256) {
+        const int u = idx / kRows, j = idx % kRows;
+        const uint32_t r = r0 + (uint32_t)j;
+        float g = 0.0f;
+        if (r < sv.R && (uint32_t)u < a.K) {
+            const uint32_t k = r / N, s = r % N;
+            g = a.in.w[(size_t)k * N + s] * a.glog[(size_t)a.tiles(s) * a.K + u];
+        }
+        P[idx] = g;
+        sv.go[(size_t)u * sv.Rp + r] = g;
+    }
+    __syncthreads();
+    // torch's leaky_relu backward: grad * (result > 0 ? 1 : slope)
+    bwd_layer<2, 16>(a.wb, P, w, lane, [&](int v, int j, float d) {
+        const uint32_t r = r0 + (uint32_t)j;
+        const float h = sv.h2[(size_t)v * sv.Rp + r];
+        const float gz = r < sv.R ? (h > 0.0f ? d : d * 0.01f) : 0.0f;
+        Q[v * kRows + j] = gz;
+        sv.g2[(size_t)v * sv.Rp + r] = gz;
+    });
+    __syncthreads();
+    bwd_layer<1, 16>(a.wb, Q, w, lane, [&](int v, int j, float d) {
+        const uint32_t r = r0 + (uint32_t)j;
+        const float h = sv.h1[(size_t)v * sv.Rp + r];
+        const float gz = r < sv.R ? (h > 0.0f ? d : d * 0.01f) : 0.0f;
+        P[v * kRows + j] = gz;
+        sv.g1[(size_t)v * sv.Rp + r] = gz;
+    });
+    __syncthreads();
+    // dx of the m_grid part (tiles 0..7 of 9; geo_feat is detached) into Q
+    bwd_layer<0, 8>(a.wb, P, w, lane, [&](int v, int j, float d) { Q[v * kRows + j] = d; });
+    __syncthreads();
+    mt_scatter(a, sLv, Q, r0, w, lane);
+}
+
+// ------------------------------------------------------ f16x3 forward
+// head_mode 0 (the default, as the inference heads): the forward's three
+// layers as f16x3 on v_mfma_f32_16x16x32_f16 (f16x3.h: each fp32 product as
+// three fp16 MFMA products of power-of-two scaled operands -- the weight
+// tensors scaled per tensor at packing, each row's inputs per row from their
+// max), 16 rows per workgroup as k_mt_fwd; fp32-equivalent, not k_mt_fwd's
+// bits (the accumulation order differs).  A layer is: the input rows' maxima
+// (LDS atomics on the magnitude bits), a split pass writing the B fragments
+// of the whole layer input into LDS once ([k-step][hi/lo][lane]), then each
+// wave's output tiles over the k-steps with the weights' A fragments from the
+// packed copy, and the store of the unscaled value.
+// Measured (round 5, 4,096-ray training step, tools/train_profile.py): the
+// forward 0.485 -> 0.34 ms; the same scheme for the backward's dx chain
+// (k_mt_bwd: 1.15 -> 1.28 ms -- its 16 KiB of B fragments cost a workgroup
+// per CU, and the kernel is bound by the m_grid scatter, not the GEMMs) and
+// for dW (0.516 -> 0.486 ms: the row loads, not the MFMAs, bound it) was not
+// kept: the backward stays exact fp32 in both modes.
+constexpr int kKp16[3] = {160, 256, 256};                 // fan-in padded to 32
+__host__ __device__ constexpr int f16_tiles(int L) { return kOp[L] / 16; }
+__host__ __device__ constexpr int f16_steps(int L) { return kKp16[L] / 32; }
+__host__ __device__ constexpr int f16_vec(int L) { return f16_tiles(L) * f16_steps(L) * 2 * 64; }
+__host__ __device__ constexpr int f16_base(int L) {       // uint4 before layer L
+    int b = 0;
+    for (int i = 0; i < L; ++i) b += f16_vec(i);
+    return b;
+}
+constexpr int kPack16Vec = f16_base(3);
+constexpr int kW16Parts = 32;                             // partial maxima per tensor
+
+// partial max |w| of tensor blockIdx.y over its part blockIdx.x
+__global__ void __launch_bounds__(256) k_mt_wmax16(MaskW mw, float* __restrict__ part) {
+    __shared__ float wm[4];
+    const int L = blockIdx.y, tid = threadIdx.x;
+    const int n = logical_out(L, mw.K) * logical_in(L), chunk = (n + kW16Parts - 1) / kW16Parts;
+    const int i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+    float m = 0.0f;
+    for (int i = i0 + tid; i < i1; i += 256) m = fmaxf(m, fabsf(mw.w[L][i]));
+    m = wave_max64(m);
+    if ((tid & 63) == 0) wm[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0) part[L * kW16Parts + blockIdx.x] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+}
+
+// packed[L][tile][step][hi/lo][lane]: lane (i, g), 8 values m:
+//   A[i][k] = W_L[16 t + i][32 s + 8 g + m] times 2^kexp[L], zero outside the
+// logical shape; kexp[L] from the tensor's partial maxima
+__global__ void __launch_bounds__(256) k_mt_pack16(MaskW mw, const float* __restrict__ part, int* __restrict__ kexp,
+                                                   uint4* __restrict__ pk) {
+    const int e = (int)(blockIdx.x * 256u + threadIdx.x);            // one (hi, lo) pair
+    if (e >= kPack16Vec / 2) return;
+    int L = 0, rem = e;
+    while (L < 2 && rem >= f16_vec(L) / 2) rem -= f16_vec(L++) / 2;
+    float wmax = 0.0f;
+    for (int q = 0; q < kW16Parts; ++q) wmax = fmaxf(wmax, part[L * kW16Parts + q]);
+    const int kx = scale_exp_of_max(wmax);
+    if (rem == 0) kexp[L] = kx;
+    const int lane = rem & 63, ts = rem >> 6, S = f16_steps(L), t = ts / S, s = ts % S;
+    const int i = lane & 15, g = lane >> 4;
+    const int lo_ = logical_out(L, mw.K), li = logical_in(L);
+    const float* W = mw.w[L];
+    float v[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int r = 16 * t + i, c = 32 * s + 8 * g + m;
+        v[m] = (r < lo_ && c < li) ? W[(size_t)r * li + c] : 0.0f;
+    }
+    uint4 hi, lo;
+    split8_f16(v, exp2i(kx), hi, lo);
+    uint4* o = pk + f16_base(L) + (size_t)(t * S + s) * 128;
+    o[lane] = hi;
+    o[64 + lane] = lo;
+}
+
+// max |v| of a row into rmax[j] (magnitude bits order as unsigned integers)
+__device__ __forceinline__ void row_max_bits(uint32_t* rmax, int j, float v) {
+    atomicMax(rmax + j, __float_as_uint(fabsf(v)));
+}
+
+// One f16x3 layer over the block's 16 rows: out[NT tiles of 16][16] from
+// in[K][16] (LDS, row j = column j of B).  All 256 threads: the split of the
+// input into B fragments (Bf, LDS [step][hi/lo][64] uint4) at each row's
+// scale, then wave w takes output tiles w, w + 4, .. (< NT) over the k-steps.
+// store(u, j, value) gets the unscaled fp32 result for unit u of row j.
+template <int L, int NT, typename Store>
+__device__ __forceinline__ void gemm16(const uint4* __restrict__ pk, const int* __restrict__ kexp, const float* in,
+                                       const uint32_t* rmax, uint4* Bf, int tid, Store store) {
+    constexpr int S = f16_steps(L), NTT = f16_tiles(L), MT = (NT + 3) / 4;
+    static_assert(NT <= NTT, "tiles");
+    // split: item (step s, B lane (j, g)) = in[32 s + 8 g + m][j], m = 0..7
+    for (int it = tid; it < S * 64; it += 256) {
+        const int s = it >> 6, bl = it & 63, j = bl & 15, g = bl >> 4;
+        float v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[m] = in[(32 * s + 8 * g + m) * kRows + j];
+        uint4 hi, lo;
+        split8_f16(v, exp2i(scale_exp_of_max(__uint_as_float(rmax[j]))), hi, lo);
+        Bf[(2 * s) * 64 + bl] = hi;
+        Bf[(2 * s + 1) * 64 + bl] = lo;
+    }
+    __syncthreads();
+    const int w = tid >> 6, lane = tid & 63, j = lane & 15, g = lane >> 4;
+    if (w >= NT) return;
+    const uint4* A = pk + f16_base(L) + lane;
+    floatx4 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    uint4 ah[2][MT], al[2][MT];
+    auto load = [&](int b, int s) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            const int t = min(w + 4 * m, NT - 1);            // past NT: repeat the last (dropped)
+            ah[b][m] = A[(size_t)(t * S + s) * 128];
+            al[b][m] = A[(size_t)(t * S + s) * 128 + 64];
+        }
+    };
+    load(0, 0);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        if (s + 1 < S) load((s + 1) & 1, s + 1);
+        const uint4 bh = Bf[(2 * s) * 64 + lane], bl = Bf[(2 * s + 1) * 64 + lane];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m] = mfma16_f16x3(ah[s & 1][m], al[s & 1][m], bh, bl, acc[m]);
+    }
+    const float iw = exp2i(-kexp[L]), ir = exp2i(-scale_exp_of_max(__uint_as_float(rmax[j])));
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int t = w + 4 * m;
+        if (t >= NT) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) store(16 * t + 4 * g + r, j, (acc[m][r] * iw) * ir);
+    }
+}
+
+struct Fwd16Args {
+    SampleIn in;
+    const uint4* pk;
+    const int* kexp;
+    Saved sv;
+};
+
+
+__global__ void __launch_bounds__(256) k_mt_fwd16(Fwd16Args a) {
+    __shared__ float XH2[256 * kRows];                    // x (160 rows), then h2
+    __shared__ float H1[256 * kRows];
+    __shared__ uint4 Bf[8 * 2 * 64];
+    __shared__ uint32_t rmax[3][kRows];
+    __shared__ LevelDesc sLv[16];
+    const int tid = threadIdx.x;
+    const uint32_t r0 = blockIdx.x * kRows;
+    const Saved& sv = a.sv;
+    if (tid < 16) sLv[tid] = a.in.grid.lv[tid];
+    if (tid < 3 * kRows) rmax[tid / kRows][tid % kRows] = 0u;
+    for (int idx = kKp[0] * kRows + tid; idx < kKp16[0] * kRows; idx += 256) XH2[idx] = 0.0f;
+    __syncthreads();
+    gather_x(a.in, sLv, r0, sv.R, XH2);
+    __syncthreads();
+    for (int idx = tid; idx < kKp[0] * kRows; idx += 256) {
+        const float v = XH2[idx];
+        sv.x[(size_t)(idx / kRows) * sv.Rp + r0 + (idx % kRows)] = v;
+        row_max_bits(rmax[0], idx % kRows, v);
+    }
+    __syncthreads();
+    gemm16<0, 16>(a.pk, a.kexp, XH2, rmax[0], Bf, tid, [&](int u, int j, float z) {
+        const float h = r0 + (uint32_t)j < sv.R ? leaky(z) : 0.0f;
+        H1[u * kRows + j] = h;
+        sv.h1[(size_t)u * sv.Rp + r0 + j] = h;
+        row_max_bits(rmax[1], j, h);
+    });
+    __syncthreads();
+    gemm16<1, 16>(a.pk, a.kexp, H1, rmax[1], Bf, tid, [&](int u, int j, float z) {
+        const float h = r0 + (uint32_t)j < sv.R ? leaky(z) : 0.0f;
+        XH2[u * kRows + j] = h;
+        sv.h2[(size_t)u * sv.Rp + r0 + j] = h;
+        row_max_bits(rmax[2], j, h);
+    });
+    __syncthreads();
+    gemm16<2, 2>(a.pk, a.kexp, XH2, rmax[2], Bf, tid, [&](int u, int j, float z) {
+        sv.o[(size_t)u * sv.Rp + r0 + j] = r0 + (uint32_t)j < sv.R ? z : 0.0f;
+    });
+}
+
 
 struct DwArgs {
     Saved sv;
@@ -435,8 +632,11 @@ __global__ void __launch_bounds__(256) k_mt_dw(DwArgs a) {
     }
 }
 
+
 struct Layout {
     float *wf, *wb;
+    uint4* pk16;             // f16x3 fragments (head_mode 0), kPack16Vec uint4
+    int* kexp16;             // their per-tensor log2 scales, then 3 x kW16Parts partial maxima
     float* rep;              // kRep x kRepRows x 8 floats (the coarse levels' gradient copies)
     Saved sv;
     size_t bytes;
@@ -459,6 +659,8 @@ Layout carve(uint32_t N, void* base) {
     const size_t Rp = L.sv.Rp;
     L.wf = take(kPackFloats);
     L.wb = take(kPackFloats);
+    L.pk16 = reinterpret_cast<uint4*>(take((size_t)kPack16Vec * 4u));
+    L.kexp16 = reinterpret_cast<int*>(take(4 + 3 * kW16Parts));
     L.rep = take((size_t)kRep * kRepRows * 8u);
     L.sv.x = take((size_t)kKp[0] * Rp);
     L.sv.h1 = take((size_t)256 * Rp);
@@ -756,12 +958,25 @@ int mask_train_forward(const samnerf_model* m, const GridDesc<16>& grid, const f
     if (ws_bytes < L.bytes)
         return fail(SAMNERF_EWORKSPACE, "mask_train_forward: workspace needs %zu bytes, got %zu", L.bytes,
                     ws_bytes);
+    // the exact fp32 fragments: the forward of head_mode 1, the backward of both
     k_mt_pack<<<div_up(kPackFloats, 256), 256, 0, s>>>(mw, L.wf, L.wb);
-    FwdArgs a;
-    a.in = SampleIn{grid, u_f, w_f, geo_f, N};
-    a.wf = L.wf;
-    a.sv = L.sv;
-    k_mt_fwd<<<L.sv.Rp / kRows, 256, 0, s>>>(a);   // rows R .. Rp saved as zeros (k_mt_dw)
+    if (m->head_mode == 0) {                        // f16x3 forward (fp32-equivalent)
+        float* part = reinterpret_cast<float*>(L.kexp16 + 4);
+        k_mt_wmax16<<<dim3(kW16Parts, 3), 256, 0, s>>>(mw, part);
+        k_mt_pack16<<<div_up(kPack16Vec / 2, 256), 256, 0, s>>>(mw, part, L.kexp16, L.pk16);
+        Fwd16Args a;
+        a.in = SampleIn{grid, u_f, w_f, geo_f, N};
+        a.pk = L.pk16;
+        a.kexp = L.kexp16;
+        a.sv = L.sv;
+        k_mt_fwd16<<<L.sv.Rp / kRows, 256, 0, s>>>(a);   // rows R .. Rp saved as zeros (k_mt_dw)
+    } else {                                        // exact fp32
+        FwdArgs a;
+        a.in = SampleIn{grid, u_f, w_f, geo_f, N};
+        a.wf = L.wf;
+        a.sv = L.sv;
+        k_mt_fwd<<<L.sv.Rp / kRows, 256, 0, s>>>(a);   // rows R .. Rp saved as zeros (k_mt_dw)
+    }
     k_mt_logits<<<div_up((uint64_t)N * mw.K, 256), 256, 0, s>>>(w_f, L.sv.o, N, mw.K, L.sv.Rp, tiles, logits);
     return check_launch("mask_train_forward");
 }

@@ -1120,16 +1120,6 @@ __global__ void __launch_bounds__(256) k_pack_w8(PackArgs a) {
     a.packed[(size_t)step * w8::kStepVec + 512 + tile * 64 + lane] = lo;
 }
 
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-// C += A.B in f16x3 on the 16 x 16 x 32 form (small terms first)
-__device__ __forceinline__ floatx4 mfma16_f16x3(uint4 ah, uint4 al, uint4 bh, uint4 bl, floatx4 c) {
-    const f16x8 Ah = __builtin_bit_cast(f16x8, ah), Al = __builtin_bit_cast(f16x8, al);
-    const f16x8 Bh = __builtin_bit_cast(f16x8, bh), Bl = __builtin_bit_cast(f16x8, bl);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(Al, Bh, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, Bl, c, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, Bh, c, 0, 0, 0);
-}
 
 template <int NBUF, int WAVES>
 struct HeadStreamW8 {

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 GRAD_TOL = 1e-4          # relative, per tensor: fp32 sums in another order, float atomics
 
 
-def _mask_nets(cuda, n_inst=5, redundant=0, sum_after=False, seed=21):
+def _mask_nets(cuda, n_inst=5, redundant=0, sum_after=False, seed=21, head_mode=1):
     spec = synth.ModelSpec(with_sam=False, with_mask=True, mask_type="default", n_inst=n_inst,
                            redundant_instance=redundant, sum_after_mlp=sum_after, grid_log2=12,
                            prop_log2=10, m_grid_log2=12)
@@ -31,7 +31,9 @@ def _mask_nets(cuda, n_inst=5, redundant=0, sum_after=False, seed=21):
     for n in (gpu, cpu):                     # main.py:255-262: only the mask head trains
         for k, p in n.named_parameters():
             p.requires_grad = k.startswith("m_grid") or k.startswith("mask_mlp")
-    gpu.head_mode = 1                        # geo_feat from exact fp32 grid_mlp GEMMs
+    # 1: geo_feat from exact fp32 grid_mlp GEMMs and the head's training
+    # forward exact fp32; 0 (the default): both f16x3 (fp32-equivalent)
+    gpu.head_mode = head_mode
     return gpu, cpu
 
 
@@ -58,12 +60,16 @@ def _grad_errors(gpu, cpu):
     return errs
 
 
-@pytest.mark.parametrize("n_inst,redundant,sum_after", [(5, 0, False), (2, 0, True), (32, 0, False),
-                                                        (1, 0, False)])
-def test_fused_mask_step_matches_cpu_twin(hip_lib, cuda, n_inst, redundant, sum_after):
+@pytest.mark.parametrize("n_inst,redundant,sum_after,head_mode",
+                         [(5, 0, False, 1), (2, 0, True, 1), (32, 0, False, 1), (1, 0, False, 1),
+                          (5, 0, False, 0), (32, 0, False, 0), (2, 0, True, 0)])
+def test_fused_mask_step_matches_cpu_twin(hip_lib, cuda, n_inst, redundant, sum_after, head_mode):
+    """head_mode 1: the exact fp32 training forward (k_mt_fwd); 0 (the
+    default): the f16x3 forward (k_mt_fwd16); the backward is exact fp32 in
+    both."""
     from oracle_backend import injected_bins, oracle_encoders
     from samnerf_amd.train import mask_train_step
-    gpu, cpu = _mask_nets(cuda, n_inst, redundant, sum_after)
+    gpu, cpu = _mask_nets(cuda, n_inst, redundant, sum_after, head_mode=head_mode)
     ro, rd = _rays(16, 4)
     gt = torch.randint(0, n_inst, (256,), generator=torch.Generator().manual_seed(3))
     bins = _fused_bins(gpu, ro.to(cuda), rd.to(cuda))
@@ -81,11 +87,12 @@ def test_fused_mask_step_matches_cpu_twin(hip_lib, cuda, n_inst, redundant, sum_
     assert not bad, bad
 
 
-def test_fused_mask_logits_match_inference_head(hip_lib, cuda):
-    """The training forward's logits (exact fp32, k_mt_fwd + k_mt_logits) equal
-    the inference head's (k_mask_head, head_mode 1) to fp32 summation order."""
+@pytest.mark.parametrize("head_mode", [1, 0])
+def test_fused_mask_logits_match_inference_head(hip_lib, cuda, head_mode):
+    """The training forward's logits (k_mt_fwd / k_mt_fwd16 + k_mt_logits) equal
+    the inference head's (k_mask_head) in the same head_mode to fp32 level."""
     from samnerf_amd.fused import FusedRenderer, render_mask_train
-    gpu, _ = _mask_nets(cuda, n_inst=7)
+    gpu, _ = _mask_nets(cuda, n_inst=7, head_mode=head_mode)
     ro, rd = _rays(24, 5)
     ro, rd = ro.to(cuda), rd.to(cuda)
     fr = FusedRenderer(gpu)
