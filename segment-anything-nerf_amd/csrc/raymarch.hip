@@ -2648,7 +2648,7 @@ int proposal_forward(const samnerf_model* m, const TrainGeometry& g, const float
     pa.rays_d = rays_d;
     pa.cnf = cnf;
     pa.N = N;
-    pa.tiles = RayTiles{0u, 0u};
+    pa.tiles = RayTiles{0u, 0u, 32u};
     pa.n_cnf = n_cnf;
     for (int i = 0; i < 6; ++i) pa.aabb[i] = m->aabb[i];
     pa.min_near = m->min_near;

@@ -413,22 +413,27 @@ __device__ __forceinline__ void lookup_level3_ref(const float* __restrict__ emb,
 // per-ray outputs (image, depth, weights_sum, head rows) written at ray_of(s),
 // so callers see ray order.  w == 0: identity (W not a multiple of 8, or N not
 // a multiple of 4 W rows).
+// tpr_log2: log2(tpr) when tpr is a power of two (the 512-wide views: a shift
+// where the generic unsigned division by the uniform tpr is ~20 VALU -- once
+// per sample in k_prop_sigma), else 32 (the division)
 struct RayTiles {
-    uint32_t w;      // view width in pixels (0: identity)
-    uint32_t tpr;    // tiles per tile row = w / 8
+    uint32_t w;           // view width in pixels (0: identity)
+    uint32_t tpr;         // tiles per tile row = w / 8
+    uint32_t tpr_log2;
     __device__ __forceinline__ uint32_t operator()(uint32_t s) const {
         if (w == 0u) return s;
         const uint32_t tile = s >> 5, in = s & 31u;
-        const uint32_t trow = tile / tpr, tcol = tile - trow * tpr;
+        const uint32_t trow = tpr_log2 < 32u ? tile >> tpr_log2 : tile / tpr, tcol = tile - trow * tpr;
         return (trow * 4u + (in >> 3)) * w + tcol * 8u + (in & 7u);
     }
 };
 
 inline RayTiles make_ray_tiles(uint32_t N, uint32_t W) {
-    RayTiles t{0u, 0u};
+    RayTiles t{0u, 0u, 32u};
     if (W >= 8u && W % 8u == 0u && N % (4u * W) == 0u) {
         t.w = W;
         t.tpr = W / 8u;
+        if ((t.tpr & (t.tpr - 1u)) == 0u) t.tpr_log2 = (uint32_t)__builtin_ctz(t.tpr);
     }
     return t;
 }
