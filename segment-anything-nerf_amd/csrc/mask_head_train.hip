@@ -298,16 +298,9 @@ __device__ __forceinline__ void mt_scatter(const BwdArgs& a, const LevelDesc* sL
             if (r >= sv.R) break;                             // wave-uniform: the tail block's last rows
             const uint32_t k = r / N, s = r % N;
             const float* up = a.in.u + (size_t)k * 3u * N + s;
-            uint32_t off[8];
-            float cw[8];
-            corner_rows<8>(sLv[l], up[0], up[N], up[2u * N], off, cw);
-            uint32_t o = off[0];
-            float wc = cw[0];
-#pragma unroll
-            for (int q = 1; q < 8; ++q) {
-                o = c == q ? off[q] : o;
-                wc = c == q ? cw[q] : wc;
-            }
+            uint32_t o;
+            float wc;
+            corner_row_of<8>(sLv[l], up[0], up[N], up[2u * N], (uint32_t)c, o, wc);
             const float v = wc * Q[(8 * l + ch) * kRows + j];
             if (o == run) {
                 acc += v;

@@ -285,6 +285,29 @@ __device__ __forceinline__ void corner_rows(const LevelDesc& d, float ux, float 
     }
 }
 
+// One corner (bit 0 x, 1 y, 2 z of c, lane-varying) of corner_rows<C>: the
+// same byte offset and the same weight bits -- (wx * wy) * wz in that order,
+// the row's terms combined as there (xor and integer adds are associative) --
+// for a lane that needs only its own corner (the mask-training scatter: lane
+// = (corner, channel)); a third of corner_rows' instructions.
+template <uint32_t C>
+__device__ __forceinline__ void corner_row_of(const LevelDesc& d, float ux, float uy, float uz, uint32_t c,
+                                              uint32_t& off, float& w) {
+    uint32_t cx, cy, cz;
+    float fx, fy, fz;
+    locate_axis(ux, d, cx, fx);
+    locate_axis(uy, d, cy, fy);
+    locate_axis(uz, d, cz, fz);
+    const uint32_t top = d.res - 1u;
+    const uint32_t x = (c & 1u) ? min(cx + 1u, top) : cx, y = (c & 2u) ? min(cy + 1u, top) : cy,
+                   z = (c & 4u) ? min(cz + 1u, top) : cz;
+    const uint32_t row = (d.flags & kHashed) ? (x ^ (y * kPrime1) ^ (z * kPrime2)) & (d.size - 1u)
+                                             : x + (uint32_t)__umul24(y, d.res) + (uint32_t)__umul24(z, d.res * d.res);
+    off = (d.off + row) * (C * 4u);
+    const float wx = (c & 1u) ? fx : 1.0f - fx, wy = (c & 2u) ? fy : 1.0f - fy, wz = (c & 4u) ? fz : 1.0f - fz;
+    w = (wx * wy) * wz;
+}
+
 // Trilinear lookup of one level (D = 3, linear interpolation, no
 // align_corners): the 8 corners in the reference's order, FMA accumulation
 // into `acc` on packed-fp32 FMAs (two channels per v_pk_fma_f32; each lane
