@@ -112,8 +112,8 @@ def parse():
                          "chunk's all-gather behind the next chunk")
     ap.add_argument("--streams", type=int, default=0,
                     help="HIP streams the views are issued on round-robin, so view i+1's kernels "
-                         "overlap view i's (each stream has its own workspace).  0 = 2 for 1-4 "
-                         "ranks, 3 for 8 (one rank's 32K-ray share: +16%%)")
+                         "overlap view i's (each stream has its own workspace).  0 = by band size: "
+                         "1 for the whole view, 2 at 2 ranks, 3 at 4-8 (measured, DESIGN.md 7)")
     ap.add_argument("--mode", choices=["render", "train", "gui", "rgbtrain"], default="render",
                     help="render: cfg 3 view throughput (the headline metric); train: cfg 5 "
                          "SAM-feature distillation step (4096 rays, forward + backward + Adam); "
@@ -574,9 +574,12 @@ class ViewRunner:
         self.args, self.renderer, self.world, self.dev = args, renderer, world, dev
         self.H, self.W, self.pose, self.intr, self.r0, self.r1 = H, W, pose, intr, r0, r1
         self.chunks = max(1, args.chunks) if world > 1 else 1
-        # measured best: 2 streams up to 4 ranks (N=1: 3.25 -> 3.18
-        # ms per view), 3 at 8 ranks
-        n_streams = args.streams or (2 if world <= 4 else 3)
+        # measured best per band size (tools/streams_ab.sh):
+        # the whole view on 1 stream (2.785 vs 2.81 ms on 2: the chip is at its
+        # power limit, so a second view in flight only shares it), a half view on
+        # 2, a quarter or an eighth on 3; --rank-share N picks as N ranks would
+        eff = args.rank_share if world == 1 and args.rank_share > 1 else world
+        n_streams = args.streams or (1 if eff == 1 else 2 if eff == 2 else 3)
         self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                            for _ in range(n_streams - 1)]
         self.n_step = 0
