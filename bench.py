@@ -112,8 +112,9 @@ def parse():
                          "chunk's all-gather behind the next chunk")
     ap.add_argument("--streams", type=int, default=0,
                     help="HIP streams the views are issued on round-robin, so view i+1's kernels "
-                         "overlap view i's (each stream has its own workspace).  0 = by band size: "
-                         "1 for the whole view, 2 at 2 ranks, 3 at 4-8 (measured, DESIGN.md 7)")
+                         "overlap view i's (each stream has its own workspace).  0 = tuned in the "
+                         "warm-up between the two counts around 1 (whole view) / 2 (2 ranks) / 3 "
+                         "(4-8 ranks) (measured, DESIGN.md 7)")
     ap.add_argument("--mode", choices=["render", "train", "gui", "rgbtrain"], default="render",
                     help="render: cfg 3 view throughput (the headline metric); train: cfg 5 "
                          "SAM-feature distillation step (4096 rays, forward + backward + Adam); "
@@ -574,14 +575,22 @@ class ViewRunner:
         self.args, self.renderer, self.world, self.dev = args, renderer, world, dev
         self.H, self.W, self.pose, self.intr, self.r0, self.r1 = H, W, pose, intr, r0, r1
         self.chunks = max(1, args.chunks) if world > 1 else 1
-        # measured best per band size (tools/streams_ab.sh):
-        # the whole view on 1 stream (2.785 vs 2.81 ms on 2: the chip is at its
-        # power limit, so a second view in flight only shares it), a half view on
-        # 2, a quarter or an eighth on 3; --rank-share N picks as N ranks would
+        # Views in flight (tools/streams_ab.sh): on the
+        # default scene the whole view is fastest on 1 stream (2.785 vs 2.81 ms
+        # on 2: the chip is at its power limit, so a second view in flight only
+        # shares it), a half view on 2, a quarter or an eighth on 3; on the
+        # opaque-sphere scene (L2-miss latency) the whole view gains 13 % from a
+        # second stream.  --streams 0 (default): the warm-up times the two
+        # candidate counts around that rule on the workload itself and the timed
+        # views use the faster (max over ranks, so every rank picks the same);
+        # --rank-share N picks as N ranks would.
         eff = args.rank_share if world == 1 and args.rank_share > 1 else world
-        n_streams = args.streams or (1 if eff == 1 else 2 if eff == 2 else 3)
+        rule = 1 if eff == 1 else 2 if eff == 2 else 3
+        self.cands = ([1, 2] if rule == 1 else [2, 3]) if not args.streams else [args.streams]
+        self.n_active = args.streams or rule
+        self.tuned = None
         self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
-                                                           for _ in range(n_streams - 1)]
+                                                           for _ in range(max(self.cands) - 1)]
         self.n_step = 0
         # fp32 transport: each rank renders its band straight into its slice of
         # the gather buffer (samnerf_render_forward_tile), no pack copy
@@ -613,7 +622,7 @@ class ViewRunner:
         return render_fn(*ray_fn(self.r0, self.r1 - self.r0))
 
     def step(self, raws=None):
-        s = self.streams[self.n_step % len(self.streams)]
+        s = self.streams[self.n_step % self.n_active]
         self.n_step += 1
         with torch.cuda.stream(s):
             return self._step_on_stream(raws)
@@ -635,9 +644,38 @@ class ViewRunner:
             raw = (ctypes.c_void_p * 6)(*[e.cuda_event for e in evs])
             return evs, raw
 
-        for _ in range(warmup):
+        # the warm-up runs on every candidate stream (each allocates its
+        # workspace on first use, outside the tuning and the timed views)
+        n_keep, self.n_active = self.n_active, max(self.cands)
+        for _ in range(max(warmup, self.n_active)):
             self.step()
         self._flush()
+        self.n_active, self.n_step = n_keep, 0
+        if len(self.cands) > 1:
+            # views in flight: time each candidate stream count on this workload
+            # (untimed warm-up work), keep the faster for the timed views
+            # (interleaved: 3 rounds of 8 views per candidate, ~0.2 s)
+            self.tuned = {k: 0.0 for k in self.cands}
+            n_tune, rounds = 8, 3
+            for _ in range(rounds):
+                for k in self.cands:
+                    self.n_active, self.n_step = k, 0
+                    torch.cuda.synchronize()
+                    if self.world > 1:
+                        dist.barrier()
+                    t0 = time.perf_counter()
+                    for _ in range(n_tune):
+                        self.step()
+                    self._flush()
+                    torch.cuda.synchronize()
+                    dtk = time.perf_counter() - t0
+                    if self.world > 1:
+                        tk = torch.tensor([dtk], device=self.dev if self.args.dist_backend == "nccl" else "cpu")
+                        dist.all_reduce(tk, op=dist.ReduceOp.MAX)
+                        dtk = tk.item()
+                    self.tuned[k] += dtk * 1e3 / (n_tune * rounds)
+            self.n_active = min(self.tuned, key=self.tuned.get)
+            self.n_step = 0
         sets = [[make_event_set() for _ in range(self.chunks)] for _ in range(steps)] if stages else None
         torch.cuda.synchronize()
         if self.world > 1:
@@ -662,7 +700,7 @@ class ViewRunner:
         if not stages:
             return dt, last, None, None
         stage_src = "the timed views"
-        if len(self.streams) > 1:
+        if self.n_active > 1:
             # Stage times for the rooflines from a single-stream pass after the
             # timed region: with several views in flight, one view's HIP events
             # also span the other streams' kernels.  Every rank runs it (the
@@ -937,13 +975,14 @@ def main():
             rn = ViewRunner(args, FusedRenderer(snet, head_mode=args.head_mode, t_thresh=t), 1, dev,
                             H, W, pose, intr, r0, r1, codec)
             dtn, lastn, stn, _ = rn.run(k, 2)
-            n1[t] = (dtn, lastn, stn)
+            n1[t] = (dtn, lastn, stn, rn.n_active, rn.tuned)
         base, fast = n1[0.0], n1[1e-4]
         # the trained-scene regime (proposal samples concentrated at a surface)
         # in the default mode: the headline's configuration on another scene
         side["surface_scene"] = {
             "value": n_total * k / base[0], "unit": "rays/s", "ms_per_step": base[0] * 1e3 / k,
             "stage_ms": base[2], "vs_headline_ms": (base[0] * 1e3 / k) / (dt * 1e3 / args.steps),
+            "streams": base[3], "streams_tuned_ms": base[4],
             "what": "the headline configuration (cfg3) on the opaque-sphere scene "
                     "(synth.make_surface_params: a trained scene's regime, samples at the surface), "
                     "default mode (reference semantics)"}
@@ -1061,7 +1100,8 @@ def main():
         rec = {
             "metric": METRIC, "value": value, "unit": "rays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt * 1e3 / args.steps,
-            "streams": len(runner.streams),
+            "streams": runner.n_active,
+            "streams_tuned_ms": runner.tuned,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": DTYPE[args.head_mode],
             "data": ("synthetic (random-init weights of the reference architecture, GUI camera)"
@@ -1074,7 +1114,7 @@ def main():
                        "rays_per_step": n_total, "num_steps": [128, 64, 32],
                        "parallelism": (f"ray-sharded row bands x{world}, RCCL all-gather of each view "
                                        f"overlapped with the next view's rendering, views issued on "
-                                       f"{len(runner.streams)} HIP streams" if args.chunks == 0 else
+                                       f"{runner.n_active} HIP streams" if args.chunks == 0 else
                                        f"ray-sharded row bands x{world}, {runner.chunks} chunks per band, "
                                        "async RCCL all-gather per chunk") if world > 1
                        else "single GPU",
