@@ -120,7 +120,64 @@ __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, u
     split_pair_f16_old(v[4], v[5], s, hi.z, lo.z);
     split_pair_f16_old(v[6], v[7], s, hi.w, lo.w);
 }
-#else
+#elif !defined(SAMNERF_SPLIT_MIX)
+// Round 5: the same split on full-dword conversions.  v_fma_mix issues at a
+// quarter of v_fma_f32's rate on gfx950 (8.2 cycles per wave64 instruction
+// against 2.2; v_cvt_pk_f16_f32 / v_cvt_f32_f16 4.1, v_mul_f32 / v_sub_f32
+// 2.2: tools/valu_rate.hip, profiles/r5v_valu_rate.json), so 16 mixes
+// (131 cycles per 8 values) cost more than a = x s, hi = cvt_pk(a), the hi
+// halves back to fp32, d = a - f32(hi), lo = cvt_pk(d): 32 instructions, 101
+// cycles.  The same bits: x s, f32(hi) and a - f32(hi) are exact, and each
+// half is rounded to fp16 once (RNE), as the mix does.  Every write is a
+// whole dword (no dst-sel hazard), each result is read at least 4
+// instructions after it is written, and the closing s_nop 1 covers the VALU
+// -> MFMA operand rule for the last lo dword.
+__device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
+    uint32_t h0, h1, h2, h3, l0, l1, l2, l3;
+    float a0, a1, a2, a3, a4, a5, a6, a7, t0, t1, t2, t3, t4, t5, t6, t7;
+    asm("v_mul_f32 %[a0], %[v0], %[s]\n\t"
+        "v_mul_f32 %[a1], %[v1], %[s]\n\t"
+        "v_mul_f32 %[a2], %[v2], %[s]\n\t"
+        "v_mul_f32 %[a3], %[v3], %[s]\n\t"
+        "v_mul_f32 %[a4], %[v4], %[s]\n\t"
+        "v_mul_f32 %[a5], %[v5], %[s]\n\t"
+        "v_mul_f32 %[a6], %[v6], %[s]\n\t"
+        "v_mul_f32 %[a7], %[v7], %[s]\n\t"
+        "v_cvt_pk_f16_f32 %[h0], %[a0], %[a1]\n\t"
+        "v_cvt_pk_f16_f32 %[h1], %[a2], %[a3]\n\t"
+        "v_cvt_pk_f16_f32 %[h2], %[a4], %[a5]\n\t"
+        "v_cvt_pk_f16_f32 %[h3], %[a6], %[a7]\n\t"
+        "v_cvt_f32_f16 %[t0], %[h0]\n\t"
+        "v_cvt_f32_f16 %[t2], %[h1]\n\t"
+        "v_cvt_f32_f16 %[t4], %[h2]\n\t"
+        "v_cvt_f32_f16 %[t6], %[h3]\n\t"
+        "v_cvt_f32_f16_sdwa %[t1], %[h0] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1\n\t"
+        "v_cvt_f32_f16_sdwa %[t3], %[h1] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1\n\t"
+        "v_cvt_f32_f16_sdwa %[t5], %[h2] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1\n\t"
+        "v_cvt_f32_f16_sdwa %[t7], %[h3] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1\n\t"
+        "v_sub_f32 %[t0], %[a0], %[t0]\n\t"
+        "v_sub_f32 %[t2], %[a2], %[t2]\n\t"
+        "v_sub_f32 %[t4], %[a4], %[t4]\n\t"
+        "v_sub_f32 %[t6], %[a6], %[t6]\n\t"
+        "v_sub_f32 %[t1], %[a1], %[t1]\n\t"
+        "v_sub_f32 %[t3], %[a3], %[t3]\n\t"
+        "v_sub_f32 %[t5], %[a5], %[t5]\n\t"
+        "v_sub_f32 %[t7], %[a7], %[t7]\n\t"
+        "v_cvt_pk_f16_f32 %[l0], %[t0], %[t1]\n\t"
+        "v_cvt_pk_f16_f32 %[l1], %[t2], %[t3]\n\t"
+        "v_cvt_pk_f16_f32 %[l2], %[t4], %[t5]\n\t"
+        "v_cvt_pk_f16_f32 %[l3], %[t6], %[t7]\n\t"
+        "s_nop 1"
+        : [h0] "=&v"(h0), [h1] "=&v"(h1), [h2] "=&v"(h2), [h3] "=&v"(h3), [l0] "=&v"(l0), [l1] "=&v"(l1),
+          [l2] "=&v"(l2), [l3] "=&v"(l3), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3),
+          [a4] "=&v"(a4), [a5] "=&v"(a5), [a6] "=&v"(a6), [a7] "=&v"(a7), [t0] "=&v"(t0), [t1] "=&v"(t1),
+          [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7)
+        : [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [v4] "v"(v[4]), [v5] "v"(v[5]),
+          [v6] "v"(v[6]), [v7] "v"(v[7]), [s] "v"(s));
+    hi = make_uint4(h0, h1, h2, h3);
+    lo = make_uint4(l0, l1, l2, l3);
+}
+#else   // SAMNERF_SPLIT_MIX: rounds 1-5's v_fma_mix form (timing A/B)
 __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
     uint32_t h0, h1, h2, h3, l0, l1, l2, l3;
     asm("v_fma_mixlo_f16 %0, %8, %16, 0\n\t"

@@ -37,7 +37,10 @@ constexpr int kChains = 16;
 constexpr int kBlock = 256;
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-enum Kind { kFma = 0, kPkFma = 1, kExp = 2, kInt = 3 };
+enum Kind { kFma = 0, kPkFma = 1, kExp = 2, kInt = 3, kMulLo = 4, kMix = 5, kMaxI = 6, kBitop3 = 7,
+           kCvtPk = 8, kCvtF32 = 9, kCvtF32Hi = 10, kMaxF = 11, kMed3 = 12,
+           kMulF = 13, kAddLshl = 14, kCndmask = 15, kFract = 16, kCvtU32 = 17, kMadU24 = 18, kLshl = 19 };
+constexpr int kKinds = 20;
 
 template <int K>
 __global__ void __launch_bounds__(kBlock) k_valu(float seed, uint32_t iters, float* __restrict__ out,
@@ -69,7 +72,29 @@ __global__ void __launch_bounds__(kBlock) k_valu(float seed, uint32_t iters, flo
                 else if constexpr (K == kPkFma)
                     asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p[j]) : "v"(mm), "v"(cc));
                 else if constexpr (K == kExp) asm volatile("v_exp_f32 %0, %0" : "+v"(a[j]));
-                else asm volatile("v_xor_b32 %0, 0x9e3779b9, %0\n\tv_add_u32 %0, %0, %1" : "+v"(u[j]) : "v"(it));
+                else if constexpr (K == kInt)
+                    asm volatile("v_xor_b32 %0, 0x9e3779b9, %0\n\tv_add_u32 %0, %0, %1" : "+v"(u[j]) : "v"(it));
+                else if constexpr (K == kMulLo) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(u[j]) : "v"(it));
+                // the f16x3 split's instruction: a half-dword write (read-modify-write of %0)
+                else if constexpr (K == kMix) asm volatile("v_fma_mixlo_f16 %0, %1, %2, 0" : "+v"(u[j]) : "v"(m), "v"(c));
+                else if constexpr (K == kMaxI) asm volatile("v_max_i32 %0, %0, %1" : "+v"(u[j]) : "v"(it));
+                else if constexpr (K == kBitop3)
+                    asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(u[j]) : "v"(it), "v"(u[(j + 1) % kChains]));
+                // conversions of a split without v_fma_mix: f32 pair -> packed f16, f16 -> f32 (low / high half)
+                else if constexpr (K == kCvtPk) asm volatile("v_cvt_pk_f16_f32 %0, %1, %0" : "+v"(u[j]) : "v"(m));
+                else if constexpr (K == kCvtF32) asm volatile("v_cvt_f32_f16 %0, %0" : "+v"(u[j]));
+                else if constexpr (K == kCvtF32Hi) asm volatile("v_cvt_f32_f16_sdwa %0, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1" : "+v"(u[j]));
+                else if constexpr (K == kMaxF) asm volatile("v_max_f32 %0, %0, %1" : "+v"(a[j]) : "v"(m));
+                else if constexpr (K == kMed3) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(m), "v"(c));
+                // the index arithmetic of the corner rows
+                else if constexpr (K == kMulF) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a[j]) : "v"(m));
+                else if constexpr (K == kAddLshl) asm volatile("v_add_lshl_u32 %0, %0, %1, 3" : "+v"(u[j]) : "v"(it));
+                else if constexpr (K == kCndmask)
+                    asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(u[j]) : "v"(it) : "vcc");
+                else if constexpr (K == kFract) asm volatile("v_fract_f32 %0, %0" : "+v"(a[j]));
+                else if constexpr (K == kCvtU32) asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(u[j]));
+                else if constexpr (K == kMadU24) asm volatile("v_mad_u32_u24 %0, %0, %1, %1" : "+v"(u[j]) : "v"(it));
+                else asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(u[j]));
             }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -133,17 +158,37 @@ int main(int argc, char** argv) {
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     const uint32_t iters = argc > 1 ? (uint32_t)atoi(argv[1]) : 4096;
     const int waves[5] = {1, 2, 3, 4, 8};
-    const char* kinds[4] = {"v_fma_f32", "v_pk_fma_f32", "v_exp_f32", "v_xor_b32+v_add_u32"};
+    const char* kinds[kKinds] = {"v_fma_f32", "v_pk_fma_f32", "v_exp_f32", "v_xor_b32+v_add_u32",
+                                 "v_mul_lo_u32", "v_fma_mixlo_f16", "v_max_i32", "v_bitop3_b32",
+                                 "v_cvt_pk_f16_f32", "v_cvt_f32_f16", "v_cvt_f32_f16_sdwa_hi", "v_max_f32", "v_med3_f32",
+                                 "v_mul_f32", "v_add_lshl_u32", "v_cndmask_b32", "v_fract_f32", "v_cvt_u32_f32",
+                                 "v_mad_u32_u24", "v_lshlrev_b32"};
     printf("{\"what\": \"independent wave64 VALU instructions per clock per SIMD by resident waves per SIMD "
            "(tools/valu_rate.hip)\", \"cus\": %d, \"iters\": %u, \"kinds\": {", cus, iters);
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < kKinds; ++k) {
         printf("%s\"%s\": {", k ? ", " : "", kinds[k]);
         for (int i = 0; i < 5; ++i) {
             // the integer form issues two instructions per chain step
             Result r = k == kFma ? run<kFma>(cus, waves[i], iters)
                      : k == kPkFma ? run<kPkFma>(cus, waves[i], iters)
                      : k == kExp ? run<kExp>(cus, waves[i], iters / 2)
-                                 : run<kInt>(cus, waves[i], iters);
+                     : k == kInt ? run<kInt>(cus, waves[i], iters)
+                     : k == kMulLo ? run<kMulLo>(cus, waves[i], iters / 2)
+                     : k == kMix ? run<kMix>(cus, waves[i], iters)
+                     : k == kMaxI ? run<kMaxI>(cus, waves[i], iters)
+                     : k == kBitop3 ? run<kBitop3>(cus, waves[i], iters)
+                     : k == kCvtPk ? run<kCvtPk>(cus, waves[i], iters)
+                     : k == kCvtF32 ? run<kCvtF32>(cus, waves[i], iters)
+                     : k == kCvtF32Hi ? run<kCvtF32Hi>(cus, waves[i], iters)
+                     : k == kMaxF ? run<kMaxF>(cus, waves[i], iters)
+                     : k == kMed3 ? run<kMed3>(cus, waves[i], iters)
+                     : k == kMulF ? run<kMulF>(cus, waves[i], iters)
+                     : k == kAddLshl ? run<kAddLshl>(cus, waves[i], iters)
+                     : k == kCndmask ? run<kCndmask>(cus, waves[i], iters)
+                     : k == kFract ? run<kFract>(cus, waves[i], iters)
+                     : k == kCvtU32 ? run<kCvtU32>(cus, waves[i], iters)
+                     : k == kMadU24 ? run<kMadU24>(cus, waves[i], iters)
+                                    : run<kLshl>(cus, waves[i], iters);
             if (k == kInt) {
                 r.inst_per_clk_simd *= 2.0;
                 r.cycles_per_inst = 1.0 / r.inst_per_clk_simd;
