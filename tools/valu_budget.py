@@ -18,7 +18,12 @@ per-sample-step instruction mix of one wave.  Phases, in program order:
             fragment reads, boundary (max / ReLU / exponent / permlane)
   composite sigma = exp, alpha, the double cumulative sum, weights, stores
 Counts are static instructions per loop trip (divergent branches of the
-position counted once), the VALU column is what issues on the VALU pipe.
+position counted once), the VALU column is what issues on the VALU pipe, and
+`cycles` prices each VALU instruction at its measured issue cost per wave64
+at 8 waves per SIMD (profiles/r5v_valu_rate.json, tools/valu_rate.hip):
+2.2 cycles for the double-rate fp32 fma / mul / add / sub and integer add /
+xor / and / or, 2.5 for v_bitop3, 4.2 for packed fp32 and everything else
+4.1, 8.1 for v_fma_mix and the transcendentals.
 """
 import collections
 import re
@@ -65,6 +70,23 @@ def ops(body):
         yield t.split()[0]
 
 
+FAST = ("v_fma_f32", "v_fmac_f32", "v_mul_f32", "v_add_f32", "v_sub_f32", "v_subrev_f32", "v_add_u32",
+        "v_sub_u32", "v_subrev_u32", "v_xor_b32", "v_and_b32", "v_or_b32")
+SLOW = ("v_fma_mix", "v_exp_f32", "v_log_f32", "v_rcp_f32", "v_rsq_f32", "v_sqrt_f32", "v_sin_f32", "v_cos_f32")
+
+
+def cycles(op):
+    if op.startswith(SLOW):
+        return 8.1
+    if op.startswith(FAST):
+        return 2.2
+    if op.startswith("v_bitop3"):
+        return 2.5
+    if op.startswith("v_pk_"):
+        return 4.2
+    return 4.1
+
+
 def is_gather(op):
     return op in ("global_load_dwordx2", "global_load_dwordx4")
 
@@ -82,7 +104,7 @@ def main():
     last_mfma = max(i for i, o in enumerate(seq) if o.startswith("v_mfma"))
     for i, op in enumerate(seq):
         if not in_mlp:
-            if op.startswith("v_fma_mix"):
+            if op.startswith(("v_fma_mix", "v_cvt_pk_f16_f32")):
                 in_mlp = True
             else:
                 p = phases[ph]
@@ -99,7 +121,7 @@ def main():
                 continue
         if i > last_mfma:
             cnt["composite"][op] += 1
-        elif op.startswith("v_fma_mix"):
+        elif op.startswith(("v_fma_mix", "v_cvt_pk_f16_f32", "v_cvt_f32_f16", "v_mul_f32", "v_sub_f32")):
             cnt["mlp:split"][op] += 1
         elif op.startswith("v_mfma"):
             cnt["mlp:mfma"][op] += 1
@@ -108,7 +130,7 @@ def main():
         else:
             cnt["mlp:boundary"][op] += 1
     tot = collections.Counter()
-    print(f"{'phase':<14}{'instr':>7}{'VALU':>7}{'VMEM':>6}{'LDS':>5}{'SALU':>6}{'nop':>5}  top opcodes")
+    print(f"{'phase':<14}{'instr':>7}{'VALU':>7}{'cycles':>8}{'VMEM':>6}{'LDS':>5}{'SALU':>6}{'nop':>5}  top opcodes")
     for p, c in cnt.items():
         n = sum(c.values())
         valu = sum(v for k, v in c.items() if k.startswith("v_") and not k.startswith("v_mfma"))
@@ -116,10 +138,12 @@ def main():
         lds = sum(v for k, v in c.items() if k.startswith("ds_"))
         salu = sum(v for k, v in c.items() if k.startswith("s_") and not k.startswith(("s_nop", "s_waitcnt")))
         nop = c.get("s_nop", 0)
-        tot.update({"instr": n, "valu": valu, "vmem": vmem, "lds": lds, "salu": salu, "nop": nop})
+        cyc = sum(v * cycles(k) for k, v in c.items() if k.startswith("v_") and not k.startswith("v_mfma"))
+        tot.update({"instr": n, "valu": valu, "vmem": vmem, "lds": lds, "salu": salu, "nop": nop, "cyc": cyc})
         top = ", ".join(f"{k} {v}" for k, v in c.most_common(4))
-        print(f"{p:<14}{n:>7}{valu:>7}{vmem:>6}{lds:>5}{salu:>6}{nop:>5}  {top}")
-    print(f"{'total':<14}{tot['instr']:>7}{tot['valu']:>7}{tot['vmem']:>6}{tot['lds']:>5}{tot['salu']:>6}{tot['nop']:>5}")
+        print(f"{p:<14}{n:>7}{valu:>7}{cyc:>8.0f}{vmem:>6}{lds:>5}{salu:>6}{nop:>5}  {top}")
+    print(f"{'total':<14}{tot['instr']:>7}{tot['valu']:>7}{tot['cyc']:>8.0f}{tot['vmem']:>6}{tot['lds']:>5}"
+          f"{tot['salu']:>6}{tot['nop']:>5}")
 
 
 if __name__ == "__main__":
