@@ -10,6 +10,8 @@
 //   x2_half global_load_dwordx2 with the odd lanes masked off (32 lanes)
 //   pair    one x4 (64 lanes) + one x2 on the odd lanes: the x-pair form of
 //           two x2 corner loads
+//   x2_g8   global_load_dwordx2, 64 lanes in 8 groups of 8 that share an address
+//   x2_uni  global_load_dwordx2, all 64 lanes one address
 // Printed: wave-instructions per clock per CU and clocks per 64-lane
 // instruction (ns from events, the in-kernel clock as in ta_rate.hip).
 //
@@ -35,7 +37,7 @@
 constexpr int kPerLane = 16;
 constexpr uint32_t kTableBytes = 16384;
 constexpr int kBlock = 256;
-enum Pattern { kX2 = 0, kX4 = 1, kX2Half = 2, kPair = 3 };
+enum Pattern { kX2 = 0, kX4 = 1, kX2Half = 2, kPair = 3, kX2G8 = 4, kX2Uni = 5 };
 
 template <int P>
 __global__ void __launch_bounds__(kBlock) k_gather(const char* __restrict__ table, const uint32_t* __restrict__ offs,
@@ -44,8 +46,10 @@ __global__ void __launch_bounds__(kBlock) k_gather(const char* __restrict__ tabl
     const uint32_t tid = blockIdx.x * kBlock + threadIdx.x;
     const bool odd = threadIdx.x & 1u;
     uint32_t o[kPerLane];
+    // the groups read their first lane's offset (x2_g8: lanes 8g .. 8g+7; x2_uni: the wave)
+    const uint32_t src = P == kX2G8 ? (tid & ~7u) : P == kX2Uni ? (tid & ~63u) : tid;
 #pragma unroll
-    for (int j = 0; j < kPerLane; ++j) o[j] = offs[(size_t)j * gridDim.x * kBlock + tid];   // 16-B aligned
+    for (int j = 0; j < kPerLane; ++j) o[j] = offs[(size_t)j * gridDim.x * kBlock + src];   // 16-B aligned
     uint32_t acc = 0;
     unsigned long long t0, r0, t1, r1;
     __builtin_amdgcn_sched_barrier(0);
@@ -55,7 +59,7 @@ __global__ void __launch_bounds__(kBlock) k_gather(const char* __restrict__ tabl
         const char* b = table + ((it & 1u) << 4);     // keeps the loads in the loop
         // one exec-masked region per trip (16 loads issued, then consumed), as
         // a kernel's level batch would be
-        if constexpr (P == kX2) {
+        if constexpr (P == kX2 || P == kX2G8 || P == kX2Uni) {
 #pragma unroll
             for (int j = 0; j < kPerLane; ++j) {
                 const uint2 v = *reinterpret_cast<const uint2*>(b + o[j]);
@@ -144,6 +148,8 @@ int main() {
     run<kX4>("x4", table, offs, blocks, iters, cus, false);
     run<kX2Half>("x2_half", table, offs, blocks, iters, cus, false);
     run<kPair>("pair_x4_plus_x2_odd", table, offs, blocks, iters, cus, false);
+    run<kX2G8>("x2_groups_of_8", table, offs, blocks, iters, cus, false);
+    run<kX2Uni>("x2_uniform", table, offs, blocks, iters, cus, false);
     printf("}}\n");
     CHECK(hipFree(offs));
     CHECK(hipFree(table));
