@@ -887,6 +887,18 @@ __device__ __forceinline__ void gather_levels_c2(const float2* __restrict__ emb,
 #ifndef SAMNERF_PROP_UNI
 #define SAMNERF_PROP_UNI 1
 #endif
+// PROP_TWO (round 5, late): a dense level whose lanes sit in two cells (the
+// wave straddles one cell boundary) reads both cells' 4 corner pairs through
+// the scalar cache and each lane takes its cell's 16 floats by v_cndmask.  A
+// 64-lane gather costs the address path at least 16 clocks per CU whatever
+// the sharing (tools/ta_mask.hip: 4 lane-addresses per clock), while the
+// selects cost 16 VALU on one SIMD of four.  Same rows, weights and FMA order
+// (bit-identical on every tools/lib_bits.py workload), but measured slower:
+// prop0 0.575 -> 0.62 ms, prop1 0.292 -> 0.289 (profiles/r5two_prop_two_cell_ab.txt):
+// the scalar loads of the second cell add latency the vector path hides.  Off.
+#ifndef SAMNERF_PROP_TWO
+#define SAMNERF_PROP_TWO 0
+#endif
 
 template <uint32_t KD, uint32_t KH>
 __device__ __forceinline__ void prop_lookup_lay(const PropArgs& a, float x, float y, float z, float* feat) {
@@ -903,7 +915,8 @@ __device__ __forceinline__ void prop_lookup_lay(const PropArgs& a, float x, floa
     const uint64_t live = __builtin_amdgcn_read_exec();
     GatherC2<5> g;
     uint32_t row[5][8];
-    bool uni[5];
+    bool uni[5], two[5], in1[5];
+    uint32_t lane1[5];
 #pragma unroll
     for (int l = 0; l < 5; ++l) {
         const LevelDesc& d = a.grid.lv[l];
@@ -914,11 +927,27 @@ __device__ __forceinline__ void prop_lookup_lay(const PropArgs& a, float x, floa
         const uint32_t top = d.res - 1u;
         const uint32_t ny = min(cy + 1u, top), nz = min(cz + 1u, top);
         uni[l] = false;
+        two[l] = false;
+        in1[l] = false;
+        lane1[l] = 0u;
         if ((KD >> l) & 1u) {
             // one cell for every live lane (wave-uniform: a ballot)
             const uint32_t c0 = __builtin_amdgcn_readfirstlane(cx), c1 = __builtin_amdgcn_readfirstlane(cy),
                            c2 = __builtin_amdgcn_readfirstlane(cz);
-            uni[l] = __builtin_amdgcn_ballot_w64(cx == c0 && cy == c1 && cz == c2) == live;
+            const bool same0 = cx == c0 && cy == c1 && cz == c2;
+            const uint64_t m0 = __builtin_amdgcn_ballot_w64(same0);
+            uni[l] = m0 == live;
+            if (SAMNERF_PROP_TWO && !uni[l]) {
+                // the first lane outside cell 0 names cell 1; two cells if
+                // every live lane is in one of them
+                const uint32_t j = (uint32_t)__builtin_ctzll(live & ~m0);
+                const bool same1 = cx == (uint32_t)__builtin_amdgcn_readlane((int)cx, (int)j) &&
+                                   cy == (uint32_t)__builtin_amdgcn_readlane((int)cy, (int)j) &&
+                                   cz == (uint32_t)__builtin_amdgcn_readlane((int)cz, (int)j);
+                two[l] = __builtin_amdgcn_ballot_w64(same0 || same1) == live;
+                in1[l] = same1;
+                lane1[l] = j;
+            }
             const bool edge = cx == top;                   // gather_issue_c2's top-cell pair
             g.fx[l] = edge ? 1.0f : g.fx[l];
             const uint32_t bx = d.off + (edge ? cx - 1u : cx);
@@ -946,6 +975,16 @@ __device__ __forceinline__ void prop_lookup_lay(const PropArgs& a, float x, floa
                     const f4a8 v = *reinterpret_cast<const f4a8*>(base + __builtin_amdgcn_readfirstlane(row[l][p]));
                     g.e[l][2 * p] = make_float2(v.x, v.y);
                     g.e[l][2 * p + 1] = make_float2(v.z, v.w);
+                }
+            } else if (SAMNERF_PROP_TWO && two[l]) {       // two cells: both by scalar loads, a select per lane
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const f4a8 v0 = *reinterpret_cast<const f4a8*>(base + __builtin_amdgcn_readfirstlane(row[l][p]));
+                    const f4a8 v1 = *reinterpret_cast<const f4a8*>(
+                        base + (uint32_t)__builtin_amdgcn_readlane((int)row[l][p], (int)lane1[l]));
+                    const bool b = in1[l];
+                    g.e[l][2 * p] = make_float2(b ? v1.x : v0.x, b ? v1.y : v0.y);
+                    g.e[l][2 * p + 1] = make_float2(b ? v1.z : v0.z, b ? v1.w : v0.w);
                 }
             } else {
 #pragma unroll
