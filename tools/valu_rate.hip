@@ -39,8 +39,8 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 
 enum Kind { kFma = 0, kPkFma = 1, kExp = 2, kInt = 3, kMulLo = 4, kMix = 5, kMaxI = 6, kBitop3 = 7,
            kCvtPk = 8, kCvtF32 = 9, kCvtF32Hi = 10, kMaxF = 11, kMed3 = 12,
-           kMulF = 13, kAddLshl = 14, kCndmask = 15, kFract = 16, kCvtU32 = 17, kMadU24 = 18, kLshl = 19 };
-constexpr int kKinds = 20;
+           kMulF = 13, kAddLshl = 14, kCndmask = 15, kFract = 16, kCvtU32 = 17, kMadU24 = 18, kLshl = 19, kCndS = 20, kCndV = 21 };
+constexpr int kKinds = 22;
 
 template <int K>
 __global__ void __launch_bounds__(kBlock) k_valu(float seed, uint32_t iters, float* __restrict__ out,
@@ -55,6 +55,7 @@ __global__ void __launch_bounds__(kBlock) k_valu(float seed, uint32_t iters, flo
         u[j] = (uint32_t)threadIdx.x * 2654435761u + (uint32_t)j;
     }
     const float m = seed * 1e-3f + 0.999f, c = seed * 1e-7f;
+    const unsigned long long smask = __builtin_amdgcn_read_exec() & 0x5555555555555555ull;
     const f2v mm = {m, m}, cc = {c, c};
     unsigned long long t0, r0, t1, r1;
     __builtin_amdgcn_sched_barrier(0);
@@ -94,7 +95,11 @@ __global__ void __launch_bounds__(kBlock) k_valu(float seed, uint32_t iters, flo
                 else if constexpr (K == kFract) asm volatile("v_fract_f32 %0, %0" : "+v"(a[j]));
                 else if constexpr (K == kCvtU32) asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(u[j]));
                 else if constexpr (K == kMadU24) asm volatile("v_mad_u32_u24 %0, %0, %1, %1" : "+v"(u[j]) : "v"(it));
-                else asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(u[j]));
+                else if constexpr (K == kLshl) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(u[j]));
+                // v_cndmask on a 64-bit SGPR condition (e64), and on a compare result written each step
+                else if constexpr (K == kCndS)
+                    asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(u[j]) : "v"(it), "s"(smask));
+                else asm volatile("v_cmp_gt_u32 vcc, %1, %0\n\tv_cndmask_b32 %0, %0, %1, vcc" : "+v"(u[j]) : "v"(it) : "vcc");
             }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -161,8 +166,8 @@ int main(int argc, char** argv) {
     const char* kinds[kKinds] = {"v_fma_f32", "v_pk_fma_f32", "v_exp_f32", "v_xor_b32+v_add_u32",
                                  "v_mul_lo_u32", "v_fma_mixlo_f16", "v_max_i32", "v_bitop3_b32",
                                  "v_cvt_pk_f16_f32", "v_cvt_f32_f16", "v_cvt_f32_f16_sdwa_hi", "v_max_f32", "v_med3_f32",
-                                 "v_mul_f32", "v_add_lshl_u32", "v_cndmask_b32", "v_fract_f32", "v_cvt_u32_f32",
-                                 "v_mad_u32_u24", "v_lshlrev_b32"};
+                                 "v_mul_f32", "v_add_lshl_u32", "v_cndmask_b32_vcc_clobber_artifact", "v_fract_f32", "v_cvt_u32_f32",
+                                 "v_mad_u32_u24", "v_lshlrev_b32", "v_cndmask_b32_e64_sgpr", "v_cmp+v_cndmask_vcc"};
     printf("{\"what\": \"independent wave64 VALU instructions per clock per SIMD by resident waves per SIMD "
            "(tools/valu_rate.hip)\", \"cus\": %d, \"iters\": %u, \"kinds\": {", cus, iters);
     for (int k = 0; k < kKinds; ++k) {
@@ -188,8 +193,10 @@ int main(int argc, char** argv) {
                      : k == kFract ? run<kFract>(cus, waves[i], iters)
                      : k == kCvtU32 ? run<kCvtU32>(cus, waves[i], iters)
                      : k == kMadU24 ? run<kMadU24>(cus, waves[i], iters)
-                                    : run<kLshl>(cus, waves[i], iters);
-            if (k == kInt) {
+                     : k == kLshl ? run<kLshl>(cus, waves[i], iters)
+                     : k == kCndS ? run<kCndS>(cus, waves[i], iters)
+                                  : run<kCndV>(cus, waves[i], iters);
+            if (k == kInt || k == kCndV) {
                 r.inst_per_clk_simd *= 2.0;
                 r.cycles_per_inst = 1.0 / r.inst_per_clk_simd;
             }
