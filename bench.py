@@ -776,6 +776,16 @@ def explain_gather(runner, views=5):
 
 
 VALU_RATE = os.path.join(REPO, "profiles", "r4_valu_rate.json")
+# per-stage issue cycles per VALU instruction: the stage kernel's opcode mix x
+# the measured per-opcode rates (tools/valu_cpi.py, round 5)
+VALU_CPI = os.path.join(REPO, "profiles", "r5_valu_cpi.json")
+
+
+def valu_cpi_of_stages():
+    try:
+        return {k: v["cycles_per_inst"] for k, v in json.load(open(VALU_CPI))["stages"].items()}
+    except Exception:
+        return {}
 
 
 def valu_cycles_per_inst():
@@ -797,9 +807,11 @@ def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None):
               / live time vs the L2's 34.5 TB/s (the tables are L2/MALL-resident;
               not for s_grid, whose box gathers read a row once per wave);
       valu -- the VALU pipe's share: issued VALU instructions (PMC SQ_INSTS_VALU
-              per ray, profiles/pmc_rates.json) x the measured cycles per
-              instruction at saturation (tools/valu_rate.hip: 2, the guide's
-              SIMD-32 rate) / (1024 SIMDs x 2.4 GHz x live time);
+              per ray, profiles/pmc_rates.json) x the stage kernel's issue
+              cycles per instruction (profiles/r5_valu_cpi.json: its opcode
+              mix priced at the measured per-opcode rates, 3.5-3.75; without
+              the file the v_fma_f32 rate, 2.2) / (1024 SIMDs x 2.4 GHz x
+              live time);
       mfma -- MFMA-busy cycles (PMC SQ_VALU_MFMA_BUSY_CYCLES per ray) over the
               same SIMD cycles; for the SAM head also from its structure (86
               k-blocks x 8 tiles x 3 v_mfma_f32_32x32x16_f16 per 32 rays).
@@ -811,6 +823,7 @@ def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None):
     st_rates = (rates or {}).get("stages", {})
     cyc_avail = lambda ms: N_SIMD * CLOCK_GHZ * 1e9 * ms * 1e-3
     cpi, cpi_src = valu_cycles_per_inst()
+    stage_cpi = valu_cpi_of_stages()
 
     def entry(st):
         ms = stage_avg.get(st, 0.0)
@@ -824,10 +837,11 @@ def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None):
                           "alg_bytes_per_ray": ALG_BYTES_PER_RAY[st]}
             cand["l2"]["frac"] = cand["l2"]["achieved"] / L2_PEAK_GBS
         if "valu_insts_per_ray" in r:
-            c = r["valu_insts_per_ray"] * band_rays * cpi
+            ci, ci_src = (stage_cpi[st], os.path.relpath(VALU_CPI, REPO)) if st in stage_cpi else (cpi, cpi_src)
+            c = r["valu_insts_per_ray"] * band_rays * ci
             cand["valu"] = {"unit": "VALU pipe cycles / SIMD cycles", "frac": c / cyc_avail(ms),
-                            "valu_insts_per_ray": r["valu_insts_per_ray"], "cycles_per_inst": cpi,
-                            "cycles_per_inst_source": cpi_src}
+                            "valu_insts_per_ray": r["valu_insts_per_ray"], "cycles_per_inst": ci,
+                            "cycles_per_inst_source": ci_src}
         if st == "sam_head":
             cyc = HEAD_MFMA_CYCLES_PER_32[head_mode] * band_rays / 32
             cand["mfma"] = {"unit": "TFLOP/s", "frac": cyc / cyc_avail(ms),
