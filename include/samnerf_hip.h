@@ -340,12 +340,18 @@ int samnerf_sgrid_backward(const samnerf_model* model, const float* grad_fsam, u
  * reach a row in), at the scale 2^(61 - ceil(log2 N) - e) with max |grad_fsam|
  * < 2^e, so no total can overflow and each is resolved to max|g| 2^-(61 -
  * ceil(log2 N)); then the totals are added to grad_embeddings as fp32.
- * accum: samnerf_sgrid_accum_size(model) bytes of device memory, all zero on
- * the first call (hipMemset) and left zero by every call. */
+ * accum: accum_bytes >= samnerf_sgrid_accum_size(model) bytes of device
+ * memory (else SAMNERF_EWORKSPACE), all zero on the first call (hipMemset)
+ * and left zero by every call; one accumulator per stream (calls on one
+ * stream run in order; concurrent calls must not share one).  A grad_fsam
+ * holding a NaN or an Inf has no fixed-point scale: such a call adds with
+ * the fp32 atomics, so the NaN / Inf reaches grad_embeddings as in the
+ * reference (bits repeat for finite gradients only). */
 size_t samnerf_sgrid_accum_size(const samnerf_model* model);
 int samnerf_sgrid_backward_det(const samnerf_model* model, const float* grad_fsam, uint32_t N,
-                               float* grad_embeddings, int64_t* accum, const void* workspace,
-                               size_t workspace_bytes, samnerf_stream_t stream);
+                               float* grad_embeddings, int64_t* accum, size_t accum_bytes,
+                               const void* workspace, size_t workspace_bytes,
+                               samnerf_stream_t stream);
 
 /* ------------------------------------------------------------- training --
  * One Adam step (torch.optim.Adam semantics, amsgrad off, maximize off) over

@@ -180,6 +180,13 @@ struct PropArgs {
     const float* pu;
     const float* bins_in;  // [T+1][N] (stages > 0)
     float* snf;            // [2][N] spacing(near), spacing(far)
+    // [N][2] slot-ordered ray records {o.xyz, spacing(near)}, {d.xyz,
+    // spacing(far)} (k_snf; null: not written).  The proposal sigma kernels
+    // read a sample's ray in two coalesced 16-B loads from its slot, instead of
+    // mapping slot -> ray (RayTiles) and gathering rays_o / rays_d / snf in
+    // four loads of 64-bit addresses: the proposal stages are bound by vector
+    // issue and the vector-memory address path.
+    float4* rec;
     float* wtmp;           // [T][N]: ds per sample
     float* bins_out;       // [TN][N]
     int32_t* inds_out;     // [TN][N] searchsorted indices, or null (parity taps only)
@@ -252,15 +259,29 @@ k_prop_sigma(PropArgs a) {
     if (LOOK != kLookBox4 && r0 >= a.N) return;
     const bool live = r0 < a.N;
     const uint32_t r = live ? r0 : a.N - 1u;              // slot
-    const uint32_t N = a.N, ray = a.tiles(r);
-    float o[3], d[3];
+    const uint32_t N = a.N;
+    // the LAY forms read k_snf's slot-ordered ray record (the ray id is then
+    // needed only for perturb's per-ray bins); the others map slot -> ray
+    constexpr bool REC = (KD | KH) == 0x1Fu && LOOK == kLookPacked;
+    float o[3], d[3], sn, sf;
+    if constexpr (REC) {
+        const char* rbase = reinterpret_cast<const char*>(a.rec);     // 32-bit offsets: saddr loads
+        const float4 ra = *reinterpret_cast<const float4*>(rbase + r * 32u),
+                     rb = *reinterpret_cast<const float4*>(rbase + r * 32u + 16u);
+        o[0] = ra.x, o[1] = ra.y, o[2] = ra.z, sn = ra.w;
+        d[0] = rb.x, d[1] = rb.y, d[2] = rb.z, sf = rb.w;
+    } else {
+        const uint32_t ray = a.tiles(r);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        o[c] = a.rays_o[(size_t)ray * 3 + c];
-        d[c] = a.rays_d[(size_t)ray * 3 + c];
+        for (int c = 0; c < 3; ++c) {
+            o[c] = a.rays_o[(size_t)ray * 3 + c];
+            d[c] = a.rays_d[(size_t)ray * 3 + c];
+        }
+        sn = a.snf[r], sf = a.snf[N + r];                   // k_snf (stage 0) / stage 0 (stage 1)
     }
-    const float sn = a.snf[r], sf = a.snf[N + r];           // k_snf (stage 0) / stage 0 (stage 1)
-    const float b0 = stage_bin<T, FIRST>(a, (int)k, r, ray), b1 = stage_bin<T, FIRST>(a, (int)k + 1, r, ray);
+    // the ray id: only perturb's per-ray bins need it (FIRST)
+    const uint32_t pray = (FIRST && a.pbins0) ? a.tiles(r) : 0u;
+    const float b0 = stage_bin<T, FIRST>(a, (int)k, r, pray), b1 = stage_bin<T, FIRST>(a, (int)k + 1, r, pray);
     const float rb_prev = real_bin(sn, sf, b0), rb_next = real_bin(sn, sf, b1);
     const float t = (rb_next + rb_prev) / 2.0f;
     float x = o[0] + d[0] * t, y = o[1] + d[1] * t, z = o[2] + d[2] * t;
@@ -337,8 +358,13 @@ __global__ void __launch_bounds__(256) k_snf(PropArgs a) {
         near = (isnan(near) || isnan(cn)) ? NAN : fmaxf(near, cn);
         far = (isnan(far) || isnan(cf)) ? NAN : fminf(far, cf);
     }
-    a.snf[r] = spacing(near);
-    a.snf[a.N + r] = spacing(far);
+    const float sn = spacing(near), sf = spacing(far);
+    a.snf[r] = sn;
+    a.snf[a.N + r] = sf;
+    if (a.rec) {
+        a.rec[2 * (size_t)r] = make_float4(o[0], o[1], o[2], sn);
+        a.rec[2 * (size_t)r + 1] = make_float4(d[0], d[1], d[2], sf);
+    }
 }
 
 // Proposal stage, part 2 (renderer.py:84-119 and 300-307), 64 rays per block.
@@ -510,6 +536,13 @@ struct FinalArgs {
     // SGPR-bound reloads, lgkmcnt waits); LDS: 0.82 ms.
     GridDesc<16> grid;
     uint32_t kdense[2], khashed[2];   // wave-uniform slot classes of k-blocks 0 / 1 (host-side)
+    // LAY 1's hashed slots (round 6): byte offset of the slot's half-wave-0
+    // level (emb + hoff8 is a uniform SGPR base); half-wave 1's level is the
+    // next one, hbit = its byte distance 8 S (S = the levels' common power-of-
+    // two size, above every masked row bit), hm8 = 8 (S - 1)  (final_layout
+    // admits LAY 1 only when every hashed slot is laid out so)
+    uint32_t hoff8[2][4];
+    uint32_t hbit, hm8;
     const float* grid_emb;  // == grid.emb, as a kernel argument so gathers are global_load (not flat)
     const float* G0;   // grid_mlp [64,32]
     const float* G1;   // [64,64]
@@ -728,6 +761,19 @@ struct SlotKinds {
     uint32_t dense, hashed;
 };
 
+// Hashed slots of a LAY 1 k-block (k_final, round 6): the table base of each
+// slot's half-wave-0 level (uniform), this lane's half-wave bit (0, or the
+// byte distance to the next level) and the byte mask.  A corner's byte offset
+// from the slot base is then X8 ^ Y8 ^ Z8 with the per-axis terms pre-shifted
+// by 3 and pre-masked (AND distributes over XOR) and the half-wave bit folded
+// into X8 (it sits above every masked bit): one v_xor_b32 per corner where
+// v_bitop3 + v_add_lshl_u32 took 6.6 cycles (profiles/r5v_valu_rate.json).
+// Same rows as the reference's (x ^ y P1 ^ z P2) & (S - 1) at offset off.
+struct HashSlots {
+    const char* base[4];
+    uint32_t hx, m8;
+};
+
 // tap (parity taps only, samnerf_taps.rows2; null otherwise): the level-
 // relative row each corner weight multiplies, tap[l * tap_ls + c] for slot l
 // and corner c (bit 0 x, 1 y, 2 z, as gridencoder.cu:61-79 / the oracle's
@@ -737,7 +783,8 @@ template <int NL>
 __device__ __forceinline__ void gather_issue_c2(const float2* __restrict__ emb, const LevelDesc* d,
                                                 float ux, float uy, float uz, GatherC2<NL>& g,
                                                 SlotKinds kinds = SlotKinds{0u, 0u},
-                                                uint32_t* tap = nullptr, int tap_ls = 8) {
+                                                uint32_t* tap = nullptr, int tap_ls = 8,
+                                                const HashSlots* hs = nullptr) {
     // byte offsets of every corner (dense-pair slots: of the 4 pairs) first,
     // then all loads, so they are in flight together
     uint32_t row[NL][8];
@@ -763,6 +810,14 @@ __device__ __forceinline__ void gather_issue_c2(const float2* __restrict__ emb, 
             const uint32_t Z[2] = {(uint32_t)__umul24(cz, r2), (uint32_t)__umul24(nz, r2)};
 #pragma unroll
             for (int p = 0; p < 4; ++p) row[l][p] = (bx + Y[p & 1] + Z[p >> 1]) << 3;
+        } else if (((kinds.hashed >> l) & 1u) && hs) {
+            // byte offsets from the slot base hs->base[l] (HashSlots)
+            const uint32_t m8 = hs->m8;
+            const uint32_t X[2] = {(cx << 3) | hs->hx, ((uint32_t)min(cx + 1u, top) << 3) | hs->hx};
+            const uint32_t Y[2] = {(cy * (kPrime1 << 3)) & m8, (ny * (kPrime1 << 3)) & m8};
+            const uint32_t Z[2] = {(cz * (kPrime2 << 3)) & m8, (nz * (kPrime2 << 3)) & m8};
+#pragma unroll
+            for (int c = 0; c < 8; ++c) row[l][c] = X[c & 1] ^ Y[(c >> 1) & 1] ^ Z[c >> 2];
         } else if ((kinds.hashed >> l) & 1u) {
             const uint32_t mask = d[l].size - 1u;
             const uint32_t X[2] = {cx, min(cx + 1u, top)};
@@ -801,6 +856,9 @@ __device__ __forceinline__ void gather_issue_c2(const float2* __restrict__ emb, 
                     tap[l * tap_ls + 2 * p] = r0;
                     tap[l * tap_ls + 2 * p + 1] = r0 + 1u;
                 }
+            } else if (((kinds.hashed >> l) & 1u) && hs) {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) tap[l * tap_ls + c] = (row[l][c] & hs->m8) >> 3;
             } else {
 #pragma unroll
                 for (int c = 0; c < 8; ++c) tap[l * tap_ls + c] = (row[l][c] >> 3) - d[l].off;
@@ -819,8 +877,9 @@ __device__ __forceinline__ void gather_issue_c2(const float2* __restrict__ emb, 
                 g.e[l][2 * p + 1] = make_float2(v.z, v.w);
             }
         } else {
+            const char* lb = (((kinds.hashed >> l) & 1u) && hs) ? hs->base[l] : base;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) g.e[l][c] = *reinterpret_cast<const float2*>(base + row[l][c]);
+            for (int c = 0; c < 8; ++c) g.e[l][c] = *reinterpret_cast<const float2*>(lb + row[l][c]);
         }
     }
 }
@@ -887,19 +946,30 @@ __device__ __forceinline__ void gather_levels_c2(const float2* __restrict__ emb,
 #ifndef SAMNERF_PROP_UNI
 #define SAMNERF_PROP_UNI 1
 #endif
-// PROP_TWO (round 5, late): a dense level whose lanes sit in two cells (the
-// wave straddles one cell boundary) reads both cells' 4 corner pairs through
-// the scalar cache and each lane takes its cell's 16 floats by v_cndmask.  A
-// 64-lane gather costs the address path at least 16 clocks per CU whatever
-// the sharing (tools/ta_mask.hip: 4 lane-addresses per clock), while the
-// selects cost 16 VALU on one SIMD of four.  Same rows, weights and FMA order
-// (bit-identical on every tools/lib_bits.py workload), but measured slower:
-// prop0 0.575 -> 0.62 ms, prop1 0.292 -> 0.289 (profiles/r5two_prop_two_cell_ab.txt):
-// the scalar loads of the second cell add latency the vector path hides.  Off.
-#ifndef SAMNERF_PROP_TWO
-#define SAMNERF_PROP_TWO 0
-#endif
+// PROP_TWO (round 5, late; removed in round 6): a dense level whose lanes sit
+// in two cells read both cells' corner pairs through the scalar cache and
+// took each lane's by v_cndmask -- bit-identical but slower (prop0 0.575 ->
+// 0.62 ms, profiles/r5two_prop_two_cell_ab.txt): the second cell's scalar
+// loads add latency the vector path hides.
 
+// Round 6, the same rows, weights and FMA order (same
+// bits), fewer VALU cycles per sample:
+//  * hashed levels: the table base of the level (emb + 8 off) is a uniform
+//    SGPR pair, and the per-axis hash terms are kept pre-shifted and
+//    pre-masked in bytes -- X8 = 8 x, Y8 = (y P1 8) & M8, Z8 = (z P2 8) & M8
+//    with M8 = 8 (size - 1), since AND distributes over XOR and the shift
+//    commutes with both -- so a corner's byte offset 8 ((x ^ y P1 ^ z P2) &
+//    (size - 1)) is ONE v_xor_b32 (2.2 cycles per wave64 instruction,
+//    profiles/r5v_valu_rate.json) where v_bitop3 + v_add_lshl_u32 took 6.6
+//    (the host admits the form only with res <= size, so X8 needs no mask);
+//  * uniform dense levels: the corner sums read the scalar-loaded rows as
+//    SGPR operands of the packed FMAs in their own branch.  The round-5 form
+//    joined them with the vector path's rows before one shared sum, and the
+//    join copied 16 SGPRs to VGPRs per level (v_mov_b32 at 4.1 cycles; the
+//    compiler also merged the fourth corner pair into a vector load).
+#ifndef SAMNERF_PROP_SPLIT
+#define SAMNERF_PROP_SPLIT 1
+#endif
 template <uint32_t KD, uint32_t KH>
 __device__ __forceinline__ void prop_lookup_lay(const PropArgs& a, float x, float y, float z, float* feat) {
     const float ux = (x + a.gs.bound) * a.gs.inv_b2, uy = (y + a.gs.bound) * a.gs.inv_b2,
@@ -913,93 +983,126 @@ __device__ __forceinline__ void prop_lookup_lay(const PropArgs& a, float x, floa
     }
     const char* base = reinterpret_cast<const char*>(a.grid.emb);
     const uint64_t live = __builtin_amdgcn_read_exec();
-    GatherC2<5> g;
+    float fx[5], fy[5], fz[5];
     uint32_t row[5][8];
-    bool uni[5], two[5], in1[5];
-    uint32_t lane1[5];
+    bool uni[5];
 #pragma unroll
     for (int l = 0; l < 5; ++l) {
-        const LevelDesc& d = a.grid.lv[l];
-        uint32_t cx, cy, cz;
-        locate_axis(ux, d, cx, g.fx[l]);
-        locate_axis(uy, d, cy, g.fy[l]);
-        locate_axis(uz, d, cz, g.fz[l]);
-        const uint32_t top = d.res - 1u;
-        const uint32_t ny = min(cy + 1u, top), nz = min(cz + 1u, top);
         uni[l] = false;
-        two[l] = false;
-        in1[l] = false;
-        lane1[l] = 0u;
         if ((KD >> l) & 1u) {
+            const LevelDesc& d = a.grid.lv[l];
+            uint32_t cx, cy, cz;
+            locate_axis(ux, d, cx, fx[l]);
+            locate_axis(uy, d, cy, fy[l]);
+            locate_axis(uz, d, cz, fz[l]);
+            const uint32_t top = d.res - 1u;
+            const uint32_t ny = min(cy + 1u, top), nz = min(cz + 1u, top);
             // one cell for every live lane (wave-uniform: a ballot)
             const uint32_t c0 = __builtin_amdgcn_readfirstlane(cx), c1 = __builtin_amdgcn_readfirstlane(cy),
                            c2 = __builtin_amdgcn_readfirstlane(cz);
             const bool same0 = cx == c0 && cy == c1 && cz == c2;
-            const uint64_t m0 = __builtin_amdgcn_ballot_w64(same0);
-            uni[l] = m0 == live;
-            if (SAMNERF_PROP_TWO && !uni[l]) {
-                // the first lane outside cell 0 names cell 1; two cells if
-                // every live lane is in one of them
-                const uint32_t j = (uint32_t)__builtin_ctzll(live & ~m0);
-                const bool same1 = cx == (uint32_t)__builtin_amdgcn_readlane((int)cx, (int)j) &&
-                                   cy == (uint32_t)__builtin_amdgcn_readlane((int)cy, (int)j) &&
-                                   cz == (uint32_t)__builtin_amdgcn_readlane((int)cz, (int)j);
-                two[l] = __builtin_amdgcn_ballot_w64(same0 || same1) == live;
-                in1[l] = same1;
-                lane1[l] = j;
-            }
+            uni[l] = __builtin_amdgcn_ballot_w64(same0) == live;
             const bool edge = cx == top;                   // gather_issue_c2's top-cell pair
-            g.fx[l] = edge ? 1.0f : g.fx[l];
+            fx[l] = edge ? 1.0f : fx[l];
             const uint32_t bx = d.off + (edge ? cx - 1u : cx);
             const uint32_t r2 = d.res * d.res;
             const uint32_t Y[2] = {(uint32_t)__umul24(cy, d.res), (uint32_t)__umul24(ny, d.res)};
             const uint32_t Z[2] = {(uint32_t)__umul24(cz, r2), (uint32_t)__umul24(nz, r2)};
 #pragma unroll
             for (int p = 0; p < 4; ++p) row[l][p] = (bx + Y[p & 1] + Z[p >> 1]) << 3;
-        } else {
-            const uint32_t mask = d.size - 1u;
-            const uint32_t X[2] = {cx, min(cx + 1u, top)};
-            const uint32_t Y[2] = {cy * kPrime1, ny * kPrime1};
-            const uint32_t Z[2] = {cz * kPrime2, nz * kPrime2};
+        }
+    }
+    // Dense levels first: the non-uniform ones' vector loads, then each
+    // uniform level's rows by scalar loads and its sum straight from the SGPRs
+    // (summed where the vector rows are, the compiler merged the two into one
+    // sum of phi'd VGPRs: 8 v_mov_b64 per level), then the vector sums; then
+    // the hashed levels' loads and sums.  PROP_SPLIT 0 issues the hashed loads
+    // with the dense ones (one memory round trip, 122-126 VGPRs: 4 waves per
+    // SIMD instead of 6).
+    f4a8 vd[5][4];
+    float2 vh[5][8];
+    auto issue_hashed = [&]() {
 #pragma unroll
-            for (int c = 0; c < 8; ++c)
-                row[l][c] = (d.off + ((X[c & 1] ^ Y[(c >> 1) & 1] ^ Z[c >> 2]) & mask)) << 3;
+        for (int l = 0; l < 5; ++l) {
+            if (!((KD >> l) & 1u)) {
+                const LevelDesc& d = a.grid.lv[l];
+                uint32_t cx, cy, cz;
+                locate_axis(ux, d, cx, fx[l]);
+                locate_axis(uy, d, cy, fy[l]);
+                locate_axis(uz, d, cz, fz[l]);
+                const uint32_t top = d.res - 1u;
+                const uint32_t ny = min(cy + 1u, top), nz = min(cz + 1u, top);
+                const uint32_t m8 = (d.size - 1u) << 3;
+                const uint32_t X[2] = {cx << 3, (uint32_t)min(cx + 1u, top) << 3};
+                const uint32_t Y[2] = {(cy * (kPrime1 << 3)) & m8, (ny * (kPrime1 << 3)) & m8};
+                const uint32_t Z[2] = {(cz * (kPrime2 << 3)) & m8, (nz * (kPrime2 << 3)) & m8};
+#pragma unroll
+                for (int c = 0; c < 8; ++c) row[l][c] = X[c & 1] ^ Y[(c >> 1) & 1] ^ Z[c >> 2];
+                const char* lb = base + (size_t)d.off * 8u;                // uniform: SGPR base
+#pragma unroll
+                for (int c = 0; c < 8; ++c) vh[l][c] = *reinterpret_cast<const float2*>(lb + row[l][c]);
+            }
+        }
+    };
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        if (((KD >> l) & 1u) && !uni[l]) {
+#pragma unroll
+            for (int p = 0; p < 4; ++p) vd[l][p] = *reinterpret_cast<const f4a8*>(base + row[l][p]);
+        }
+    }
+    if (!SAMNERF_PROP_SPLIT) issue_hashed();
+    // corner pair p of a dense level holds corners 2p (x) and 2p + 1 (x + 1)
+    auto dense_sum = [&](int l, const f4a8* v) {
+        f2v w[4];
+        corner_weights_pk(fx[l], fy[l], fz[l], w);
+        f2v acc = {0.0f, 0.0f};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const float w0 = corner_w(w, 2 * p), w1 = corner_w(w, 2 * p + 1);
+            acc = __builtin_elementwise_fma(f2v{w0, w0}, f2v{v[p].x, v[p].y}, acc);
+            acc = __builtin_elementwise_fma(f2v{w1, w1}, f2v{v[p].z, v[p].w}, acc);
+        }
+        return acc;
+    };
+    f2v fl[5];                 // per level (an array of 10 floats updated in branches became one
+                               // phi'd aggregate: v_mov chains at every join)
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        if (((KD >> l) & 1u) && uni[l]) {
+            // the scalar cache: wave-uniform rows, through a constant-address-
+            // space pointer (the compiler may not turn them into vector loads)
+            f4a8 sd[4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+                sd[p] = *(const __attribute__((address_space(4))) f4a8*)(
+                    base + (uint32_t)__builtin_amdgcn_readfirstlane(row[l][p]));
+            fl[l] = dense_sum(l, sd);
+        }
+    }
+#pragma unroll
+    for (int l = 0; l < 5; ++l)
+        if (((KD >> l) & 1u) && !uni[l]) fl[l] = dense_sum(l, vd[l]);
+    if (SAMNERF_PROP_SPLIT) issue_hashed();
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        if (!((KD >> l) & 1u)) {
+            f2v w[4];
+            corner_weights_pk(fx[l], fy[l], fz[l], w);
+            f2v acc = {0.0f, 0.0f};
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float wt = corner_w(w, c);
+                acc = __builtin_elementwise_fma(f2v{wt, wt}, f2v{vh[l][c].x, vh[l][c].y}, acc);
+            }
+            fl[l] = acc;
         }
     }
 #pragma unroll
     for (int l = 0; l < 5; ++l) {
-        if ((KD >> l) & 1u) {
-            if (uni[l]) {                                  // the scalar cache: wave-uniform rows
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const f4a8 v = *reinterpret_cast<const f4a8*>(base + __builtin_amdgcn_readfirstlane(row[l][p]));
-                    g.e[l][2 * p] = make_float2(v.x, v.y);
-                    g.e[l][2 * p + 1] = make_float2(v.z, v.w);
-                }
-            } else if (SAMNERF_PROP_TWO && two[l]) {       // two cells: both by scalar loads, a select per lane
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const f4a8 v0 = *reinterpret_cast<const f4a8*>(base + __builtin_amdgcn_readfirstlane(row[l][p]));
-                    const f4a8 v1 = *reinterpret_cast<const f4a8*>(
-                        base + (uint32_t)__builtin_amdgcn_readlane((int)row[l][p], (int)lane1[l]));
-                    const bool b = in1[l];
-                    g.e[l][2 * p] = make_float2(b ? v1.x : v0.x, b ? v1.y : v0.y);
-                    g.e[l][2 * p + 1] = make_float2(b ? v1.z : v0.z, b ? v1.w : v0.w);
-                }
-            } else {
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const f4a8 v = *reinterpret_cast<const f4a8*>(base + row[l][p]);
-                    g.e[l][2 * p] = make_float2(v.x, v.y);
-                    g.e[l][2 * p + 1] = make_float2(v.z, v.w);
-                }
-            }
-        } else {
-#pragma unroll
-            for (int c = 0; c < 8; ++c) g.e[l][c] = *reinterpret_cast<const float2*>(base + row[l][c]);
-        }
+        feat[2 * l] = fl[l].x;
+        feat[2 * l + 1] = fl[l].y;
     }
-    gather_finish_c2<5, true>(g, feat);
 }
 
 __device__ __forceinline__ LevelDesc select_level(const LevelDesc& p, const LevelDesc& q, bool hi) {
@@ -1266,7 +1369,14 @@ k_final(FinalArgs a) {
             if (TAP && a.rows_tap && live && r % a.tap_stride == 0u)
                 rt = a.rows_tap + ((size_t)(r / a.tap_stride) * T + k) * 128u + (8 * kb + hh) * 8;
             GatherC2<4> g;
-            gather_issue_c2<4>(emb, dl, ux, uy, uz, g, kinds(kb), rt, 16);
+            HashSlots hs;
+            if constexpr (LAY == 1) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) hs.base[q] = reinterpret_cast<const char*>(a.grid_emb) + a.hoff8[kb][q];
+                hs.hx = hh ? a.hbit : 0u;
+                hs.m8 = a.hm8;
+            }
+            gather_issue_c2<4>(emb, dl, ux, uy, uz, g, kinds(kb), rt, 16, LAY == 1 ? &hs : nullptr);
             if (first) store_position(i, ux, uy, uz);
             gather_finish_c2<4, S == 1>(g, f);
         };
@@ -1951,9 +2061,18 @@ constexpr uint32_t kBwdBoxCells = 64;
 // gradient.  The per-wave butterfly merge is a fixed order, so it stays.
 struct DetAcc {
     unsigned long long* acc;   // [rows][8] int64 (two's complement), null: the fp32 atomics
-    const uint32_t* hdr;       // hdr[0]: max |grad_fsam| (float bits), k_sgrid_det_max
+    const uint32_t* hdr;       // hdr[0]: max |grad_fsam| (float bits), k_sgrid_det_max;
+                               // hdr[1]: non-zero when grad_fsam holds a NaN or an Inf
     int log2n;                 // ceil(log2 N)
 };
+
+// A gradient with a NaN or an Inf has no fixed-point scale (frexpf(inf) is
+// unspecified and a NaN converts to INT64_MIN), and the reference's atomics
+// (gridencoder.cu:252-349) propagate it into every row the ray reaches: such
+// a call takes the fp32 atomic form (wave-uniform: one header word), whose
+// sums carry the NaN / Inf like the reference's.  Bits repeat only for finite
+// gradients, which is all the deterministic mode promises.
+__device__ __forceinline__ bool sgrid_det_nonfinite(const DetAcc& d) { return d.hdr[1] != 0u; }
 
 // 2^shift of the fixed point: max |g| < 2^e and at most N rays of weights
 // summing to <= 1 reach a row, so |total| < 2^(log2n + e) and |total| 2^shift
@@ -1996,8 +2115,9 @@ k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __rest
     // on a pending row absorbs its sum, only rows the ray has left are added to
     // memory (consecutive samples of a ray share cells at the coarse levels)
     const bool run = !DET && max_cells == 0u && d.res <= run_res;     // block-uniform
-    const double dscale = DET ? ldexp(1.0, sgrid_det_shift(det)) : 0.0;
-    unsigned long long* const dbase = DET ? det.acc + (size_t)d.off * 8u + ch : nullptr;
+    const bool fixed = DET && !sgrid_det_nonfinite(det);  // uniform: the header word
+    const double dscale = fixed ? ldexp(1.0, sgrid_det_shift(det)) : 0.0;
+    unsigned long long* const dbase = fixed ? det.acc + (size_t)d.off * 8u + ch : nullptr;
     uint32_t prow[8];
     float pval[8];
 #pragma unroll
@@ -2116,7 +2236,7 @@ k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __rest
                     }
                 }
                 if (alive) {
-                    if constexpr (DET)
+                    if (DET && fixed)
                         atomicAdd(dbase + (size_t)row * 8u,
                                   (unsigned long long)__double2ll_rn((double)val * dscale));
                     else
@@ -2131,24 +2251,32 @@ k_sgrid_backward(uint32_t N, RayTiles tiles, GridDesc<16> g, const float* __rest
             if (prow[c] != 0xFFFFFFFFu) atomicAdd(base + (size_t)prow[c] * 8u, pval[c]);
 }
 
-// max |grad_fsam[ray, 0:128]| into hdr[0] (zeroed by the host): float bits of
-// non-negative values order as unsigned integers, so the atomic max is exact
+// max |grad_fsam[ray, 0:128]| into hdr[0] and a non-finite flag into hdr[1]
+// (both zeroed by the host): float bits of non-negative values order as
+// unsigned integers, so the atomic max is exact
 __global__ void __launch_bounds__(256)
 k_sgrid_det_max(const float* __restrict__ grad, uint32_t N, uint32_t gstride, uint32_t* hdr) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     float m = 0.0f;
+    bool bad = false;
     if (t < (uint64_t)N * 32u) {                     // 4 features per thread
         const float4 v = *reinterpret_cast<const float4*>(grad + (size_t)(t >> 5) * gstride + (t & 31u) * 4u);
         m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+        bad = !(isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w));
     }
     m = wave_max64(m);
-    if ((threadIdx.x & 63u) == 0u && m > 0.0f) atomicMax(hdr, __float_as_uint(m));
+    const bool any_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
+    if ((threadIdx.x & 63u) == 0u) {
+        if (m > 0.0f && isfinite(m)) atomicMax(hdr, __float_as_uint(m));
+        if (any_bad) atomicOr(hdr + 1, 1u);
+    }
 }
 
 // the fixed-point totals into the fp32 gradient (accumulated into, as the
 // atomic form), the accumulator left zero for the next call
 __global__ void __launch_bounds__(256)
 k_sgrid_det_finish(DetAcc det, float* __restrict__ gemb, uint64_t n) {
+    if (sgrid_det_nonfinite(det)) return;            // the fp32 atomics ran: the accumulator is untouched
     const double inv = ldexp(1.0, -sgrid_det_shift(det));
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
@@ -2252,6 +2380,7 @@ namespace {
 
 struct Workspace {
     float* snf;
+    float4* rec;       // [N][2] slot-ordered ray records (k_snf, PropArgs::rec)
     float* bins1;
     float* bins2;
     float* wtmp;
@@ -2335,7 +2464,31 @@ int final_layout(const FinalArgs& fa) {
     if (v && atoi(v) == 0) return 0;
     for (int kb = 0; kb < 2; ++kb)
         if (fa.kdense[kb] != kLay1Dense[kb] || fa.khashed[kb] != kLay1Hashed[kb]) return 0;
+    if (fa.hbit == 0u) return 0;                      // hashed slots not laid out for HashSlots
     return fa.gs.inv_b2 != 0.0f ? 1 : 0;
+}
+
+// LAY 1's HashSlots layout (FinalArgs::hoff8 / hbit / hm8): every hashed slot
+// holds two consecutive levels of one power-of-two size S (the reference's
+// 2^19 hash tables) with res <= S; else hbit = 0 and LAY 1 is not used.
+void set_hash_slots(FinalArgs& fa, const GridDesc<16>& g) {
+    fa.hbit = fa.hm8 = 0u;
+    uint32_t S = 0u;
+    for (int kb = 0; kb < 2; ++kb)
+        for (int q = 0; q < 4; ++q) {
+            fa.hoff8[kb][q] = 0u;
+            if (!((fa.khashed[kb] >> q) & 1u)) continue;
+            const LevelDesc& a = g.lv[final_level(kb, 0, q)];
+            const LevelDesc& b = g.lv[final_level(kb, 1, q)];
+            if (!S) S = a.size;
+            if (a.size != S || b.size != S || (S & (S - 1u)) || b.off != a.off + S || a.res > S || b.res > S ||
+                (uint64_t)S * 8u > (1ull << 31))
+                return;
+            fa.hoff8[kb][q] = a.off * 8u;
+        }
+    if (!S) return;
+    fa.hbit = S * 8u;
+    fa.hm8 = (S - 1u) * 8u;
 }
 
 // k_sgrid_box4 packs cell indices and extents into 10 bits
@@ -2362,7 +2515,12 @@ void launch_prop_sigma(int look, uint32_t N, hipStream_t s, const PropArgs& pa) 
         kh |= (pa.grid.lv[l].flags & kHashed) ? 1u << l : 0u;
     }
     const char* pl = diag_env("SAMNERF_PROP_LAY");
-    const bool lay = (look == kLookPacked || look == kLookAuto) && pa.gs.inv_b2 != 0.0f && !(pl && atoi(pl) == 0);
+    // the LAY forms' byte-offset hash terms need res <= size on hashed levels
+    bool small_res = true;
+    for (int l = 0; l < 5; ++l)
+        if ((pa.grid.lv[l].flags & kHashed) && pa.grid.lv[l].res > pa.grid.lv[l].size) small_res = false;
+    const bool lay = (look == kLookPacked || look == kLookAuto) && pa.gs.inv_b2 != 0.0f &&
+                     !(pl && atoi(pl) == 0) && small_res && pa.rec;
     const bool lay_ok = lay && ((kd == 0x07u && kh == 0x18u) || (kd == 0x03u && kh == 0x1Cu));
     g_last_forms[T == 128 ? 0 : 1] = lay_ok ? kd | kh << 8 : 0u;
     if (lay && kd == 0x07u && kh == 0x18u) {
@@ -2589,6 +2747,7 @@ Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
     };
     const size_t n = N;
     w.snf = take(2 * n);
+    w.rec = reinterpret_cast<float4*>(take(8 * n));
     w.bins1 = take((m->num_steps[1] + 1) * n);
     w.bins2 = take((m->num_steps[2] + 1) * n);
     w.wtmp = take((size_t)std::max(m->num_steps[0], m->num_steps[1]) * n);
@@ -2693,6 +2852,7 @@ int proposal_forward(const samnerf_model* m, const TrainGeometry& g, const float
     pa.min_near = m->min_near;
     pa.gs = make_grid_scale(m->grid_bound);
     pa.snf = o.snf;
+    pa.rec = o.rec;
     pa.grid = g.prop[0];
     pa.W0 = m->prop_mlp[0][0];
     pa.W1 = m->prop_mlp[0][1];
@@ -2845,6 +3005,7 @@ int render_impl(const samnerf_model* m, const float* rays_o, const float* rays_d
     pa.min_near = m->min_near;
     pa.gs = make_grid_scale(m->grid_bound);
     pa.snf = w.snf;
+    pa.rec = w.rec;
     pa.wtmp = w.wtmp;
     // parity taps (samnerf_set_taps): the stages write their intermediates to
     // the caller's buffers instead of the workspace; the kernels are the same
@@ -2922,6 +3083,7 @@ int render_impl(const samnerf_model* m, const float* rays_o, const float* rays_d
             fa.khashed[kb] |= (ha && hb) ? 1u << q : 0u;
         }
     }
+    set_hash_slots(fa, gg);
     fa.G0 = m->grid_mlp[0];
     fa.G1 = m->grid_mlp[1];
     fa.G2 = m->grid_mlp[2];
@@ -3206,14 +3368,17 @@ size_t samnerf_sgrid_accum_size(const samnerf_model* m) {
 }
 
 int samnerf_sgrid_backward_det(const samnerf_model* m, const float* grad_fsam, uint32_t N,
-                               float* grad_embeddings, int64_t* accum, const void* workspace,
-                               size_t workspace_bytes, samnerf_stream_t stream) {
+                               float* grad_embeddings, int64_t* accum, size_t accum_bytes,
+                               const void* workspace, size_t workspace_bytes, samnerf_stream_t stream) {
     if (!m || !grad_fsam || !grad_embeddings || !workspace || !accum)
         return fail(SAMNERF_EINVAL, "sgrid_backward_det: null pointer");
     if (!m->with_sam) return fail(SAMNERF_EINVAL, "sgrid_backward_det: model has no s_grid");
     Workspace w = carve(m, N, const_cast<void*>(workspace));
     if (workspace_bytes < w.bytes)
         return fail(SAMNERF_EWORKSPACE, "sgrid_backward_det: workspace too small");
+    if (accum_bytes < samnerf_sgrid_accum_size(m))
+        return fail(SAMNERF_EWORKSPACE, "sgrid_backward_det: accumulator needs %zu bytes, got %zu",
+                    samnerf_sgrid_accum_size(m), accum_bytes);
     if (N == 0) return SAMNERF_OK;
     GridDesc<16> gs;
     int rc = make_grid_desc(m->s_grid, 8, 16, gs, "s_grid");
@@ -3226,7 +3391,7 @@ int samnerf_sgrid_backward_det(const samnerf_model* m, const float* grad_fsam, u
     det.hdr = hdr;
     det.log2n = 0;
     while ((1ull << det.log2n) < (uint64_t)N) ++det.log2n;
-    if (hipMemsetAsync(hdr, 0, sizeof(uint32_t), s) != hipSuccess)
+    if (hipMemsetAsync(hdr, 0, 2 * sizeof(uint32_t), s) != hipSuccess)
         return fail(SAMNERF_ELAUNCH, "sgrid_backward_det: header reset failed");
     k_sgrid_det_max<<<div_up((uint64_t)N * 32u, 256), 256, 0, s>>>(grad_fsam, N, kRow, hdr);
     k_sgrid_backward<32, true><<<dim3(div_up((uint64_t)N * 8, 256), 16, 1), 256, 0, s>>>(

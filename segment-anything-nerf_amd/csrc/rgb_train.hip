@@ -1091,6 +1091,7 @@ RtWorkspace carve_rt(const samnerf_model* m, uint32_t N, void* base) {
     };
     const size_t n = N;
     w.p.snf = take(2 * n);
+    w.p.rec = reinterpret_cast<float4*>(take(8 * n));
     w.p.ds0 = take(128 * n);
     w.p.w0 = take(128 * n);
     w.p.bins1 = take(65 * n);

@@ -81,6 +81,7 @@ struct TrainGeometry {
 };
 struct ProposalOut {
     float* snf;                // [2][N] spacing(near), spacing(far)
+    float4* rec;               // [N][2] slot-ordered ray records (PropArgs::rec)
     float* ds0;                // [128][N] delta * sigma of stage 0
     float* w0;                 // [128][N] its composited weights
     float* bins1;              // [65][N] resampled bins

@@ -72,7 +72,7 @@ _SIGS = {
     "samnerf_sgrid_backward": ([ctypes.POINTER(SamnerfModel), _vp, _u32, _vp, _vp, _sz, _vp],
                                _int),
     "samnerf_sgrid_accum_size": ([ctypes.POINTER(SamnerfModel)], _sz),
-    "samnerf_sgrid_backward_det": ([ctypes.POINTER(SamnerfModel), _vp, _u32, _vp, _vp, _vp, _sz, _vp],
+    "samnerf_sgrid_backward_det": ([ctypes.POINTER(SamnerfModel), _vp, _u32, _vp, _vp, _sz, _vp, _sz, _vp],
                                    _int),
     "samnerf_mask_forward": ([ctypes.POINTER(SamnerfModel), _u32, _vp, _vp, _sz, _vp], _int),
     "samnerf_tile_words": ([], _u32),

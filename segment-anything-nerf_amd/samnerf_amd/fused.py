@@ -233,11 +233,16 @@ class FusedRenderer:
         (samnerf_set_taps): ds0 [N,128], ds1 [N,64], their weights w0, w1, bins1 [N,65],
         bins2 [N,33] and their searchsorted indices inds1, inds2 (int32), the
         final stage's sigma2, w2 [N,32] and positions u2 [N,32,3] -- ray-major
-        views of the kernels' sample-major buffers -- and, for the rays
-        tap_rays = arange(0, N, stride), the corner rows rows2 (grid, k_final)
-        and srows (s_grid, k_sgrid_box4; -1 where a sample was skipped)
-        [len(tap_rays), 32, 16, 8] int32 (level-relative).  taps=<int> sets
-        that stride (default 61).
+        views of the kernels' sample-major buffers -- and the corner rows
+        rows2 (grid, k_final) and srows (s_grid, k_sgrid_box4; -1 where a
+        sample was skipped) [len(tap_rays), 32, 16, 8] int32 (level-relative)
+        of every stride-th kernel SLOT (slots 0, stride, 2 stride, ..).
+        tap_rays holds the ray ids of those slots, in the rows' order:
+        without view_width it is arange(0, N, stride); with view_width
+        (ray tiles) it is ray_of_slots(N, view_width)[arange(0, N, stride)],
+        neither sorted nor evenly spaced -- pair rows2[i] / srows[i] with
+        tap_rays[i], never with i * stride.  taps=<int> sets the stride
+        (default 61).
         own_workspace=True renders into a fresh workspace (from torch's
         caching allocator) instead of the per-stream one, so a caller can
         keep it (training: the backward reads its sample weights/positions).
@@ -401,12 +406,20 @@ class FusedRenderer:
         grad_rows = grad_rows.contiguous()
         assert grad_rows.shape[1] == ROW
         if self.deterministic:
+            # one fixed-point accumulator per (device, stream), like workspace():
+            # calls on one stream reuse it in order (each leaves it zero);
+            # concurrent calls on other streams never share one
             size = lib().samnerf_sgrid_accum_size(ctypes.byref(m))
-            if self._accum is None or self._accum.numel() < size or self._accum.device != grad_rows.device:
-                self._accum = torch.zeros(max(size, 1), dtype=torch.uint8, device=grad_rows.device)
+            dev = grad_rows.device
+            key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+            if self._accum is None:
+                self._accum = {}
+            acc = self._accum.get(key)
+            if acc is None or acc.numel() < size:
+                acc = self._accum[key] = torch.zeros(max(size, 1), dtype=torch.uint8, device=dev)
             check(lib().samnerf_sgrid_backward_det(ctypes.byref(m), _ptr(grad_rows), N,
-                                                   _ptr(grad_embeddings), _ptr(self._accum), _ptr(ws), need,
-                                                   _stream(grad_rows)), "sgrid_backward_det")
+                                                   _ptr(grad_embeddings), _ptr(acc), acc.numel(), _ptr(ws),
+                                                   need, _stream(grad_rows)), "sgrid_backward_det")
             return
         check(lib().samnerf_sgrid_backward(ctypes.byref(m), _ptr(grad_rows), N,
                                            _ptr(grad_embeddings), _ptr(ws), need,

@@ -78,7 +78,7 @@ def test_fused_mask_step_matches_cpu_twin(hip_lib, cuda, n_inst, redundant, sum_
     with oracle_encoders(), injected_bins(bins):
         pred_c, loss_c = mask_train_step(cpu, ro, rd, gt)
         loss_c.backward()
-    assert abs(float(loss) - float(loss_c)) <= 1e-5 * abs(float(loss_c)) + 1e-7, (float(loss), float(loss_c))
+    assert abs(float(loss.detach()) - float(loss_c.detach())) <= 1e-5 * abs(float(loss_c.detach())) + 1e-7, (float(loss.detach()), float(loss_c.detach()))
     errs = _grad_errors(gpu, cpu)
     print("relative gradient errors:", {k: f"{v:.1e}" for k, v in errs.items()})
     assert set(errs) == {"m_grid.embeddings", "mask_mlp.0.net.0.weight", "mask_mlp.0.net.1.weight",
@@ -174,7 +174,7 @@ def test_fused_adaptive_mask_step_matches_cpu_twin(hip_lib, cuda, adaptive_type,
     with oracle_encoders(), injected_bins(bins):
         pred_c, loss_c = mask_train_step(cpu, ro, rd, gt)
         loss_c.backward()
-    assert abs(float(loss) - float(loss_c)) <= 1e-5 * abs(float(loss_c)) + 1e-7, (float(loss), float(loss_c))
+    assert abs(float(loss.detach()) - float(loss_c.detach())) <= 1e-5 * abs(float(loss_c.detach())) + 1e-7, (float(loss.detach()), float(loss_c.detach()))
     errs = _grad_errors(gpu, cpu)
     print(adaptive_type, "relative gradient errors:", {k: f"{v:.1e}" for k, v in errs.items()})
     n_layers = 6 if adaptive_type == "density" else 8

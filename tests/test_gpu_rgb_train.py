@@ -104,7 +104,7 @@ def test_fused_rgb_step_matches_cpu_twin(hip_lib, cuda):
     for k in ("proposal_loss", "distort_loss"):
         a, b = float(out[k]), float(out_c[k])
         assert abs(a - b) <= 1e-4 * abs(b) + 1e-8, (k, a, b)
-    assert abs(float(loss) - float(loss_c)) <= 1e-4 * abs(float(loss_c)) + 1e-7
+    assert abs(float(loss.detach()) - float(loss_c.detach())) <= 1e-4 * abs(float(loss_c.detach())) + 1e-7
     _compare_grads(gpu, cpu)
 
 
@@ -165,7 +165,7 @@ def test_fused_rgb_step_vs_float64_twin(hip_lib, cuda, lam):
     print("relative gradient error vs float64 twin (hip | cpu fp32):")
     for k in errs["hip"]:
         print(f"  {k:32s} {errs['hip'][k]:.2e} | {errs['cpu_fp32'][k]:.2e}")
-    assert abs(float(loss) - loss64) <= 2e-6 * abs(loss64)
+    assert abs(float(loss.detach()) - loss64) <= 2e-6 * abs(loss64)
     bad = {k: (v, errs["cpu_fp32"][k]) for k, v in errs["hip"].items()
            if v > max(2.0 * errs["cpu_fp32"][k], 1e-5)}
     assert not bad, bad
@@ -189,7 +189,7 @@ def test_fused_rgb_step_matches_torch_path_perturbed(hip_lib, cuda):
         img_t, loss_t, out_t = rgb_train_step(b, ro, rd, gt, global_step=1)
         loss_t.backward()
     assert (img - img_t.detach()).abs().max().item() < 1e-5
-    assert abs(float(loss) - float(loss_t)) <= 1e-4 * abs(float(loss_t)) + 1e-7
+    assert abs(float(loss.detach()) - float(loss_t.detach())) <= 1e-4 * abs(float(loss_t.detach())) + 1e-7
     assert abs(float(out["proposal_loss"]) - float(out_t["proposal_loss"])) <= \
         1e-4 * abs(float(out_t["proposal_loss"])) + 1e-8
     _compare_grads(a, b)
@@ -210,7 +210,7 @@ def test_fused_rgb_step_without_proposal_update(hip_lib, cuda):
     with injected_bins(bins):
         _, loss_t, _ = rgb_train_step(b, ro, rd, gt, global_step=3001)
         loss_t.backward()
-    assert abs(float(loss) - float(loss_t)) <= 1e-4 * abs(float(loss_t)) + 1e-7
+    assert abs(float(loss.detach()) - float(loss_t.detach())) <= 1e-4 * abs(float(loss_t.detach())) + 1e-7
     assert all(p.grad is None for p in a.prop_encoders.parameters())
     assert all(p.grad is None for p in a.prop_mlp.parameters())
     _compare_grads(a, b)
@@ -232,7 +232,7 @@ def test_fused_rgb_step_entropy_and_background(hip_lib, cuda):
         _, loss_t, _ = rgb_train_step(b, ro, rd, gt, global_step=2, perturb=False)
         loss_t.backward()
     assert float(out["entropy"]) > 0
-    assert abs(float(loss) - float(loss_t)) <= 1e-4 * abs(float(loss_t)) + 1e-7
+    assert abs(float(loss.detach()) - float(loss_t.detach())) <= 1e-4 * abs(float(loss_t.detach())) + 1e-7
     _compare_grads(a, b)
 
 
@@ -250,7 +250,7 @@ def test_fused_rgb_training_reduces_loss(hip_lib, cuda):
         opt.zero_grad(set_to_none=True)
         _, loss, _ = rgb_train_step_fused(net, ro, rd, gt, global_step=step)
         opt.step()
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
     assert losses[-1] < 0.5 * losses[0], losses
 
 
@@ -275,7 +275,7 @@ def test_fused_rgb_step_ragged_batches(hip_lib, cuda, n_rays):
         img_t, loss_t, _ = rgb_train_step(b, ro, rd, gt, global_step=1, cam_near_far=cnf)
         loss_t.backward()
     assert (img - img_t.detach()).abs().max().item() < 1e-5
-    assert abs(float(loss) - float(loss_t)) <= 1e-4 * abs(float(loss_t)) + 1e-7
+    assert abs(float(loss.detach()) - float(loss_t.detach())) <= 1e-4 * abs(float(loss_t.detach())) + 1e-7
     _compare_grads(a, b)
 
 
@@ -327,7 +327,7 @@ def test_train_mode_render_runs_the_training_kernels(hip_lib, cuda):
     torch.testing.assert_close(out_c["weights"].sum(-1), out_c["weights_sum"].detach(), rtol=1e-5, atol=1e-6)
     assert img_c.requires_grad and loss_c.requires_grad
     loss_c.backward()
-    assert abs(float(loss_c) - float(loss_a)) <= 1e-6 * abs(float(loss_a))
+    assert abs(float(loss_c.detach()) - float(loss_a.detach())) <= 1e-6 * abs(float(loss_a.detach()))
     for (k, pa), (_, pc) in zip(a.named_parameters(), c.named_parameters()):
         err = float((pa.grad - pc.grad).norm() / pa.grad.norm().clamp_min(1e-30))
         assert err < 1e-5, (k, err)
@@ -368,7 +368,7 @@ def test_autograd_rgb_step_with_depth_and_weights_sum_loss(hip_lib, cuda):
         loss = (o["image"].mean() + 0.3 * o["depth"].mean() + 2.0 * o["weights_sum"].mean()
                 + o["proposal_loss"])
         loss.backward()
-        outs.append(float(loss))
+        outs.append(float(loss.detach()))
     assert abs(outs[0] - outs[1]) <= 1e-5 * abs(outs[1])
     _compare_grads(a, b)
 
@@ -395,5 +395,5 @@ def test_fused_render_weights_are_differentiable(hip_lib, cuda):
     with injected_bins(bins):
         lb = loss_of(b)
         lb.backward()
-    assert abs(float(la) - float(lb)) <= 1e-5 * abs(float(lb)) + 1e-7
+    assert abs(float(la.detach()) - float(lb.detach())) <= 1e-5 * abs(float(lb.detach())) + 1e-7
     _compare_grads(a, b)

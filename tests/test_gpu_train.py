@@ -92,7 +92,7 @@ def test_distillation_step_matches_cpu_twin_full_tables(hip_lib, cuda, det):
         pred = F.interpolate(pred, gt.shape[2:], mode="bilinear")
         lc = F.mse_loss(pred, gt, reduction="none").mean()
         lc.backward()
-    assert abs(float(lg) - float(lc)) <= 1e-4 * abs(float(lc)), (float(lg), float(lc))
+    assert abs(float(lg.detach()) - float(lc.detach())) <= 1e-4 * abs(float(lc.detach())), (float(lg.detach()), float(lc.detach()))
     errs = {}
     for (k, pg), (_, pc) in zip(nets["gpu"].named_parameters(), nets["cpu"].named_parameters()):
         if not pc.requires_grad:
@@ -173,7 +173,8 @@ def test_sgrid_backward_deterministic_mode(hip_lib, cuda):
         fr.sgrid_backward(g, ws, ge)
         dets.append(ge)
     n = net.s_grid.embeddings.numel() * 8
-    assert not fr._accum[:n].any()                          # left zero for the next call
+    (acc,) = fr._accum.values()                             # one stream: one accumulator
+    assert not acc[:n].any()                                # left zero for the next call
     fr.deterministic = False
     ref = torch.zeros_like(net.s_grid.embeddings)
     fr.sgrid_backward(g, ws, ref)
@@ -186,6 +187,62 @@ def test_sgrid_backward_deterministic_mode(hip_lib, cuda):
     # row; the fixed-point totals are exact sums rounded once: they differ
     # at the atomic form's own order noise (measured 6.9e-7 / 1.6e-6)
     assert (ref != 0).sum() > 10000 and rel < 1e-5 and mx < 1e-5, (rel, mx)
+
+
+def test_sgrid_backward_deterministic_nonfinite_and_size(hip_lib, cuda):
+    """a NaN (or Inf) in grad_fsam has no fixed-point scale; the
+    deterministic scatter then adds with the fp32 atomics, so the NaN / Inf
+    reaches the rows its ray touches (as the reference's atomics,
+    gridencoder.cu:252-349) and every other row keeps the fp32-atomic value,
+    instead of turning into large finite garbage.  A finite call after it is
+    bit-identical to one before it (the accumulator stays clean), and a C
+    caller's accumulator smaller than samnerf_sgrid_accum_size gets
+    SAMNERF_EWORKSPACE, not an out-of-bounds write."""
+    import ctypes
+    from samnerf_amd import ops
+    from samnerf_amd._lib import lib
+    from samnerf_amd.fused import FusedRenderer, ROW
+    spec = synth.ModelSpec(with_sam=True, grid_log2=14, s_grid_log2=14, prop_log2=12)
+    net = make_net(spec, synth.make_params(spec, seed=5, emb_scale=0.5, ln_jitter=0.1), cuda)
+    pose, intr = synth.gui_camera(32, 32, rot=synth.random_rotation(3))
+    ro, rd = ops.get_rays(pose, intr, 32, 32, device=cuda)
+    N = ro.shape[0]
+    fr = FusedRenderer(net, deterministic=True)
+    rows = torch.empty(N, ROW, device=cuda)
+    ws = fr.render(ro, rd, rows=rows, keep_workspace=True, feats=False, own_workspace=True)["_workspace"]
+    g = torch.randn(N, ROW, device=cuda, generator=torch.Generator(device=cuda).manual_seed(4))
+    clean = torch.zeros_like(net.s_grid.embeddings)
+    fr.sgrid_backward(g, ws, clean)
+    for bad in (float("nan"), float("inf")):
+        gb = g.clone()
+        gb[17, 3] = bad                                      # ray 17, level 0, channel 3
+        ge = torch.zeros_like(net.s_grid.embeddings)
+        fr.sgrid_backward(gb, ws, ge)
+        torch.cuda.synchronize()
+        hit = ~torch.isfinite(ge)
+        assert hit.any(), bad                                # propagated, as the reference's atomics
+        if bad != bad:
+            assert bool(torch.isnan(ge[hit]).all())
+        else:                                                # +-inf, or NaN where inf met 0 / -inf
+            assert bool(torch.isinf(ge[hit]).any())
+        # only level 0's channel 3 rows can carry it (the bad entry's column)
+        lv0 = int(net.s_grid.offsets[1])
+        assert not hit[lv0:].any() and not hit[:, [0, 1, 2, 4, 5, 6, 7]].any()
+        ok = ~hit
+        # elsewhere the fp32-atomic sums: within their order noise of the fixed point
+        assert ((ge[ok] - clean[ok]).abs().max() / clean.abs().max()).item() < 1e-5
+    again = torch.zeros_like(net.s_grid.embeddings)
+    fr.sgrid_backward(g, ws, again)
+    assert torch.equal(again, clean)                         # the accumulator was left clean
+    # C ABI: a too-small accumulator is refused before any launch
+    wsb, need, m, vw = ws
+    m.view_width = vw
+    size = lib().samnerf_sgrid_accum_size(ctypes.byref(m))
+    small = torch.zeros(size - 8, dtype=torch.uint8, device=cuda)
+    rc = lib().samnerf_sgrid_backward_det(ctypes.byref(m), ctypes.c_void_p(g.data_ptr()), N,
+                                          ctypes.c_void_p(again.data_ptr()), ctypes.c_void_p(small.data_ptr()),
+                                          small.numel(), ctypes.c_void_p(wsb.data_ptr()), need, None)
+    assert rc != 0 and b"accumulator" in lib().samnerf_last_error()
 
 
 def test_distillation_steps_repeat_bit_for_bit(hip_lib, cuda):
@@ -335,7 +392,7 @@ def test_rgb_train_step_gradients_match_cpu_twin(hip_lib, cuda):
     k_err = (gpu.grid.embeddings.grad.cpu() - k_ref).norm() / k_ref.norm()
     assert k_err < 1e-4, float(k_err)
     # (2) end to end: forward loss to fp32 rounding
-    assert abs(float(lg) - float(lc)) <= 1e-4 * abs(float(lc)) + 1e-7, (float(lg), float(lc))
+    assert abs(float(lg.detach()) - float(lc.detach())) <= 1e-4 * abs(float(lc.detach())) + 1e-7, (float(lg.detach()), float(lc.detach()))
     # (3) end to end gradients at the same samples: every tensor within 3e-4
     # relative (float atomics, reassociated sums; the proposal loss's fp32
     # sums ~1e-4)
@@ -363,7 +420,7 @@ def test_rgb_training_reduces_loss(hip_lib, cuda):
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
     assert losses[-1] < 0.5 * losses[0], losses
 
 
