@@ -66,6 +66,31 @@ def _link(objs, lib):
             raise RuntimeError(f"link failed:\n{r.stderr}")
 
 
+ASM_DIR = os.path.join(HERE, "build", "asm")
+
+
+def build_asm(jobs=None, sources=None):
+    """Device assembly (hipcc --cuda-device-only -S, the product flags) of
+    every product source into build/asm/<src>.s, rebuilt when older than its
+    inputs: the input of the inline-asm hazard lint (tools/isa_hazards.py,
+    tests/test_isa_hazards.py), which needs the ;;#ASMSTART / ;;#ASMEND
+    markers a disassembly does not carry."""
+    os.makedirs(ASM_DIR, exist_ok=True)
+    srcs = [s for s in (sources or SOURCES) if s.endswith(".hip")]
+
+    def one(src):
+        out = os.path.join(ASM_DIR, src + ".s")
+        if _newer(os.path.join(CSRC, src), out):
+            cmd = [HIPCC] + FLAGS + ["--cuda-device-only", "-S", os.path.join(CSRC, src), "-o", out]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc -S failed on {src}:\n{r.stderr}")
+        return out
+
+    with cf.ThreadPoolExecutor(jobs or min(len(srcs), os.cpu_count() or 4, 8)) as ex:
+        return list(ex.map(one, srcs))
+
+
 def build(jobs=None, verbose=True, diag=True):
     """The product library, and (diag=True) the diagnostic build beside it."""
     os.makedirs(OBJ_DIR, exist_ok=True)

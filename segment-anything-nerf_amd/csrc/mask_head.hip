@@ -352,6 +352,8 @@ struct MaskStagerDma {
 // would add a canonicalising v_max per value, and the compare-and-select form
 // takes three VALU.  The multiply comes first and reads x, so the compiler
 // has already placed x's MFMA-result wait states before the asm reads it.
+// Only for outputs that reach an MFMA through further VALU (the f16x3 split):
+// hipcc pads one wait state after an asm statement, an MFMA operand needs two.
 __device__ __forceinline__ float leaky(float x) {
     const float t = x * 0.01f;
     float r;
@@ -371,7 +373,12 @@ __device__ __forceinline__ int epilogue(floatx16 (&acc)[8], uint4 (&a0)[kHkb], u
     for (int t = 0; t < 8; ++t)
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            acc[t][q] = leaky(acc[t][q]);
+            // exact fp32: the value feeds an MFMA B operand directly, and an
+            // asm statement's output gets one wait state from hipcc where the
+            // MFMA needs two (tools/isa_hazards.py R1) -- fmaxf, which the
+            // compiler schedules and pads (and canonicalises), instead
+            if constexpr (EXACT) acc[t][q] = fmaxf(acc[t][q], acc[t][q] * 0.01f);
+            else acc[t][q] = leaky(acc[t][q]);
             if constexpr (!EXACT) m = fmaxf(m, fabsf(acc[t][q]));
         }
     int k = 0;
