@@ -589,6 +589,7 @@ class ViewRunner:
         self.cands = ([1, 2] if rule == 1 else [2, 3]) if not args.streams else [args.streams]
         self.n_active = args.streams or rule
         self.tuned = None
+        self.clock = None
         self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                            for _ in range(max(self.cands) - 1)]
         self.n_step = 0
@@ -676,21 +677,31 @@ class ViewRunner:
                     self.tuned[k] += dtk * 1e3 / (n_tune * rounds)
             self.n_active = min(self.tuned, key=self.tuned.get)
             self.n_step = 0
-        sets = [[make_event_set() for _ in range(self.chunks)] for _ in range(steps)] if stages else None
+        stamps = torch.zeros(2, 768, dtype=torch.int64, device=self.dev)
         torch.cuda.synchronize()
         if self.world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        # the shader clock of the timed views: one stamp before the first and
+        # one after the last (the current stream waits for the others first)
+        lib().samnerf_clock_stamp(ctypes.c_void_p(stamps[0].data_ptr()),
+                                  ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
         last = None
         for i in range(steps):
-            last = self.step([raw for _, raw in sets[i]] if stages else None)
+            last = self.step()                   # no stage events in the timed views (below)
         flushed = self._flush()                  # the last view's gather is inside the timed region
+        cur = torch.cuda.current_stream(self.dev)
+        for st in self.streams:
+            if st.cuda_stream != cur.cuda_stream:
+                cur.wait_stream(st)
+        lib().samnerf_clock_stamp(ctypes.c_void_p(stamps[1].data_ptr()), ctypes.c_void_p(cur.cuda_stream))
         torch.cuda.synchronize()
         if self.world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
         lib().samnerf_set_stage_events(None, 0)
+        self.clock = timed_clock(stamps.cpu().numpy())
         if flushed:
             last = flushed[-1]
         if self.world > 1:
@@ -699,26 +710,45 @@ class ViewRunner:
             dt = t.item()
         if not stages:
             return dt, last, None, None
-        stage_src = "the timed views"
-        if self.n_active > 1:
-            # Stage times for the rooflines from a single-stream pass after the
-            # timed region: with several views in flight, one view's HIP events
-            # also span the other streams' kernels.  Every rank runs it (the
-            # views' gathers are collectives).
-            n_roof = min(steps, 5)
-            sets = [[make_event_set() for _ in range(self.chunks)] for _ in range(n_roof)]
-            torch.cuda.synchronize()
-            for i in range(n_roof):
-                self._step_on_stream([raw for _, raw in sets[i]])
-            self._flush()
-            torch.cuda.synchronize()
-            lib().samnerf_set_stage_events(None, 0)
-            stage_src = f"a single-stream pass of {n_roof} views after the timed region"
+        # Stage times for the rooflines from a single-stream pass after the
+        # timed region: with several views in flight, one view's HIP events
+        # also span the other streams' kernels, and the timed views carry no
+        # per-stage event records at all (round 6).  Every rank runs it (the
+        # views' gathers are collectives).
+        n_roof = min(steps, 5)
+        sets = [[make_event_set() for _ in range(self.chunks)] for _ in range(n_roof)]
+        torch.cuda.synchronize()
+        for i in range(n_roof):
+            self._step_on_stream([raw for _, raw in sets[i]])
+        self._flush()
+        torch.cuda.synchronize()
+        lib().samnerf_set_stage_events(None, 0)
+        stage_src = f"a single-stream pass of {n_roof} views after the timed region"
         stage_avg = {}          # per step: summed over the chunks of the rank's band
         for j, st in enumerate(STAGES):
             stage_avg[st] = float(np.mean([sum(evs[j].elapsed_time(evs[j + 1]) for evs, _ in chunk_sets)
                                            for chunk_sets in sets]))
         return dt, last, stage_avg, stage_src
+
+
+def timed_clock(stamps):
+    """Shader clock of the timed views from two samnerf_clock_stamp records
+    (256 workgroups each: XCC id, s_memtime, s_memrealtime): per XCD the
+    median tick counts at each end, clock = d(memtime) / d(memrealtime) x
+    100 MHz; the mean over the XCDs seen at both ends."""
+    a, b = stamps[0].reshape(256, 3), stamps[1].reshape(256, 3)
+    per = {}
+    for x in sorted(set(a[:, 0].tolist()) & set(b[:, 0].tolist())):
+        ta, tb = a[a[:, 0] == x], b[b[:, 0] == x]
+        dt = float(np.median(tb[:, 1]) - np.median(ta[:, 1]))
+        dr = float(np.median(tb[:, 2]) - np.median(ta[:, 2]))
+        if dr > 0:
+            per[int(x)] = dt / dr * 0.1                 # GHz (s_memrealtime: 100 MHz)
+    if not per:
+        return None
+    return {"ghz": float(np.mean(list(per.values()))), "per_xcd_ghz": {str(k): round(v, 4) for k, v in per.items()},
+            "what": "shader clock over the timed views: s_memtime ticks / s_memrealtime (100 MHz) between "
+                    "two samnerf_clock_stamp launches bracketing them (median per XCD, mean over XCDs)"}
 
 
 def explain_gather(runner, views=5):
@@ -778,7 +808,7 @@ def explain_gather(runner, views=5):
 VALU_RATE = os.path.join(REPO, "profiles", "r4_valu_rate.json")
 # per-stage issue cycles per VALU instruction: the stage kernel's opcode mix x
 # the measured per-opcode rates (tools/valu_cpi.py, round 5)
-VALU_CPI = os.path.join(REPO, "profiles", "r5_valu_cpi.json")
+VALU_CPI = os.path.join(REPO, "profiles", "r6_valu_cpi.json")
 
 
 def valu_cpi_of_stages():
@@ -800,7 +830,7 @@ def valu_cycles_per_inst():
         return 2.0, "MI355X_MICROARCH.md (2 cycles per v_fma_f32, SIMD-32)"
 
 
-def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None):
+def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None, timed_clock=None):
     """`roofline` of the dominant kernel and every stage, each against the
     guide peak of its units:
       l2   -- algorithmic bytes (embedding gathers + ray I/O, ALG_BYTES_PER_RAY)
@@ -808,7 +838,7 @@ def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None):
               not for s_grid, whose box gathers read a row once per wave);
       valu -- the VALU pipe's share: issued VALU instructions (PMC SQ_INSTS_VALU
               per ray, profiles/pmc_rates.json) x the stage kernel's issue
-              cycles per instruction (profiles/r5_valu_cpi.json: its opcode
+              cycles per instruction (profiles/r6_valu_cpi.json: its opcode
               mix priced at the measured per-opcode rates, 3.5-3.75; without
               the file the v_fma_f32 rate, 2.2) / (1024 SIMDs x 2.4 GHz x
               live time);
@@ -841,7 +871,32 @@ def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None):
             c = r["valu_insts_per_ray"] * band_rays * ci
             cand["valu"] = {"unit": "VALU pipe cycles / SIMD cycles", "frac": c / cyc_avail(ms),
                             "valu_insts_per_ray": r["valu_insts_per_ray"], "cycles_per_inst": ci,
-                            "cycles_per_inst_source": ci_src}
+                            "cycles_per_inst_source": ci_src,
+                            # the other basis: every VALU
+                            # instruction at the measured v_fma_f32 rate
+                            "frac_fma_rate_basis": r["valu_insts_per_ray"] * band_rays * cpi / cyc_avail(ms),
+                            "fma_rate_cycles_per_inst": cpi, "fma_rate_source": cpi_src}
+            if "valu_cycles_per_ray" in r:
+                # the counter's VALU cycles: SQ_ACTIVE_INST_VALU
+                # x 4 (quad-cycles each wave spends on VALU instructions; the
+                # basis of AMD's derived VALUBusy = 100 SQ_ACTIVE_INST_VALU /
+                # CU_NUM / GRBM_GUI_ACTIVE, rocprofiler-sdk counter_defs.yaml),
+                # against the static opcode-mix estimate; beyond 10 % apart the
+                # line takes the counter.  (SQ_THREAD_CYCLES_VALU / 64, the
+                # other gfx950 VALU counter, is ~1.0 per instruction: it counts
+                # lane-instructions, not issue cycles -- profiles/r6c_valu_counters.txt.)
+                pc = r["valu_cycles_per_ray"] * band_rays
+                v = cand["valu"]
+                v["pmc_cycles_per_inst"] = r["valu_cycles_per_ray"] / r["valu_insts_per_ray"]
+                v["frac_pmc"] = pc / cyc_avail(ms)
+                v["static_over_pmc"] = c / pc if pc > 0 else None
+                if pc > 0 and abs(c / pc - 1.0) > 0.10:
+                    v["frac_static_opcode_mix"] = v["frac"]
+                    v["frac"] = v["frac_pmc"]
+                    v["basis"] = ("PMC: SQ_ACTIVE_INST_VALU x 4 (VALUBusy); the static opcode-mix estimate is "
+                                  "more than 10 % below it")
+                else:
+                    v["basis"] = "static opcode mix, within 10 % of PMC SQ_ACTIVE_INST_VALU x 4"
         if st == "sam_head":
             cyc = HEAD_MFMA_CYCLES_PER_32[head_mode] * band_rays / 32
             cand["mfma"] = {"unit": "TFLOP/s", "frac": cyc / cyc_avail(ms),
@@ -876,6 +931,12 @@ def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None):
             # ran at (profiles/kernel_clock.json, tools/kernel_clock.py)
             e["measured_clock_ghz"] = clk
             e["frac_at_measured_clock"] = e["frac"] * CLOCK_GHZ / clk
+        if timed_clock and bound in ("valu", "mfma"):
+            # at the clock measured live over this run's timed views
+            e["timed_clock_ghz"] = timed_clock["ghz"]
+            e["frac_at_timed_clock"] = e["frac"] * CLOCK_GHZ / timed_clock["ghz"]
+            if "frac_fma_rate_basis" in e:
+                e["frac_fma_rate_basis_at_timed_clock"] = e["frac_fma_rate_basis"] * CLOCK_GHZ / timed_clock["ghz"]
         if "ta_busy_frac_in_pmc_run" in r:
             e["ta_busy_frac_in_pmc_run"] = r["ta_busy_frac_in_pmc_run"]
         return e
@@ -946,7 +1007,8 @@ def main():
     runner = ViewRunner(args, renderer, world, dev, H, W, pose, intr, r0, r1, codec)
     dt, last, stage_avg, stage_src = runner.run(args.steps, args.warmup)
     value = n_total * args.steps / dt
-    roof, stage_roof = rooflines(stage_avg, band_rays, args.head_mode, pmc_rates(), stage_clocks())
+    roof, stage_roof = rooflines(stage_avg, band_rays, args.head_mode, pmc_rates(), stage_clocks(),
+                                 runner.clock)
 
     side = {}
     if world > 1 and args.chunks == 0 and codec == "fp32":
@@ -1126,6 +1188,14 @@ def main():
                        else f"{H}x{W} view", **({"rank_share": f"rows {r0}-{r1} of {args.rank_share} bands"}
                                                  if world == 1 and args.rank_share > 1 else {}),
                        "rays_per_step": n_total, "num_steps": [128, 64, 32],
+                       # how the timed views ran: views in
+                       # flight (HIP streams) the warm-up tuner chose, its
+                       # per-candidate ms per view, and the shader clock
+                       # measured over the timed views
+                       "views_in_flight": runner.n_active,
+                       "views_in_flight_tuned_ms": ({str(k): round(v, 4) for k, v in runner.tuned.items()}
+                                                    if runner.tuned else None),
+                       "timed_clock_ghz": round(runner.clock["ghz"], 4) if runner.clock else None,
                        "parallelism": (f"ray-sharded row bands x{world}, RCCL all-gather of each view "
                                        f"overlapped with the next view's rendering, views issued on "
                                        f"{runner.n_active} HIP streams" if args.chunks == 0 else
@@ -1136,6 +1206,7 @@ def main():
                                                     "scale, |err| <= 2^-14 of the ray max; own band fp32)"
                                                     if codec == "q16" else " (1,044 B/ray, exact)")}
                           if world > 1 and args.chunks == 0 else {})},
+            "timed_clock": runner.clock,
             "stage_ms_source": stage_src,
             "roofline": roof,
             "stage_ms": stage_avg,

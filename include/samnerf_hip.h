@@ -219,6 +219,14 @@ typedef struct {
      * 1-0.5/T, T) + (rand - 0.5) / T of stages 1 and 2, [N][T] with T = num_steps[s]+1.
      * Set per call; all NULL = perturb=False (the default), all three or none. */
     const float* perturb[3];
+    /* 1: the render workspace already holds this model's packed MLP weights
+     * (the f16x3 grid_mlp fragments and the SAM head's weight stream) from an
+     * earlier samnerf_render_forward(_tile) on the same workspace with the same
+     * weights and head_mode, so the packing launches (k_pack_grid_mlp,
+     * k_head_wmax, k_pack_h16: ~25 us per call) are skipped; 0 (default):
+     * pack.  The caller vouches for it (fused.py: the weights' data pointers
+     * and torch version counters); the diagnostic library always packs. */
+    int reuse_packed;
 } samnerf_model;
 
 /* Bytes of device workspace samnerf_render_forward needs for N rays. */
@@ -533,6 +541,14 @@ int samnerf_set_stage_events(void* const* events, uint32_t n);
  * reference grid's compile-time slot layout, 0 = run-time); out[3] reserved.
  * Writes min(n, 4) entries, returns 4.  Thread-local, no GPU work. */
 int samnerf_last_forms(uint32_t* out, uint32_t n);
+
+/* Measurement hook (bench.py): one stamp of the shader clock on `stream`,
+ * from 256 single-wave workgroups (every XCD): out[3 * b + 0] = XCC id,
+ * out[3 * b + 1] = s_memtime (shader-clock ticks), out[3 * b + 2] =
+ * s_memrealtime (100 MHz) of workgroup b; out holds 768 uint64.  Two stamps
+ * around the timed views give the clock they ran at per XCD:
+ * d(memtime) / d(memrealtime) x 100 MHz.  Costs one ~5-us launch. */
+int samnerf_clock_stamp(uint64_t* out, samnerf_stream_t stream);
 
 #ifdef __cplusplus
 }

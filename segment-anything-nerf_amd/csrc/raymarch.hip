@@ -36,7 +36,7 @@ using namespace samnerf;
 
 namespace samnerf {
 int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, float* samvit,
-                     float* packed, hipStream_t s, uint32_t ld = 256u);
+                     float* packed, hipStream_t s, uint32_t ld = 256u, bool pack = true);
 size_t sam_head_packed_floats();
 int mask_head_forward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
                       const float* geo_f, uint32_t N, float* out, RayTiles tiles, float* packed,
@@ -2288,6 +2288,22 @@ k_sgrid_det_finish(DetAcc det, float* __restrict__ gemb, uint64_t n) {
     }
 }
 
+// The shader clock over a stretch of the stream (samnerf_clock_stamp, the
+// bench's timed views): workgroup b stamps its XCC id, s_memtime (one tick
+// per shader cycle, MI355X_MICROARCH.md) and s_memrealtime (100 MHz).  The
+// read-only counter instructions only (scalar reads; the stores are vector).
+__global__ void __launch_bounds__(64) k_clock_stamp(unsigned long long* out) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    const unsigned long long rt = __builtin_amdgcn_s_memrealtime();
+    // XCC_ID: hwreg 20, bits [3:0] (gfx940+)
+    const unsigned xcc = __builtin_amdgcn_s_getreg((20u) | (0u << 6) | ((4u - 1u) << 11));
+    if (threadIdx.x == 0) {
+        out[3 * blockIdx.x + 0] = xcc;
+        out[3 * blockIdx.x + 1] = t;
+        out[3 * blockIdx.x + 2] = rt;
+    }
+}
+
 // ------------------------------------------------------- step kernels ----
 
 __global__ void __launch_bounds__(256)
@@ -2489,6 +2505,18 @@ void set_hash_slots(FinalArgs& fa, const GridDesc<16>& g) {
     if (!S) return;
     fa.hbit = S * 8u;
     fa.hm8 = (S - 1u) * 8u;
+}
+
+// The per-render packing launches (grid_mlp fragments, the SAM head's weight
+// stream) run unless the caller vouches that the workspace already holds this
+// model's packed weights (samnerf_model::reuse_packed); the diagnostic build,
+// whose kernel forms switch with the environment, always packs.
+bool pack_weights(const samnerf_model* m) {
+#ifdef SAMNERF_DIAG_VARIANTS
+    return true;
+#else
+    return m->reuse_packed == 0;
+#endif
 }
 
 // k_sgrid_box4 packs cell indices and extents into 10 bits
@@ -3164,7 +3192,7 @@ int render_impl(const samnerf_model* m, const float* rays_o, const float* rays_d
     } else {
         fa.gpack = w.gpack;
         fa.gexp = w.gexp;
-        k_pack_grid_mlp<<<1, 256, 0, s>>>(fa, w.gpack, w.gexp);
+        if (pack_weights(m)) k_pack_grid_mlp<<<1, 256, 0, s>>>(fa, w.gpack, w.gexp);
         launch_final<false>(seg, N, s, fa, m->sum_after_mlp != 0, ad);
     }
 
@@ -3192,7 +3220,7 @@ int render_impl(const samnerf_model* m, const float* rays_o, const float* rays_d
         }
         if ((rc = check_launch("render"))) return rc;
         mark_stage(4, s);
-        if (samvit) rc = sam_head_forward(m, rows, N, samvit, w.packed, s, ol.sv_ld);
+        if (samvit) rc = sam_head_forward(m, rows, N, samvit, w.packed, s, ol.sv_ld, pack_weights(m));
         mark_stage(5, s);
         if (rc == SAMNERF_OK) rc = copy_final_taps(tp, w, N, s);
         return rc;
@@ -3251,6 +3279,13 @@ int samnerf_set_stage_events(void* const* events, uint32_t n) {
 int samnerf_last_forms(uint32_t* out, uint32_t n) {
     for (uint32_t i = 0; out && i < n && i < 4; ++i) out[i] = g_last_forms[i];
     return 4;
+}
+
+int samnerf_clock_stamp(uint64_t* out, samnerf_stream_t stream) {
+    if (!out) return fail(SAMNERF_EINVAL, "clock_stamp: null pointer");
+    k_clock_stamp<<<256, 64, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        reinterpret_cast<unsigned long long*>(out));
+    return check_launch("clock_stamp");
 }
 
 int samnerf_set_taps(const samnerf_taps* taps, uint32_t N) {

@@ -1726,7 +1726,7 @@ size_t sam_head_packed_floats() {
 }
 
 int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, float* samvit,
-                     float* packed, hipStream_t s, uint32_t ld) {
+                     float* packed, hipStream_t s, uint32_t ld, bool pack) {
     const bool vec = ld % 4u == 0u && reinterpret_cast<uintptr_t>(samvit) % 16u == 0u;
 #if defined(SAMNERF_DIAG_VARIANTS) || SAMNERF_HEAD_W8
     if (m->head_mode == 0 && head_w8()) {                        // f16x3, 16-ray waves
@@ -1735,8 +1735,10 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         p.packed = reinterpret_cast<uint4*>(packed);
         p.kexp = reinterpret_cast<int*>(packed + (size_t)w8::kPackedVec * 4);
         p.part = packed + (size_t)w8::kPackedVec * 4 + 8;
-        k_head_wmax<<<dim3(kWmaxParts, 5), 256, 0, s>>>(p);
-        k_pack_w8<<<div_up((uint32_t)w8::kSteps * 8u * 64u, 256), 256, 0, s>>>(p);
+        if (pack) {                       // (the diagnostic library always packs: pack_weights)
+            k_head_wmax<<<dim3(kWmaxParts, 5), 256, 0, s>>>(p);
+            k_pack_w8<<<div_up((uint32_t)w8::kSteps * 8u * 64u, 256), 256, 0, s>>>(p);
+        }
         HeadArgsH a{};
         a.rows = rows;
         a.N = N;
@@ -1768,8 +1770,10 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         p.packed = reinterpret_cast<uint4*>(packed);
         p.kexp = reinterpret_cast<int*>(packed + (size_t)kPackedVec * 4 * kHeadCopies);
         p.part = packed + (size_t)kPackedVec * 4 * kHeadCopies + 8;
-        k_head_wmax<<<dim3(kWmaxParts, 5), 256, 0, s>>>(p);
-        k_pack_h16<<<div_up((uint32_t)kSteps * 8u * 64u, 256), 256, 0, s>>>(p);
+        if (pack) {                       // else the workspace holds them (samnerf_model::reuse_packed)
+            k_head_wmax<<<dim3(kWmaxParts, 5), 256, 0, s>>>(p);
+            k_pack_h16<<<div_up((uint32_t)kSteps * 8u * 64u, 256), 256, 0, s>>>(p);
+        }
         HeadArgsH a;
         a.rows = rows;
         a.N = N;
@@ -1822,8 +1826,9 @@ int sam_head_forward(const samnerf_model* m, const float* rows, uint32_t N, floa
         return check_launch("sam_head_h16");
     }
     const uint32_t nvec = 8u * kTotalGroups * 64u;
-    k_pack<<<div_up(nvec, 256), 256, 0, s>>>(m->sam_w[0], m->sam_w[1], m->sam_w[2], m->sam_w[3],
-                                             m->sam_w[4], packed);
+    if (pack)
+        k_pack<<<div_up(nvec, 256), 256, 0, s>>>(m->sam_w[0], m->sam_w[1], m->sam_w[2], m->sam_w[3],
+                                                 m->sam_w[4], packed);
     HeadArgs a;
     a.rows = rows;
     a.N = N;
@@ -1861,7 +1866,7 @@ int samnerf_sam_head_forward(const samnerf_model* m, const float* rows, uint32_t
         return fail(SAMNERF_EWORKSPACE, "sam_head_forward: workspace needs %zu bytes, got %zu", need,
                     workspace_bytes);
     return sam_head_forward(m, rows, N, samvit, static_cast<float*>(workspace),
-                            reinterpret_cast<hipStream_t>(stream), 256u);
+                            reinterpret_cast<hipStream_t>(stream), 256u, true);
 }
 
 }  // extern "C"

@@ -39,7 +39,7 @@ class SamnerfModel(ctypes.Structure):
                 ("t_thresh", _f32), ("view_width", _u32),
                 ("with_mask", _int), ("mask_kind", _int), ("m_grid", SamnerfGrid), ("mask_w", _vp * 8),
                 ("mask_out", _u32),
-                ("sum_after_mlp", _int), ("perturb", _vp * 3)]
+                ("sum_after_mlp", _int), ("perturb", _vp * 3), ("reuse_packed", _int)]
 
 
 _SIGS = {
@@ -81,6 +81,7 @@ _SIGS = {
     "samnerf_set_stage_events": ([ctypes.POINTER(_vp), _u32], _int),
     "samnerf_set_taps": ([ctypes.c_void_p, _u32], _int),
     "samnerf_last_forms": ([ctypes.c_void_p, _u32], _int),
+    "samnerf_clock_stamp": ([_vp, _vp], _int),
     "samnerf_adam_step": ([ctypes.c_void_p, _u32, _f64, _f64, _f64, _f64, _f64, _u32, _vp], _int),
     "samnerf_rgb_train_workspace_size": ([ctypes.POINTER(SamnerfModel), _u32], _sz),
     "samnerf_rgb_train_step": ([ctypes.POINTER(SamnerfModel), _vp, _vp, _u32, _vp, _u32, _vp,

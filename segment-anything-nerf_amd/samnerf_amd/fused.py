@@ -102,6 +102,8 @@ class FusedRenderer:
         self.deterministic = bool(deterministic)
         self._accum = None
         self._ws = None
+        self._packed = {}      # (device, stream) -> what its workspace's packed weights are
+        self.last_reuse_packed = 0
         self._keep = []
         self._model = None
         self._model_key_cached = None
@@ -202,12 +204,30 @@ class FusedRenderer:
         m.sum_after_mlp = int(bool(getattr(opt, "sum_after_mlp", False)))
         return m
 
+    def invalidate_packed(self):
+        """Forget the packed weights of every workspace: call after changing
+        grid_mlp or SAM-head weights in a way torch's version counter does not
+        see (writes through `.data`, or through raw pointers from C)."""
+        self._packed = {}
+
+    def _pack_signature(self, m):
+        """What the packed weights of a render depend on: head_mode and the
+        packed tensors (grid_mlp, the SAM head's weights) as (data pointer,
+        torch version counter) -- an in-place update (optimizer step, copy_,
+        load_state_dict, FusedAdam) bumps the counter, a new tensor changes
+        the pointer; `.data` writes do not (invalidate_packed)."""
+        n = self.net
+        ts = [n.grid_mlp.net[i].weight for i in range(3)]
+        if m.with_sam:
+            ts += [n.samvit_mlp[0].net[i].weight for i in range(5)]
+        return (int(m.head_mode), tuple((t.data_ptr(), t._version) for t in ts))
+
     def workspace(self, m, N, device):
         """Scratch of one render call, one buffer per (device, stream): calls
         on one stream reuse it in stream order; renders issued on different
         streams (concurrent views) never share one."""
         need = lib().samnerf_render_workspace_size(ctypes.byref(m), N)
-        key = (device, torch.cuda.current_stream(device).cuda_stream)
+        key = (device, _stream_key(device))
         if self._ws is None:
             self._ws = {}
         ws = self._ws.get(key)
@@ -286,11 +306,21 @@ class FusedRenderer:
         else:
             for i in range(3):
                 m.perturb[i] = None
+        pack_key = None
         if own_workspace:
             need = lib().samnerf_render_workspace_size(ctypes.byref(m), N)
             ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+            m.reuse_packed = 0
         else:
             ws, need = self.workspace(m, N, dev)
+            # the packed MLP weights this per-stream workspace holds from its
+            # last render are reused when the weights are the same tensors at
+            # the same version (samnerf_model.reuse_packed: ~25 us per view);
+            # the SAM head's are packed only by renders that run the head
+            head = bool(m.with_sam and feats)
+            pack_key = (ws.data_ptr(), self._pack_signature(m))
+            have = self._packed.get((dev, _stream_key(dev)))
+            m.reuse_packed = int(have is not None and have[0] == pack_key and (have[1] or not head))
         if bg_color is None:
             bg = 1.0
         elif torch.is_tensor(bg_color):
@@ -351,6 +381,12 @@ class FusedRenderer:
                     ctypes.byref(m), _ptr(rays_o), _ptr(rays_d), N, _ptr(cnf), n_cnf, bg, _ptr(image),
                     _ptr(depth), _ptr(wsum), _ptr(samvit), _ptr(rows), _ptr(ws), need, _stream(rays_o)),
                     "render_forward")
+            self.last_reuse_packed = int(m.reuse_packed)
+            if pack_key is not None:
+                key = (dev, _stream_key(dev))
+                if m.reuse_packed:                 # nothing packed: the head's stays as it was
+                    head = head or self._packed[key][1]
+                self._packed[key] = (pack_key, head)
             if mask and mask_logits:
                 logits = torch.empty(N, int(m.mask_out), device=dev)
                 check(lib().samnerf_mask_forward(ctypes.byref(m), N, _ptr(logits), _ptr(ws), need,
@@ -360,6 +396,7 @@ class FusedRenderer:
                 lib().samnerf_set_taps(None, 0)
             for i in range(3):
                 m.perturb[i] = None
+            m.reuse_packed = 0
         out = {"image": image, "depth": depth, "weights_sum": wsum}
         if mask and mask_logits:
             out["instance_mask_logits"] = logits
@@ -424,6 +461,10 @@ class FusedRenderer:
         check(lib().samnerf_sgrid_backward(ctypes.byref(m), _ptr(grad_rows), N,
                                            _ptr(grad_embeddings), _ptr(ws), need,
                                            _stream(grad_rows)), "sgrid_backward")
+
+
+def _stream_key(device):
+    return torch.cuda.current_stream(device).cuda_stream
 
 
 class _FusedSamRows(torch.autograd.Function):

@@ -10,6 +10,7 @@ constructor arguments, parameter groups, state keys ('step', 'exp_avg',
 import ctypes
 
 import torch
+from torch.autograd.graph import increment_version
 
 from ._lib import SamnerfAdamTensor, check, lib
 
@@ -56,4 +57,9 @@ class FusedAdam(torch.optim.Optimizer):
                 check(lib().samnerf_adam_step(ctypes.byref(tab), len(ps), float(group["lr"]), float(b1),
                                               float(b2), float(group["eps"]),
                                               float(group["weight_decay"]), t, stream), "adam_step")
+                # the kernel writes through raw pointers: bump each parameter's
+                # version counter as torch's in-place update would (autograd's
+                # saved-tensor checks, FusedRenderer's packed-weight reuse)
+                for p in ps:
+                    increment_version(p)
         return loss

@@ -673,3 +673,50 @@ def test_product_runs_the_specialised_forms(hip_lib, cuda):
     for n in (81920, 40000):
         fr.render(ro[:n], rd[:n])
         assert last_forms() == [0x1807, 0x1C03, 1, 0], n
+
+
+def test_packed_weight_reuse(hip_lib, cuda):
+    """samnerf_model.reuse_packed (round 6): a render on the same per-stream
+    workspace with unchanged grid_mlp / SAM-head weights skips the packing
+    launches and gives the same bits; an in-place weight update (torch op,
+    FusedAdam), a render without features before one with them, and
+    head_mode all force a repack -- each render equal, bit for bit, to a fresh
+    renderer's."""
+    from samnerf_amd import ops
+    from samnerf_amd._lib import lib
+    from samnerf_amd.fused import FusedRenderer
+    from samnerf_amd.optim import FusedAdam
+    if lib().samnerf_diag_variants():
+        pytest.skip("the diagnostic library always packs")
+    spec = synth.ModelSpec(with_sam=True, grid_log2=14, s_grid_log2=14, prop_log2=12)
+    net = make_net(spec, synth.make_params(spec, seed=41, emb_scale=0.5, ln_jitter=0.1), cuda)
+    pose, intr = synth.gui_camera(64, 64, rot=synth.random_rotation(5))
+    ro, rd = ops.get_rays(pose, intr, 64, 64, device=cuda)
+    keys = ("image", "depth", "weights_sum", "samvit")
+
+    def same(a, b):
+        return all(torch.equal(a[k], b[k]) for k in keys if k in a or k in b)
+
+    fr = FusedRenderer(net)
+    a = fr.render(ro, rd)
+    assert fr.last_reuse_packed == 0
+    b = fr.render(ro, rd)
+    assert fr.last_reuse_packed == 1 and same(a, b)
+    with torch.no_grad():                                   # in place: version counter bumps
+        net.grid_mlp.net[1].weight.mul_(1.5)
+    c = fr.render(ro, rd)
+    assert fr.last_reuse_packed == 0 and same(c, FusedRenderer(net).render(ro, rd)) and not same(a, c)
+    w = net.samvit_mlp[0].net[2].weight
+    w.grad = torch.randn_like(w)
+    FusedAdam([w], lr=1e-2).step()                          # raw-pointer update, version bumped
+    d = fr.render(ro, rd)
+    assert fr.last_reuse_packed == 0 and same(d, FusedRenderer(net).render(ro, rd)) and not same(c, d)
+    fr2 = FusedRenderer(net)
+    fr2.render(ro, rd, feats=False)                         # the head's weights not packed
+    e = fr2.render(ro, rd)
+    assert fr2.last_reuse_packed == 0 and same(e, d)
+    f = fr2.render(ro, rd)
+    assert fr2.last_reuse_packed == 1 and same(f, d)
+    fr2._head_mode = 1                                      # (the model struct is rebuilt)
+    g = fr2.render(ro, rd)
+    assert fr2.last_reuse_packed == 0 and same(g, FusedRenderer(net, head_mode=1).render(ro, rd))

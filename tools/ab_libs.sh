@@ -14,6 +14,6 @@ for r in $(seq 1 $ROUNDS); do
     timeout -k 10 120 python bench.py --steps 30 --no-alt --cpu-rays 0 --ref-gpu-rays 0 ${AB_ARGS:-} > "$OUT/${tag}_$r.log" 2>&1
     rc=$?
     if [ $rc -ne 0 ]; then echo "$tag round $r rc=$rc"; tail -3 "$OUT/${tag}_$r.log"; exit $rc; fi
-    tail -1 "$OUT/${tag}_$r.log" | python -c "import json,sys; r=json.loads(sys.stdin.read()); print('$tag', $r, round(r['ms_per_step'],4), {k: round(v,4) for k,v in r['stage_ms'].items()})"
+    tail -1 "$OUT/${tag}_$r.log" | python -c "import json,sys; r=json.loads(sys.stdin.read()); print('$tag', $r, round(r['ms_per_step'],4), {k: round(v,4) for k,v in r['stage_ms'].items()}, 'clock', r['config'].get('timed_clock_ghz'), 'views_in_flight', r['config'].get('views_in_flight'))"
   done
 done

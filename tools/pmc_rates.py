@@ -71,6 +71,16 @@ def main(root):
             e["wave_cycle_shares"] = {"wait_any": c["SQ_WAIT_ANY"] / wc,
                                       "wait_inst_any": c.get("SQ_WAIT_INST_ANY", 0.0) / wc,
                                       "active_inst_any": c.get("SQ_ACTIVE_INST_ANY", 0.0) / wc}
+        if "SQ_THREAD_CYCLES_VALU" in c:
+            # VALU pipe occupancy from the counter (round 6, VERDICT r5 item
+            # 2): thread-cycles of VALU execution per SIMD / 64 lanes = the
+            # SIMD cycles its VALU spent (full waves), next to the static
+            # opcode-mix estimate (valu_insts_per_ray x cycles per instruction)
+            e["valu_pipe_cycles_per_ray"] = c["SQ_THREAD_CYCLES_VALU"] / 64.0 / RAYS
+        if "SQ_ACTIVE_INST_VALU2" in c:
+            e["valu_dual_issue_quad_cycles_per_ray"] = c["SQ_ACTIVE_INST_VALU2"] / RAYS
+        if "SQ_VALU_MFMA_COEXEC_CYCLES" in c:
+            e["mfma_coexec_cycles_per_ray"] = c["SQ_VALU_MFMA_COEXEC_CYCLES"] / RAYS
         if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
             e["mfma_busy_cycles_per_ray"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / RAYS
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:

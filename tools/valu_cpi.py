@@ -11,7 +11,7 @@ The mix is the static one of the kernel's hot region: the loop holding the
 most VALU instructions (k_final's sample loop), or the whole body (the
 loop-free proposal kernels; k_sgrid_box4 and the SAM head, whose rotated loops
 hold nearly all of it).  Writes
-profiles/r5_valu_cpi.json.  usage (CPU, from the repo root):
+profiles/r6_valu_cpi.json.  usage (CPU, from the repo root):
   python tools/valu_cpi.py
 """
 import json
@@ -123,7 +123,7 @@ def main():
         res["stages"][st] = {"kernel": name, "region": kind, "valu_insts": len(v), "valu_cycles": round(cyc, 1),
                              "cycles_per_inst": round(cyc / max(1, len(v)), 3)}
         print(st, res["stages"][st]["region"], len(v), round(cyc / max(1, len(v)), 3), file=sys.stderr)
-    json.dump(res, open(os.path.join(ROOT, "profiles", "r5_valu_cpi.json"), "w"), indent=1)
+    json.dump(res, open(os.path.join(ROOT, "profiles", "r6_valu_cpi.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":
