@@ -36,7 +36,8 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 // Power-of-two scale s and its inverse for a column (or row) whose largest
 // magnitude is `maxabs` (>= 0): maxabs * s in [2^13, 2^14) -- one binade below
 // fp16's top, so values up to 4x the maximum a scale was chosen for still fit
-// (k_final's layer 1 takes its two k-blocks one at a time).  The exponent is
+// (the headroom k_final's one-block-at-a-time layer 1, SAMNERF_FINAL_JOINT = 0,
+// relies on; the default joint form takes one scale over both k-blocks).  The exponent is
 // clamped so that both s and 1/s are normal floats (all-zero or tiny columns
 // get s = 2^125; inf / NaN columns s = 2^-115 and stay inf / NaN).
 struct Scale2 {
@@ -89,6 +90,7 @@ __device__ __forceinline__ float exp2i(int k) {
 // The same split in plain C (v_pk_mul_f32, v_cvt_pk_f16_f32, conversions back,
 // a subtraction, v_cvt_pk_f16_f32 again): full-dword writes the compiler
 // schedules and pads itself; the same bits (x s and x s - hi are exact).
+template <bool LEAD = false>   // compiler code: hipcc pads its hazards
 __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
     uint32_t h[4], l[4];
 #pragma unroll
@@ -114,6 +116,7 @@ __device__ __forceinline__ void split_pair_f16_old(float x, float y, float s, ui
     hi = h;
     lo = l;
 }
+template <bool LEAD = false>   // timing variants: no leading pad
 __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
     split_pair_f16_old(v[0], v[1], s, hi.x, lo.x);
     split_pair_f16_old(v[2], v[3], s, hi.y, lo.y);
@@ -131,53 +134,65 @@ __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, u
 // half is rounded to fp16 once (RNE), as the mix does.  Every write is a
 // whole dword (no dst-sel hazard), each result is read at least 4
 // instructions after it is written, and the closing s_nop 1 covers the VALU
-// -> MFMA operand rule for the last lo dword.
+// -> MFMA operand rule for the last lo dword.  hipcc does not pad an MFMA
+// whose result registers the statement's outputs reuse (it cannot see into
+// the string): LEAD = true opens it with s_nop 7, the 8 wait states a 4-pass
+// XDL result needs before a VALU writes the same registers -- the call sites
+// whose schedule puts the statement right behind MFMAs (k_sam_head_w8, found
+// by tests/test_isa_hazards.py) take it.
+#define SAMNERF_SPLIT8_ASM \
+    "v_mul_f32 %[a0], %[v0], %[s]\n\t" \
+    "v_mul_f32 %[a1], %[v1], %[s]\n\t" \
+    "v_mul_f32 %[a2], %[v2], %[s]\n\t" \
+    "v_mul_f32 %[a3], %[v3], %[s]\n\t" \
+    "v_mul_f32 %[a4], %[v4], %[s]\n\t" \
+    "v_mul_f32 %[a5], %[v5], %[s]\n\t" \
+    "v_mul_f32 %[a6], %[v6], %[s]\n\t" \
+    "v_mul_f32 %[a7], %[v7], %[s]\n\t" \
+    "v_cvt_pk_f16_f32 %[h0], %[a0], %[a1]\n\t" \
+    "v_cvt_pk_f16_f32 %[h1], %[a2], %[a3]\n\t" \
+    "v_cvt_pk_f16_f32 %[h2], %[a4], %[a5]\n\t" \
+    "v_cvt_pk_f16_f32 %[h3], %[a6], %[a7]\n\t" \
+    "v_cvt_f32_f16 %[t0], %[h0]\n\t" \
+    "v_cvt_f32_f16 %[t2], %[h1]\n\t" \
+    "v_cvt_f32_f16 %[t4], %[h2]\n\t" \
+    "v_cvt_f32_f16 %[t6], %[h3]\n\t" \
+    "v_cvt_f32_f16_sdwa %[t1], %[h0] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1\n\t" \
+    "v_cvt_f32_f16_sdwa %[t3], %[h1] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1\n\t" \
+    "v_cvt_f32_f16_sdwa %[t5], %[h2] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1\n\t" \
+    "v_cvt_f32_f16_sdwa %[t7], %[h3] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1\n\t" \
+    "v_sub_f32 %[t0], %[a0], %[t0]\n\t" \
+    "v_sub_f32 %[t2], %[a2], %[t2]\n\t" \
+    "v_sub_f32 %[t4], %[a4], %[t4]\n\t" \
+    "v_sub_f32 %[t6], %[a6], %[t6]\n\t" \
+    "v_sub_f32 %[t1], %[a1], %[t1]\n\t" \
+    "v_sub_f32 %[t3], %[a3], %[t3]\n\t" \
+    "v_sub_f32 %[t5], %[a5], %[t5]\n\t" \
+    "v_sub_f32 %[t7], %[a7], %[t7]\n\t" \
+    "v_cvt_pk_f16_f32 %[l0], %[t0], %[t1]\n\t" \
+    "v_cvt_pk_f16_f32 %[l1], %[t2], %[t3]\n\t" \
+    "v_cvt_pk_f16_f32 %[l2], %[t4], %[t5]\n\t" \
+    "v_cvt_pk_f16_f32 %[l3], %[t6], %[t7]\n\t" \
+    "s_nop 1"
+#define SAMNERF_SPLIT8_OUT \
+    [h0] "=&v"(h0), [h1] "=&v"(h1), [h2] "=&v"(h2), [h3] "=&v"(h3), [l0] "=&v"(l0), [l1] "=&v"(l1), \
+    [l2] "=&v"(l2), [l3] "=&v"(l3), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), \
+    [a4] "=&v"(a4), [a5] "=&v"(a5), [a6] "=&v"(a6), [a7] "=&v"(a7), [t0] "=&v"(t0), [t1] "=&v"(t1), \
+    [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7)
+#define SAMNERF_SPLIT8_IN \
+    [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [v4] "v"(v[4]), [v5] "v"(v[5]), \
+    [v6] "v"(v[6]), [v7] "v"(v[7]), [s] "v"(s)
+template <bool LEAD = false>
 __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
     uint32_t h0, h1, h2, h3, l0, l1, l2, l3;
     float a0, a1, a2, a3, a4, a5, a6, a7, t0, t1, t2, t3, t4, t5, t6, t7;
-    asm("v_mul_f32 %[a0], %[v0], %[s]\n\t"
-        "v_mul_f32 %[a1], %[v1], %[s]\n\t"
-        "v_mul_f32 %[a2], %[v2], %[s]\n\t"
-        "v_mul_f32 %[a3], %[v3], %[s]\n\t"
-        "v_mul_f32 %[a4], %[v4], %[s]\n\t"
-        "v_mul_f32 %[a5], %[v5], %[s]\n\t"
-        "v_mul_f32 %[a6], %[v6], %[s]\n\t"
-        "v_mul_f32 %[a7], %[v7], %[s]\n\t"
-        "v_cvt_pk_f16_f32 %[h0], %[a0], %[a1]\n\t"
-        "v_cvt_pk_f16_f32 %[h1], %[a2], %[a3]\n\t"
-        "v_cvt_pk_f16_f32 %[h2], %[a4], %[a5]\n\t"
-        "v_cvt_pk_f16_f32 %[h3], %[a6], %[a7]\n\t"
-        "v_cvt_f32_f16 %[t0], %[h0]\n\t"
-        "v_cvt_f32_f16 %[t2], %[h1]\n\t"
-        "v_cvt_f32_f16 %[t4], %[h2]\n\t"
-        "v_cvt_f32_f16 %[t6], %[h3]\n\t"
-        "v_cvt_f32_f16_sdwa %[t1], %[h0] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1\n\t"
-        "v_cvt_f32_f16_sdwa %[t3], %[h1] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1\n\t"
-        "v_cvt_f32_f16_sdwa %[t5], %[h2] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1\n\t"
-        "v_cvt_f32_f16_sdwa %[t7], %[h3] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1\n\t"
-        "v_sub_f32 %[t0], %[a0], %[t0]\n\t"
-        "v_sub_f32 %[t2], %[a2], %[t2]\n\t"
-        "v_sub_f32 %[t4], %[a4], %[t4]\n\t"
-        "v_sub_f32 %[t6], %[a6], %[t6]\n\t"
-        "v_sub_f32 %[t1], %[a1], %[t1]\n\t"
-        "v_sub_f32 %[t3], %[a3], %[t3]\n\t"
-        "v_sub_f32 %[t5], %[a5], %[t5]\n\t"
-        "v_sub_f32 %[t7], %[a7], %[t7]\n\t"
-        "v_cvt_pk_f16_f32 %[l0], %[t0], %[t1]\n\t"
-        "v_cvt_pk_f16_f32 %[l1], %[t2], %[t3]\n\t"
-        "v_cvt_pk_f16_f32 %[l2], %[t4], %[t5]\n\t"
-        "v_cvt_pk_f16_f32 %[l3], %[t6], %[t7]\n\t"
-        "s_nop 1"
-        : [h0] "=&v"(h0), [h1] "=&v"(h1), [h2] "=&v"(h2), [h3] "=&v"(h3), [l0] "=&v"(l0), [l1] "=&v"(l1),
-          [l2] "=&v"(l2), [l3] "=&v"(l3), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3),
-          [a4] "=&v"(a4), [a5] "=&v"(a5), [a6] "=&v"(a6), [a7] "=&v"(a7), [t0] "=&v"(t0), [t1] "=&v"(t1),
-          [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7)
-        : [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [v4] "v"(v[4]), [v5] "v"(v[5]),
-          [v6] "v"(v[6]), [v7] "v"(v[7]), [s] "v"(s));
+    if constexpr (LEAD) asm("s_nop 7\n\t" SAMNERF_SPLIT8_ASM : SAMNERF_SPLIT8_OUT : SAMNERF_SPLIT8_IN);
+    else asm(SAMNERF_SPLIT8_ASM : SAMNERF_SPLIT8_OUT : SAMNERF_SPLIT8_IN);
     hi = make_uint4(h0, h1, h2, h3);
     lo = make_uint4(l0, l1, l2, l3);
 }
 #else   // SAMNERF_SPLIT_MIX: rounds 1-5's v_fma_mix form (timing A/B)
+template <bool LEAD = false>   // timing variants: no leading pad
 __device__ __forceinline__ void split8_f16(const float* v, float s, uint4& hi, uint4& lo) {
     uint32_t h0, h1, h2, h3, l0, l1, l2, l3;
     asm("v_fma_mixlo_f16 %0, %8, %16, 0\n\t"

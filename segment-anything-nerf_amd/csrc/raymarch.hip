@@ -1354,12 +1354,17 @@ k_final(FinalArgs a) {
         // two that puts the sample column's max |input| in [2^13, 2^14);
         // e_h1 / e_h2 / e_o3 = log2 of the factor a layer's accumulators carry
         // over the true values (input scales + weight-tensor scales).  Layer 1
-        // takes its two k-blocks one at a time (holding the first block's
-        // features through the second gather costs ~50 VGPRs): the running
-        // scale is the first block's, lowered -- and the accumulators rescaled
-        // by the same exact power of two -- when the second block's max needs
-        // a scale two or more binades lower (up to one binade it still fits
-        // fp16 at the first block's scale, f16x3.h).
+        // (the default, SAMNERF_FINAL_JOINT = 1, round 5) gathers both k-blocks
+        // first and takes ONE scale from the column's max over all 32 inputs
+        // (16 levels x 2 channels): the dense and hashed levels share it, so a
+        // level far below the column max keeps fewer significant bits in its
+        // fp16 halves -- down to 2^-27 of the max it stays normal fp16, and the
+        // f16x3 products stay within the error bound of an exact fp32 GEMM
+        // (tests/test_gpu_render.py::test_final_joint_scale_over_wide_level_ranges
+        // against the exact-fp32 form on levels 2^-20 .. 1 apart).  The
+        // one-block-at-a-time form (SAMNERF_FINAL_JOINT = 0: the second block
+        // rescales the accumulators by an exact power of two when its max needs
+        // a scale two or more binades lower) remains as a build switch.
         int k1 = 0, e_h1 = 0, e_h2 = 0;
         // this half-wave's 8 features of k-block kb (levels 8 kb + hh + 2 q)
         auto gather_kb = [&](int kb, float* f, bool first) {
@@ -2774,6 +2779,12 @@ Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
         return q;
     };
     const size_t n = N;
+    // the packed weights first: their offsets do not depend on N, so a
+    // render of another ray count on the same workspace finds them where
+    // the packing render left them (samnerf_model::reuse_packed)
+    w.gpack = reinterpret_cast<uint4*>(take((size_t)2 * kFSlots * 64 * 4));
+    w.gexp = reinterpret_cast<int*>(take(4));
+    w.packed = take(m->with_sam ? sam_head_packed_floats() : 0);
     w.snf = take(2 * n);
     w.rec = reinterpret_cast<float4*>(take(8 * n));
     w.bins1 = take((m->num_steps[1] + 1) * n);
@@ -2782,9 +2793,6 @@ Workspace carve(const samnerf_model* m, uint32_t N, void* base) {
     w.u_f = take(3 * (size_t)m->num_steps[2] * n);
     w.w_f = take((size_t)m->num_steps[2] * n);
     w.rows = take((size_t)kRow * n);
-    w.packed = take(m->with_sam ? sam_head_packed_floats() : 0);
-    w.gpack = reinterpret_cast<uint4*>(take((size_t)2 * kFSlots * 64 * 4));
-    w.gexp = reinterpret_cast<int*>(take(4));
     const bool mdef = m->with_mask && m->mask_kind == 0, madapt = m->with_mask && m->mask_kind > 0;
     w.geo_f = take(mdef ? (size_t)16 * m->num_steps[2] * n : 0);
     w.mpacked = take(mdef ? mask_head_packed_floats() : 0);

@@ -999,7 +999,7 @@ k_sam_head_h16q(HeadArgsH a, uint32_t ntiles) {
 }
 
 #ifndef SAMNERF_HEAD_W8
-#define SAMNERF_HEAD_W8 0
+#define SAMNERF_HEAD_W8 1                     // 0: k_sam_head_h16q, 2: two 4-wave workgroups per CU
 #endif
 #if defined(SAMNERF_DIAG_VARIANTS) || SAMNERF_HEAD_W8
 // ============================================ f16x3, 16-ray waves, 2 per SIMD
@@ -1042,12 +1042,15 @@ k_sam_head_h16q(HeadArgsH a, uint32_t ntiles) {
 // Measured (round 5, profiles/r5l_head_forms.txt): the head alone, back to
 // back, 0.608 ms against 0.697 for k_sam_head_h16q (-13 %; the two
 // 4-wave-workgroups form 0.676); inside the view 0.54 against 0.565 ms, but
-// the view is not faster (2.856-2.890 against 2.851-2.866 ms): the stages
-// after the head run 2-4 % slower -- the chip is at its power limit through
-// the view (2.1-2.2 GHz), so a head that finishes sooner at the same MFMA and
-// more LDS work moves the clock, not the view.  The per-step barrier also
-// keeps the 8 waves in lockstep, so their layer boundaries coincide.  Kept for
-// the diagnostic build (forms 30 / 31) and SAMNERF_HEAD_W8 timing builds.
+// the view was not faster then (2.856-2.890 against 2.851-2.866 ms): the
+// chip is at its power limit through the view (2.1-2.2 GHz).  Round 6, after
+// the proposal / k_final VALU cuts, three interleaved rounds of the view with
+// the live shader clock (profiles/r6d_head_w8_ab.txt): 8-wave workgroups
+// 2.773-2.836 ms (head 0.504-0.509) against 2.800-2.894 (0.551-0.569) for
+// k_sam_head_h16q at the same clocks, every round; the two 4-wave-workgroups
+// form loses (2.878-2.899).  So the 8-wave form is the product
+// (SAMNERF_HEAD_W8 = 1); h16q stays the default of SAMNERF_HEAD_W8 = 0 builds
+// and the diagnostic forms (SAMNERF_HEAD_V other than 30 / 31).
 namespace w8 {
 constexpr int kXkb = 6;                               // 163 inputs -> 6 k-blocks of 32
 constexpr int kHkb = 8;                               // 256 -> 8
@@ -1217,7 +1220,7 @@ __device__ __forceinline__ void split_w8(const floatx4 (&acc)[16], float s, uint
     for (int b = 0; b < w8::kHkb; ++b) {
         const float v[8] = {acc[2 * b][0], acc[2 * b][1], acc[2 * b][2], acc[2 * b][3],
                             acc[2 * b + 1][0], acc[2 * b + 1][1], acc[2 * b + 1][2], acc[2 * b + 1][3]};
-        split8_f16(v, s, ah[b], al[b]);
+        split8_f16<true>(v, s, ah[b], al[b]);
     }
 }
 
@@ -1323,7 +1326,7 @@ k_sam_head_w8(HeadArgsH a, uint32_t ntiles) {
             for (int kb = 0; kb < w8::kXkb; ++kb) {
                 float v[8];
                 x8(kb, v);
-                split8_f16(v, sc_s, xh[kb], xl[kb]);
+                split8_f16<true>(v, sc_s, xh[kb], xl[kb]);
             }
         };
         Scale2 sc = scale_of_max(xmax);
@@ -1707,8 +1710,9 @@ static int device_cus() {
     return cus[dev];
 }
 
-// the 16-ray two-waves-per-SIMD head (k_sam_head_w8): SAMNERF_HEAD_W8=1 / 2
-// at build time (timing builds), or diagnostic forms 30 / 31
+// the 16-ray two-waves-per-SIMD head (k_sam_head_w8): SAMNERF_HEAD_W8=1 (the
+// product) / 2 at build time, or diagnostic forms 30 / 31; any other
+// SAMNERF_HEAD_V in the diagnostic build selects a k_sam_head_h16 form
 [[maybe_unused]] static int head_w8() {      // 0: k_sam_head_h16q, 1: 8-wave workgroups, 2: two 4-wave workgroups per CU
 #ifdef SAMNERF_DIAG_VARIANTS
     const char* v = diag_env("SAMNERF_HEAD_V");

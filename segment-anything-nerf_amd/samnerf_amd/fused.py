@@ -220,7 +220,9 @@ class FusedRenderer:
         ts = [n.grid_mlp.net[i].weight for i in range(3)]
         if m.with_sam:
             ts += [n.samvit_mlp[0].net[i].weight for i in range(5)]
-        return (int(m.head_mode), tuple((t.data_ptr(), t._version) for t in ts))
+        # (the packed regions lead the workspace, raymarch.hip carve(): their
+        # place does not depend on N; the model fields before them are here)
+        return (int(m.head_mode), int(m.with_sam), tuple((t.data_ptr(), t._version) for t in ts))
 
     def workspace(self, m, N, device):
         """Scratch of one render call, one buffer per (device, stream): calls

@@ -156,8 +156,11 @@ def test_early_exit_nan_sigma_stays_in_its_segment(hip_lib, cuda):
     ws = fr.render(ro, rd, keep_workspace=True)["_workspace"][0]
     with torch.no_grad():
         net.grid_mlp.net[2].weight[0].fill_(float("nan"))   # sigma row of grid_mlp's last layer
-    # carve(): snf 2N, bins1 65N, bins2 33N, wtmp 128N, u_f 96N, w_f 32N, rows 164N floats
-    off = sum(_align256(4 * f * N) for f in (2, 65, 33, 128, 96, 32))
+    # carve(): the N-independent packed weights first (gpack 2 x 16 slots x 64
+    # lanes x 4 words, gexp 4 floats, no SAM head), then snf 2N, rec 8N,
+    # bins1 65N, bins2 33N, wtmp 128N, u_f 96N, w_f 32N, rows 164N floats
+    off = _align256(4 * 2 * 16 * 64 * 4) + _align256(4 * 4)
+    off += sum(_align256(4 * f * N) for f in (2, 8, 65, 33, 128, 96, 32))
     region = ws[off:off + 4 * 164 * N]
     region.fill_(0x5A)
     out = fr.render(ro, rd, keep_workspace=True)

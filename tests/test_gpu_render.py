@@ -251,7 +251,8 @@ def test_sam_head_f16x3_scaling_over_wide_ranges(hip_lib, cuda):
 
 @pytest.mark.parametrize("n", [1000, 128 * 300 + 37, 128 * 1024])
 def test_sam_head_persistent_form_bit_identical(hip_lib, cuda, n):
-    """The product head (k_sam_head_h16q: one workgroup per CU over 128-ray
+    """The persistent 32-ray head (k_sam_head_h16q, the product through round
+    5 and the diagnostic build's form 0: one workgroup per CU over 128-ray
     tiles, the next tile's rows streamed into LDS, the weight ring running on
     across tiles) equals the one-block-per-tile kernel (diagnostic form 4) bit
     for bit: ragged tails, more tiles than compute units (several tiles per
@@ -266,28 +267,31 @@ def test_sam_head_persistent_form_bit_identical(hip_lib, cuda, n):
     rows *= 10.0 ** (torch.rand(n, 1, generator=g) * 8 - 4)
     rows[:, 163] = 0.0
     rows = rows.to(cuda)
-    prod = FusedRenderer(net).sam_head(rows)
-    os.environ["SAMNERF_HEAD_V"] = "4"
+    out = {}
     try:
         with _lib.diag_library():
-            tile = FusedRenderer(net).sam_head(rows)
+            for form in ("0", "4"):
+                os.environ["SAMNERF_HEAD_V"] = form
+                out[form] = FusedRenderer(net).sam_head(rows)
     finally:
         os.environ.pop("SAMNERF_HEAD_V", None)
-    assert torch.isfinite(prod).all()
-    assert torch.equal(prod, tile)
+    assert torch.isfinite(out["0"]).all()
+    assert torch.equal(out["0"], out["4"])
 
 
 
 @pytest.mark.parametrize("form", ["30", "31"])
 @pytest.mark.parametrize("n", [1000, 128 * 300 + 37, 128 * 1024])
 def test_sam_head_w8_form_is_fp32_equivalent(hip_lib, cuda, n, form):
-    """The 16-ray two-waves-per-SIMD head (k_sam_head_w8, diagnostic forms 30:
-    one 8-wave workgroup per CU, 128-ray tiles; 31: two 4-wave workgroups per
-    CU, 64-ray tiles; v_mfma_f32_16x16x32_f16, 32-deep k-blocks) on
-    rows spanning 1e-4 .. 1e4 per ray: as close to the float64 head as the
-    exact fp32 MFMA head (within 2x), within 1e-6 of the product f16x3 head
-    relative to the output scale; ragged tails and several tiles per
-    workgroup (the rows streamed into LDS, the weight ring across tiles)."""
+    """The 16-ray two-waves-per-SIMD head (k_sam_head_w8; form 30, the
+    product since round 6: one 8-wave workgroup per CU, 128-ray tiles; 31: two
+    4-wave workgroups per CU, 64-ray tiles; v_mfma_f32_16x16x32_f16, 32-deep
+    k-blocks) on rows spanning 1e-4 .. 1e4 per ray: as close to the float64
+    head as the exact fp32 MFMA head (within 2x), within 1e-6 of the 32-ray
+    f16x3 head (k_sam_head_h16q, diagnostic form 0) relative to the output
+    scale; form 30 of the diagnostic build is the product bit for bit; ragged
+    tails and several tiles per workgroup (the rows streamed into LDS, the
+    weight ring across tiles)."""
     import copy
     from samnerf_amd import _lib
     from samnerf_amd.fused import FusedRenderer
@@ -300,14 +304,18 @@ def test_sam_head_w8_form_is_fp32_equivalent(hip_lib, cuda, n, form):
     rows[:5] = 0.0
     rows[:, 163] = 0.0
     rows = rows.to(cuda)
-    prod = FusedRenderer(net).sam_head(rows).cpu().double()
+    product = FusedRenderer(net).sam_head(rows).cpu().double()
     ex = FusedRenderer(net, head_mode=1).sam_head(rows).cpu().double()
-    os.environ["SAMNERF_HEAD_V"] = form
     try:
         with _lib.diag_library():
+            os.environ["SAMNERF_HEAD_V"] = "0"
+            prod = FusedRenderer(net).sam_head(rows).cpu().double()
+            os.environ["SAMNERF_HEAD_V"] = form
             w8 = FusedRenderer(net).sam_head(rows).cpu().double()
     finally:
         os.environ.pop("SAMNERF_HEAD_V", None)
+    if form == "30":
+        assert torch.equal(w8, product)
     head = copy.deepcopy(net.samvit_mlp).cpu()
     with torch.no_grad():
         ref = head.double()(rows[:, :163].cpu().double())
@@ -338,6 +346,41 @@ def test_exact_fp32_mode_vs_oracle(hip_lib, cuda):
     f = {k: max_abs(fast[k], ref[k]) for k in ("image", "weights_sum", "samvit")}
     print("exact vs oracle", e, "f16x3 vs oracle", f, "f16x3 vs exact",
           max_abs(exact["samvit"], fast["samvit"]))
+    assert e["image"] < 2e-6 and e["weights_sum"] < 2e-6 and e["samvit"] < 2e-5, e
+    assert f["image"] < 2e-6 and f["weights_sum"] < 2e-6 and f["samvit"] < 2e-5, f
+    assert max_abs(exact["samvit"], fast["samvit"]) < 2e-5
+
+
+@pytest.mark.parametrize("small", ["hashed", "dense"])
+def test_final_joint_scale_over_wide_level_ranges(hip_lib, cuda, small):
+    """k_final's layer 1 takes ONE f16x3 scale over both k-blocks
+    (all 16 levels, SAMNERF_FINAL_JOINT), so a level far below the column's
+    max keeps fewer bits in its fp16 halves.  With the hashed (or the dense)
+    levels' embeddings 2^-20 of the others, the default form still sits at
+    fp32 rounding against the oracle and the exact-fp32 form, as at equal
+    magnitudes (test_exact_fp32_mode_vs_oracle)."""
+    from samnerf_amd import ops
+    from samnerf_amd.fused import FusedRenderer
+    spec = synth.ModelSpec(with_sam=True)
+    params = dict(synth.make_params(spec, seed=13, emb_scale=0.5, ln_jitter=0.1))
+    net = make_net(spec, params, cuda)
+    off5 = int(net.grid.offsets[5])                           # levels 0-4 dense, 5-15 hashed
+    emb = np.array(params["grid.embeddings"], dtype=np.float32, copy=True)
+    if small == "hashed":
+        emb[off5:] *= np.float32(2.0 ** -20)
+    else:
+        emb[:off5] *= np.float32(2.0 ** -20)
+    params["grid.embeddings"] = emb
+    with torch.no_grad():
+        net.grid.embeddings.copy_(torch.from_numpy(emb))
+    pose, intr = synth.gui_camera(64, 64, rot=synth.random_rotation(8))
+    ro, rd = ops.get_rays(pose, intr, 64, 64, device=cuda)
+    exact = FusedRenderer(net, head_mode=1).render(ro, rd)
+    fast = FusedRenderer(net, head_mode=0).render(ro, rd)
+    ref = oracle_for(spec, params).run(ro.cpu(), rd.cpu(), return_feats=1)
+    e = {k: max_abs(exact[k], ref[k]) for k in ("image", "weights_sum", "samvit")}
+    f = {k: max_abs(fast[k], ref[k]) for k in ("image", "weights_sum", "samvit")}
+    print(small, "exact vs oracle", e, "f16x3 vs oracle", f)
     assert e["image"] < 2e-6 and e["weights_sum"] < 2e-6 and e["samvit"] < 2e-5, e
     assert f["image"] < 2e-6 and f["weights_sum"] < 2e-6 and f["samvit"] < 2e-5, f
     assert max_abs(exact["samvit"], fast["samvit"]) < 2e-5
@@ -711,6 +754,11 @@ def test_packed_weight_reuse(hip_lib, cuda):
     FusedAdam([w], lr=1e-2).step()                          # raw-pointer update, version bumped
     d = fr.render(ro, rd)
     assert fr.last_reuse_packed == 0 and same(d, FusedRenderer(net).render(ro, rd)) and not same(c, d)
+    # another ray count on the same workspace: the packed weights sit at
+    # N-independent offsets (raymarch.hip carve())
+    n2 = 1000
+    h = fr.render(ro[:n2], rd[:n2])
+    assert fr.last_reuse_packed == 1 and same(h, FusedRenderer(net).render(ro[:n2], rd[:n2]))
     fr2 = FusedRenderer(net)
     fr2.render(ro, rd, feats=False)                         # the head's weights not packed
     e = fr2.render(ro, rd)

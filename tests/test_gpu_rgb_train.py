@@ -102,7 +102,7 @@ def test_fused_rgb_step_matches_cpu_twin(hip_lib, cuda):
     assert (img.cpu() - img_c.detach()).abs().max().item() < 1e-5
     assert (out["weights_sum"].cpu() - out_c["weights_sum"].detach()).abs().max().item() < 1e-5
     for k in ("proposal_loss", "distort_loss"):
-        a, b = float(out[k]), float(out_c[k])
+        a, b = (float(torch.as_tensor(x).detach()) for x in (out[k], out_c[k]))
         assert abs(a - b) <= 1e-4 * abs(b) + 1e-8, (k, a, b)
     assert abs(float(loss.detach()) - float(loss_c.detach())) <= 1e-4 * abs(float(loss_c.detach())) + 1e-7
     _compare_grads(gpu, cpu)

@@ -61,6 +61,26 @@ def test_r2_mfma_result_read_early_and_accumulation_chain_allowed():
     assert lint_text(seq.replace("s_nop 7", "s_nop 11")) == []
 
 
+def test_r2_asm_overwrites_an_mfma_result_in_flight():
+    """The second hazard the lint found (round 6, k_sam_head_w8 once it became
+    the product): hipcc scheduled the f16x3 split's asm right behind a 4-pass
+    MFMA chain and gave its outputs the chain's result registers, so the
+    split's first v_mul wrote v0 / v1 while the MFMA writing v[0:3] was in
+    flight (the split now opens with s_nop 7 there: split8_f16<true>)."""
+    seq = """
+        v_mfma_f32_16x16x32_f16 v[0:3], v[8:11], v[58:61], v[0:3]
+        v_mfma_f32_16x16x32_f16 v[78:81], v[8:11], v[62:65], v[0:3]
+        ;;#ASMSTART
+        v_mul_f32 v0, v82, v182
+        v_mul_f32 v1, v57, v182
+        ;;#ASMEND
+    """
+    found = lint_text(seq)
+    assert found and all(f[0] in ("R2", "R3") for f in found), found
+    fixed = seq.replace(";;#ASMSTART", ";;#ASMSTART\n        s_nop 7")
+    assert lint_text(fixed) == []
+
+
 def test_r3_write_after_mfma_srcc_read():
     seq = """
         ;;#ASMSTART
