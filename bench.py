@@ -589,6 +589,7 @@ class ViewRunner:
         self.cands = ([1, 2] if rule == 1 else [2, 3]) if not args.streams else [args.streams]
         self.n_active = args.streams or rule
         self.tuned = None
+        self.tuned_clock = None
         self.clock = None
         self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                            for _ in range(max(self.cands) - 1)]
@@ -658,16 +659,27 @@ class ViewRunner:
             # (interleaved: 3 rounds of 8 views per candidate, ~0.2 s)
             self.tuned = {k: 0.0 for k in self.cands}
             n_tune, rounds = 8, 3
-            for _ in range(rounds):
-                for k in self.cands:
+            # the shader clock of each tuning group too (the timed views'
+            # clock is beside it in the line: a box whose clock moved between
+            # the tuning and the timed views shows it)
+            tstamps = torch.zeros(rounds * len(self.cands), 2, 768, dtype=torch.int64, device=self.dev)
+            cur = torch.cuda.current_stream(self.dev)
+            for rnd in range(rounds):
+                for ci, k in enumerate(self.cands):
                     self.n_active, self.n_step = k, 0
                     torch.cuda.synchronize()
                     if self.world > 1:
                         dist.barrier()
                     t0 = time.perf_counter()
+                    sg = tstamps[rnd * len(self.cands) + ci]
+                    lib().samnerf_clock_stamp(ctypes.c_void_p(sg[0].data_ptr()), ctypes.c_void_p(cur.cuda_stream))
                     for _ in range(n_tune):
                         self.step()
                     self._flush()
+                    for st in self.streams:
+                        if st.cuda_stream != cur.cuda_stream:
+                            cur.wait_stream(st)
+                    lib().samnerf_clock_stamp(ctypes.c_void_p(sg[1].data_ptr()), ctypes.c_void_p(cur.cuda_stream))
                     torch.cuda.synchronize()
                     dtk = time.perf_counter() - t0
                     if self.world > 1:
@@ -677,6 +689,12 @@ class ViewRunner:
                     self.tuned[k] += dtk * 1e3 / (n_tune * rounds)
             self.n_active = min(self.tuned, key=self.tuned.get)
             self.n_step = 0
+            ts = tstamps.cpu().numpy()
+            self.tuned_clock = {}
+            for ci, k in enumerate(self.cands):
+                g = [timed_clock(ts[rnd * len(self.cands) + ci]) for rnd in range(rounds)]
+                g = [c["ghz"] for c in g if c]
+                self.tuned_clock[k] = float(np.mean(g)) if g else None
         stamps = torch.zeros(2, 768, dtype=torch.int64, device=self.dev)
         torch.cuda.synchronize()
         if self.world > 1:
@@ -1195,6 +1213,9 @@ def main():
                        "views_in_flight": runner.n_active,
                        "views_in_flight_tuned_ms": ({str(k): round(v, 4) for k, v in runner.tuned.items()}
                                                     if runner.tuned else None),
+                       "views_in_flight_tuned_clock_ghz": ({str(k): (round(v, 4) if v else None)
+                                                            for k, v in runner.tuned_clock.items()}
+                                                           if runner.tuned_clock else None),
                        "timed_clock_ghz": round(runner.clock["ghz"], 4) if runner.clock else None,
                        "parallelism": (f"ray-sharded row bands x{world}, RCCL all-gather of each view "
                                        f"overlapped with the next view's rendering, views issued on "

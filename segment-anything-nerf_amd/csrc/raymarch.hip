@@ -191,6 +191,7 @@ struct PropArgs {
     float* bins_out;       // [TN][N]
     int32_t* inds_out;     // [TN][N] searchsorted indices, or null (parity taps only)
     float* w_out;          // [T][N] composited weights, or null (parity taps only)
+    uint32_t pdf_seq;      // diagnostic build, SAMNERF_PDF_SEQ=1: every ray on the sequential phase A
 };
 
 // Bin i of a stage's input for slot r (ray `ray`): stage 0 linspace(0, 1, T+1)
@@ -378,9 +379,19 @@ __global__ void __launch_bounds__(256) k_snf(PropArgs a) {
 // indices and bins are identical, with a quarter of the dependent steps.
 template <int T, int TN, bool FIRST>
 __device__ __forceinline__ void prop_pdf_phases(const PropArgs& a, float* sw, uint32_t r0, uint32_t nr);
+#ifndef SAMNERF_PDF_SPLIT
+#define SAMNERF_PDF_SPLIT 1                  // phase A split over the block's 4 waves (below)
+#endif
+#ifndef SAMNERF_PDF_SPLIT_MIN
+#define SAMNERF_PDF_SPLIT_MIN 128            // from this many samples per ray
+#endif
 
 template <int T, int TN, bool FIRST>
-__global__ void __launch_bounds__(256) k_prop_pdf(PropArgs a) {
+__global__ void __launch_bounds__(256)
+// T = 128: 4 waves per SIMD, the 4 blocks per CU the ds rows' LDS allows
+// (the split phase A otherwise takes 146 VGPRs, 3 waves)
+__attribute__((amdgpu_waves_per_eu(T >= 128 ? 4 : 1, T >= 128 ? 4 : 8)))
+k_prop_pdf(PropArgs a) {
     constexpr int SW = T + 1;                 // T + 1 cdf entries per row (odd stride)
     __shared__ float sw[64 * SW];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, part = tid >> 6;
@@ -407,13 +418,163 @@ __global__ void __launch_bounds__(256) k_prop_pdf(PropArgs a) {
     prop_pdf_phases<T, TN, FIRST>(a, sw, r0, nr);
 }
 
+// Exact-sum window of a run of float terms (phase A's double cumulative
+// sums): the exponent fields of its non-zero terms and whether any term is
+// subnormal, infinite or NaN.  When every term is normal or zero and the
+// exponents of the largest and smallest non-zero term differ by at most 22,
+// every partial sum of up to 128 of them is a multiple of the smallest
+// term's ulp below 2^(e_max + 8), i.e. exactly representable in double
+// (53 bits): then each partial sum is the exact real sum, whatever order it
+// was formed in, and a prefix taken as (sum of the earlier quarters) + (this
+// quarter's terms in order) is bit for bit the sequential prefix.
+struct SumWindow {
+    uint32_t emin = 0xFFu, emax = 0u, bad = 0u;
+    __device__ __forceinline__ void add(float v) {
+        const uint32_t e = (__float_as_uint(v) >> 23) & 0xFFu;
+        const bool nz = (__float_as_uint(v) & 0x7FFFFFFFu) != 0u;
+        bad |= (nz && (e == 0u || e == 0xFFu)) ? 1u : 0u;
+        emin = nz ? min(emin, e) : emin;
+        emax = nz ? max(emax, e) : emax;
+    }
+    __device__ __forceinline__ uint32_t pack() const { return bad << 16 | emax << 8 | emin; }
+};
+__device__ __forceinline__ bool sum_window_exact(const uint32_t* w4) {
+    uint32_t emin = 0xFFu, emax = 0u, bad = 0u;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        emin = min(emin, w4[p] & 0xFFu);
+        emax = max(emax, (w4[p] >> 8) & 0xFFu);
+        bad |= w4[p] >> 16;
+    }
+    return bad == 0u && (emax < emin || emax - emin <= 22u);
+}
+
 // Phases A and B of the proposal pdf over 64 rays whose ds rows sit in LDS
 // (row stride T + 1); every thread of the block calls it after a barrier.
+//
+// Phase A (SAMNERF_PDF_SPLIT, round 6): the four waves of the block take a
+// quarter of each ray's samples.  The reference's two serial chains -- the
+// double cumulative sum of ds behind the transmittance, and the double
+// cumulative sum of the pdf behind the cdf -- are prefix sums: each wave sums
+// its quarter in order, the quarter sums meet in LDS, and each wave runs its
+// quarter from the sum of the quarters before it.  That is the sequential
+// result bit for bit when the ray's terms pass the exact-sum window
+// (SumWindow), checked per ray at run time; a ray that does not (ds spanning
+// more than 2^22, or non-finite) takes the whole sequential chain in wave 0
+// as before.  The pdf terms (w + 0.01) / sum with w in [0, 1] always pass.
+// One serial chain of 128 steps per ray, one wave per SIMD at the LDS-bound
+// occupancy, was the latency that bounded k_prop_pdf.
 template <int T, int TN, bool FIRST>
 __device__ __forceinline__ void prop_pdf_phases(const PropArgs& a, float* sw, uint32_t r0, uint32_t nr) {
     constexpr int SW = T + 1;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, part = tid >> 6, N = a.N;
     float* row = sw + lane * SW;
+    // stage 0 only: at T = 64 the split's barriers and registers cost more
+    // than the 64-step chains it shortens (prop1 0.304-0.308 against
+    // 0.299-0.303 ms sequential; prop0 0.552-0.560 against 0.580-0.588)
+    constexpr bool kSplit = SAMNERF_PDF_SPLIT && T >= SAMNERF_PDF_SPLIT_MIN;
+    if constexpr (kSplit) {
+    constexpr int Q = T / 4;
+    __shared__ double qsum[4][64];            // per quarter and ray: the quarter's double sum
+    __shared__ uint32_t qwin[4][64];          // and its SumWindow
+    const bool rl = lane < nr;
+    const int k0 = (int)part * Q;
+    // A1: ds quarter sums (the last sample's ds is replaced by +inf and the
+    // sum after it is never read: not part of the window)
+    {
+        SumWindow win;
+        double q = 0.0;
+        if (rl) {
+#pragma unroll 8
+            for (int k = k0; k < k0 + Q; ++k) {
+                if (k == T - 1) break;
+                const float ds = row[k];
+                win.add(ds);
+                q += (double)ds;
+            }
+        }
+        qsum[part][lane] = q;
+        qwin[part][lane] = win.pack();
+    }
+    __syncthreads();
+    // A2: composite.  Exact rays: each wave its quarter from the earlier
+    // quarters' sum; the others: wave 0 the whole ray, in order.
+    if (rl) {
+        const uint32_t w4[4] = {qwin[0][lane], qwin[1][lane], qwin[2][lane], qwin[3][lane]};
+        if (!a.pdf_seq && sum_window_exact(w4)) {
+            double cum = 0.0;
+            for (int p = 0; p < (int)part; ++p) cum += qsum[p][lane];
+#pragma unroll 8
+            for (int k = k0; k < k0 + Q; ++k) row[k] = composite_step(row[k], cum, k == T - 1);
+        } else if (part == 0) {
+            double cum = 0.0;
+#pragma unroll 8
+            for (int k = 0; k < T; ++k) row[k] = composite_step(row[k], cum, k == T - 1);
+        }
+    }
+    __syncthreads();
+    // A3: the weights out (taps) and the torch-ordered normaliser (each wave
+    // for itself, over all T weights), then -- after a barrier, so no wave
+    // still reads weights -- each wave replaces its quarter's weights by their
+    // pdf (w + 0.01) / sum in place and forms the quarter's double sum
+    float wsum = 0.0f;
+    if (rl) {
+        if (a.w_out)
+            for (int k = k0; k < k0 + Q; ++k) a.w_out[(size_t)k * N + r0 + lane] = row[k];
+        wsum = torch_row_sum(T, [&](int i) { return row[i] + 0.01f; });
+    }
+    __syncthreads();
+    float pfirst = 0.0f;                      // this quarter's first pdf (A4 reads it from here)
+    {
+        SumWindow win;
+        double q = 0.0;
+        if (rl) {
+#pragma unroll 8
+            for (int k = k0; k < k0 + Q; ++k) {
+                const float pdf = (row[k] + 0.01f) / wsum;
+                row[k] = pdf;
+                win.add(pdf);
+                q += (double)pdf;
+            }
+            pfirst = row[k0];
+        }
+        qsum[part][lane] = q;
+        qwin[part][lane] = win.pack();
+    }
+    __syncthreads();
+    // A4: cdf[i + 1] = min(float(double cumsum of pdf), 1) in place: wave p
+    // writes entries k0 + 1 .. k0 + Q, of which only k0 + Q is a pdf another
+    // wave reads -- the next wave's first, which it holds in pfirst
+    if (rl) {
+        const uint32_t w4[4] = {qwin[0][lane], qwin[1][lane], qwin[2][lane], qwin[3][lane]};
+        if (!a.pdf_seq && sum_window_exact(w4)) {
+            double c = 0.0;
+            for (int p = 0; p < (int)part; ++p) c += qsum[p][lane];
+            if (part == 0) row[0] = 0.0f;
+            float pnext = pfirst;
+#pragma unroll 8
+            for (int i = 0; i < Q; ++i) {
+                const float pi = pnext;
+                if (i + 1 < Q) pnext = row[k0 + i + 1];
+                c += (double)pi;
+                row[k0 + i + 1] = fminf((float)c, 1.0f);
+            }
+        } else if (part == 0) {
+            // not exact (a NaN pdf): wave 0 the whole chain in order, the
+            // other waves write nothing of this ray (every pdf is in LDS:
+            // no wave wrote a cdf entry of it)
+            double c = 0.0;
+            float pnext = row[0];
+            row[0] = 0.0f;
+            for (int i = 0; i < T; ++i) {
+                const float pi = pnext;
+                if (i + 1 < T) pnext = row[i + 1];
+                c += (double)pi;
+                row[i + 1] = fminf((float)c, 1.0f);
+            }
+        }
+    }
+    } else {
     if (part == 0 && lane < nr) {
         // unrolled by 8: the LDS reads run ahead of the double-precision
         // chains (a full unroll takes 248 VGPRs and halves occupancy)
@@ -434,6 +595,7 @@ __device__ __forceinline__ void prop_pdf_phases(const PropArgs& a, float* sw, ui
             c += (double)pdf;
             row[i + 1] = fminf((float)c, 1.0f);
         }
+    }
     }
     __syncthreads();
     if (lane >= nr) return;
@@ -2882,6 +3044,10 @@ int proposal_forward(const samnerf_model* m, const TrainGeometry& g, const float
     pa.rays_d = rays_d;
     pa.cnf = cnf;
     pa.N = N;
+    {
+        const char* ps = diag_env("SAMNERF_PDF_SEQ");
+        pa.pdf_seq = ps && atoi(ps) != 0 ? 1u : 0u;
+    }
     pa.tiles = RayTiles{0u, 0u, 32u};
     pa.n_cnf = n_cnf;
     for (int i = 0; i < 6; ++i) pa.aabb[i] = m->aabb[i];
@@ -3035,6 +3201,10 @@ int render_impl(const samnerf_model* m, const float* rays_o, const float* rays_d
     pa.rays_d = rays_d;
     pa.cnf = cam_near_far;
     pa.N = N;
+    {
+        const char* ps = diag_env("SAMNERF_PDF_SEQ");
+        pa.pdf_seq = ps && atoi(ps) != 0 ? 1u : 0u;
+    }
     pa.tiles = tiles;
     pa.n_cnf = n_cnf;
     for (int i = 0; i < 6; ++i) pa.aabb[i] = m->aabb[i];

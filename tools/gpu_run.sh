@@ -34,7 +34,7 @@ if has smoke; then
 fi
 if has tests; then
   step tests 900 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -q ${PYTEST_K:+-k "$PYTEST_K"} \
-    -p no:cacheprovider -rfE --timeout 120 --timeout-method thread --durations=15
+    -p no:cacheprovider -rfE --timeout 120 --timeout-method thread --durations=15 ${PYTEST_ARGS:-}
   rc=$?
   grep -E "passed|failed" "$OUT/tests.log" | tail -3
   [ $rc -ne 0 ] && [ "${KEEP_GOING:-0}" != "1" ] && exit $rc
