@@ -1958,6 +1958,12 @@ struct SgridArgs {
     // [N / tap_stride][T][16][8] (k_sgrid_box4)
     uint32_t* rows_tap;
     uint32_t tap_stride;
+    // diagnostic build only (SAMNERF_SGRID_PATHS = hex device address of 8
+    // uint64): per (wave, sample, level) of k_sgrid_box4, [0] uniform-cell,
+    // [1] staged box, [2] direct gathers; [3] wave-samples skipped (all
+    // weights 0); [4] box slots and [5] box cells of the staged boxes; null
+    // in every other render
+    unsigned long long* paths;
 };
 
 // f_sam = sum_k w_k * s_grid(x_k).  A block is one level x 64 neighbouring
@@ -2109,6 +2115,9 @@ k_sgrid_box4(SgridArgs a) {
         const float nz = ld(ub, (kn * 3u + 2u) * N4 + rr * 4u);
         const float nw = ld(wb, kn * N4 + rr * 4u);
         // samples with weight 0 on all 64 rays (N1's dropped samples) add nothing
+#ifdef SAMNERF_DIAG_VARIANTS
+        if (a.paths && lane == 0u && __builtin_amdgcn_ballot_w64(w != 0.0f) == 0) atomicAdd(a.paths + 3, 1ull);
+#endif
         if (__builtin_amdgcn_ballot_w64(w != 0.0f) != 0) {
             const f2v wv = {w, w};
             auto add = [&](int l, const float* f) {
@@ -2137,6 +2146,16 @@ k_sgrid_box4(SgridArgs a) {
                 uint32_t* rt = nullptr;                     // parity taps only
                 if (TAP && live && r % a.tap_stride == 0u)
                     rt = a.rows_tap + ((size_t)(r / a.tap_stride) * T + k) * 128u + (4 * g + l) * 8;
+#ifdef SAMNERF_DIAG_VARIANTS
+                if (a.paths && lane == 0u) {
+                    const int path = (SGRID_UNI && b.uni && ordered) ? 0 : b.slots <= kBoxSlots ? 1 : 2;
+                    atomicAdd(a.paths + path, 1ull);
+                    if (path == 1) {
+                        atomicAdd(a.paths + 4, (unsigned long long)b.slots);
+                        atomicAdd(a.paths + 5, (unsigned long long)(b.ex * b.ey * b.ez));
+                    }
+                }
+#endif
                 if (SGRID_UNI && b.uni && ordered) {
                     // one cell for the whole wave: its 8 corner rows through the
                     // scalar cache, no box staging, no LDS reads (round 5)
@@ -3384,6 +3403,10 @@ int render_impl(const samnerf_model* m, const float* rays_o, const float* rays_d
         sa.rows = rows;
         sa.rows_tap = tp.srows;
         sa.tap_stride = tp.row_stride ? tp.row_stride : 1u;
+        {
+            const char* pp = diag_env("SAMNERF_SGRID_PATHS");
+            sa.paths = pp ? reinterpret_cast<unsigned long long*>(strtoull(pp, nullptr, 16)) : nullptr;
+        }
         mark_stage(3, s);
         const dim3 sg(xcd_blocks(div_up(N, 64)), 16);
         const dim3 sb(xcd_blocks(div_up(N, 64)), 4);
