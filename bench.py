@@ -887,7 +887,8 @@ def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None, timed_clock=N
         if "valu_insts_per_ray" in r:
             ci, ci_src = (stage_cpi[st], os.path.relpath(VALU_CPI, REPO)) if st in stage_cpi else (cpi, cpi_src)
             c = r["valu_insts_per_ray"] * band_rays * ci
-            cand["valu"] = {"unit": "VALU pipe cycles / SIMD cycles", "frac": c / cyc_avail(ms),
+            cand["valu"] = {"unit": "VALU-busy cycles per SIMD per ns (GHz); peak = the nominal clock",
+                            "frac": c / cyc_avail(ms),
                             "valu_insts_per_ray": r["valu_insts_per_ray"], "cycles_per_inst": ci,
                             "cycles_per_inst_source": ci_src,
                             # the other basis: every VALU
@@ -915,19 +916,26 @@ def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None, timed_clock=N
                                   "more than 10 % below it")
                 else:
                     v["basis"] = "static opcode mix, within 10 % of PMC SQ_ACTIVE_INST_VALU x 4"
+            # achieved / peak in the unit: VALU-busy cycles per SIMD per ns
+            # against the SIMD's nominal 2.4 cycles per ns (frac = their ratio)
+            cand["valu"]["achieved"] = cand["valu"]["frac"] * CLOCK_GHZ
+            cand["valu"]["peak"] = CLOCK_GHZ
         if st == "sam_head":
             cyc = HEAD_MFMA_CYCLES_PER_32[head_mode] * band_rays / 32
             cand["mfma"] = {"unit": "TFLOP/s", "frac": cyc / cyc_avail(ms),
                             "achieved_fp32_equiv": HEAD_FLOP_PER_RAY * band_rays / (ms * 1e-3) / 1e12,
                             "peak": F32_MFMA_PEAK_TFS if head_mode == 1 else BF16_MFMA_PEAK_TFS,
+                            "achieved": None,
                             "basis": "MFMA issue cycles of the head's structure (f16x3: 86 k-blocks x 8 "
                                      "tiles x 3 v_mfma_f32_32x32x16_f16 per 32 rays) / (1024 SIMDs x "
                                      "2.4 GHz x time)"}
+            cand["mfma"]["achieved"] = cand["mfma"]["frac"] * cand["mfma"]["peak"]   # at the structure's rate
             if "mfma_busy_cycles_per_ray" in r:
                 cand["mfma"]["pmc_mfma_busy_frac"] = r["mfma_busy_cycles_per_ray"] * band_rays / cyc_avail(ms)
         elif r.get("mfma_busy_cycles_per_ray"):
-            cand["mfma"] = {"unit": "MFMA busy cycles / SIMD cycles",
-                            "frac": r["mfma_busy_cycles_per_ray"] * band_rays / cyc_avail(ms)}
+            f = r["mfma_busy_cycles_per_ray"] * band_rays / cyc_avail(ms)
+            cand["mfma"] = {"unit": "MFMA-busy cycles per SIMD per ns (GHz); peak = the nominal clock",
+                            "frac": f, "achieved": f * CLOCK_GHZ, "peak": CLOCK_GHZ}
         if not cand:
             return None
         bound = max(cand, key=lambda k: cand[k]["frac"])
