@@ -553,11 +553,419 @@ k_mask_head(MaskArgs a) {
     }
 }
 
+// ============================================ f16x3, 16-ray waves, 2 per SIMD
+// (round 6; SAMNERF_MASK_W8, the SAM head's k_sam_head_w8 structure applied
+// to the mask head).  k_mask_head holds 426 registers per
+// 32-ray wave, one wave per SIMD, so each sample's m_grid gathers and its
+// MFMAs run one after the other on every SIMD (the gathers were the largest
+// single stall, see the ring's note above).  Here a workgroup is 8 waves of
+// 16 ray slots (128 slots, as before) on v_mfma_f32_16x16x32_f16: a layer's
+// 256 units are 16 accumulator tiles of 4 registers (64 where the 32-ray form
+// holds 128), so two waves share a SIMD and one wave's gathers, splits and
+// leaky_relu run under the other's MFMAs.
+//
+// Lane (j, g): ray slot j of the wave, input group g (8 inputs of a 32-deep
+// k-block).  Layer 0's k-block b < 4 is m_grid levels 4 b .. 4 b + 3 (lane
+// group g: level 4 b + g, its 8 channels = one 32-B corner row per corner),
+// k-block 4 is geo_feat (g 0: 0-7, g 1: 8-14 + pad, g 2-3: zero padding).
+// A hidden layer's k-block b is the accumulator tiles 2 b, 2 b + 1 (hunit,
+// the weights packed permuted to match), as in k_sam_head_w8.  Weight steps
+// of 16 KiB (8 tiles x 32-deep k-block, hi / lo): layer 0 10 steps (5
+// k-blocks x 2 halves of the tiles), layer 1 16, layer 2 OT (one per 16-unit
+// output tile, its 8 k-blocks in the step's 8 slots): 26 + OT per sample,
+// streamed through a 4-step LDS ring by LDS DMA (2 x 1 KiB per wave and step).
+// Arithmetic: the f16x3 products with per-tensor weight scales and per-ray
+// activation scales, as k_mask_head, over 32-deep instead of 16-deep k-blocks:
+// fp32-equivalent, not bit-identical to it (tests/test_gpu_mask.py: the
+// reference's goldens and the unfused op sequence within 1e-3, ragged
+// launches bit-equal to the full launch).
+// Measured (profiles/r6m_mask_w8_ab.txt, r6n_mask_w8_ab.txt, interleaved):
+// the --with_mask 512^2 view 7.57-7.71 ms against 7.84-7.94 for k_mask_head
+// (-3.5 %); 169 registers, no scratch.  Not the 2x two waves per SIMD could
+// give: the per-step barrier keeps a workgroup's 8 waves in lockstep, so the
+// two waves of a SIMD gather and multiply at the same time; two independent
+// 4-wave workgroups per CU (SAMNERF_MASK_W8=2) drift apart but must keep the
+// inputs in registers (no LDS for two rings and two input stages) and spill:
+// 9.1-9.2 ms.  Two levels' corner rows in flight instead of one: the same
+// time (MW8_LEVELS=2, 200 registers).
+#ifndef SAMNERF_MASK_W8
+#define SAMNERF_MASK_W8 1
+#endif
+#ifndef MW8_LEVELS
+#define MW8_LEVELS 1                          // levels' corner rows in flight per lane (1, 2 or 4)
+#endif
+namespace mw8 {
+constexpr int kRays = 16;                                      // ray slots per wave
+constexpr int kL0 = 5, kH = 8;                                   // layer-0 / hidden k-blocks (32 deep)
+constexpr int kNbuf = 4;
+constexpr int steps(int ot) { return 2 * kL0 + 2 * kH + ot; }
+__host__ __device__ constexpr int hunit(int b, int g, int m) { return 32 * b + (m < 4 ? 4 * g + m : 16 + 4 * g + m - 4); }
+}  // namespace mw8
+
+// packed[step][hi/lo][slot 8][lane 64] (step layout above), then kexp[3]
+template <int OT>
+__global__ void __launch_bounds__(1024)
+k_mask_pack_w8(const float* __restrict__ w0, const float* __restrict__ w1, const float* __restrict__ w2,
+               uint32_t K, uint4* __restrict__ packed) {
+    __shared__ float wm[3][16];
+    __shared__ int ke[3];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float m0 = 0.0f, m1 = 0.0f, m2 = 0.0f;
+    for (int i = tid; i < 256 * kMIn; i += 1024) m0 = fmaxf(m0, fabsf(w0[i]));
+    for (int i = tid; i < 256 * 256; i += 1024) m1 = fmaxf(m1, fabsf(w1[i]));
+    for (int i = tid; i < (int)K * 256; i += 1024) m2 = fmaxf(m2, fabsf(w2[i]));
+    m0 = wave_max64(m0);
+    m1 = wave_max64(m1);
+    m2 = wave_max64(m2);
+    if (lane == 0) {
+        wm[0][wave] = m0;
+        wm[1][wave] = m1;
+        wm[2][wave] = m2;
+    }
+    __syncthreads();
+    if (tid < 3) {
+        float m = 0.0f;
+        for (int w = 0; w < 16; ++w) m = fmaxf(m, wm[tid][w]);
+        ke[tid] = scale_exp_of_max(m);
+    }
+    __syncthreads();
+    constexpr int S = mw8::steps(OT);
+    for (int t = tid; t < S * 8 * 64; t += 1024) {
+        const int l = t & 63, slot = (t >> 6) & 7, step = t >> 9;
+        const int i = l & 15, g = l >> 4;
+        int layer;
+        float v[8];
+        if (step < 2 * mw8::kL0) {                     // layer 0: k-block step / 2, tiles 8 (step & 1) + slot
+            layer = 0;
+            const int unit = 16 * (8 * (step & 1) + slot) + i;
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int col = 32 * (step >> 1) + 8 * g + m;
+                v[m] = col < kMIn ? w0[unit * kMIn + col] : 0.0f;
+            }
+        } else if (step < 2 * (mw8::kL0 + mw8::kH)) {  // layer 1
+            layer = 1;
+            const int q = step - 2 * mw8::kL0, unit = 16 * (8 * (q & 1) + slot) + i;
+#pragma unroll
+            for (int m = 0; m < 8; ++m) v[m] = w1[unit * 256 + mw8::hunit(q >> 1, g, m)];
+        } else {                                       // layer 2: output tile step - 26, k-block = slot
+            layer = 2;
+            const int unit = 16 * (step - 2 * (mw8::kL0 + mw8::kH)) + i;
+#pragma unroll
+            for (int m = 0; m < 8; ++m) v[m] = (uint32_t)unit < K ? w2[unit * 256 + mw8::hunit(slot, g, m)] : 0.0f;
+        }
+        uint4 a, b;
+        to_operand<false>(v, exp2i(ke[layer]), a, b);
+        packed[(size_t)step * kStepVec + slot * 64 + l] = a;
+        packed[(size_t)step * kStepVec + 512 + slot * 64 + l] = b;
+    }
+    if (tid < 3) reinterpret_cast<int*>(packed + (size_t)S * kStepVec)[tid] = ke[tid];
+}
+
+template <int OT, int WAVES>
+struct MaskStreamW8 {
+    static constexpr int S = mw8::steps(OT);
+    static constexpr int kPieces = 16 / WAVES;          // 1-KiB pieces per wave and step
+    const uint4* __restrict__ packed;
+    uint4* Wb;            // [kNbuf][kStepVec]
+    int wave, lane;
+    uint32_t step, total;
+
+    // wave w moves uint4 64 kPieces w .. of step s (kPieces x 1 KiB) into
+    // ring slot s % kNbuf by LDS DMA; the step's offset is opaque (formed
+    // here, not hoisted as per-step pointers).  No VGPR is written inside the
+    // statements: a VGPR output could land on a register an MFMA issued just
+    // before still reads or writes, which hipcc does not pad for an asm
+    // statement (tools/isa_hazards.py R2 / R3)
+    __device__ __forceinline__ void request(uint32_t s) {
+        uint32_t so = (s % (uint32_t)S) * (uint32_t)(kStepVec * 16);
+        asm volatile("" : "+s"(so));
+        const char* base = reinterpret_cast<const char*>(packed) + so;
+        const uint32_t vo = (uint32_t)(wave * 64 * kPieces + lane) * 16u;
+        const uint32_t d = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)(Wb + (size_t)(s % (uint32_t)mw8::kNbuf) * kStepVec + wave * 64 * kPieces));
+#pragma unroll
+        for (int c = 0; c < kPieces; ++c) {
+            const uint32_t vc = vo + 1024u * (uint32_t)c;
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(vc), "s"(base), "s"(d + 1024u * (uint32_t)c));
+        }
+    }
+    __device__ __forceinline__ void begin() {
+        for (uint32_t s = 0; s + 1 < (uint32_t)mw8::kNbuf && s < total; ++s) request(s);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    __device__ __forceinline__ const uint4* start() {
+        if (step + mw8::kNbuf - 1 < total) request(step + mw8::kNbuf - 1);
+        return Wb + (size_t)(step % (uint32_t)mw8::kNbuf) * kStepVec + lane;
+    }
+    // step + 1's pieces landed: younger than them are at most the kPieces
+    // (kNbuf - 2) pieces of the steps after it (other loads in between only make the wait
+    // stricter); at the end of the stream everything
+    __device__ __forceinline__ void finish() {
+        if (step + mw8::kNbuf - 1 < total) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPieces * (mw8::kNbuf - 2)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        ++step;
+    }
+    // one 32-deep k-block of the current layer for tiles 8 HALF .. 8 HALF + 7
+    // (fragments in two batches of 4 tiles: 32 registers, not 64, at the
+    // layer-1 peak -- accumulators, operands and fragments -- of a 256-register wave)
+    template <int HALF>
+    __device__ __forceinline__ void run(floatx4 (&acc)[16], const uint4& bh, const uint4& bl) {
+        const uint4* cur = start();
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            uint4 fh[4], fl[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                fh[t] = cur[(4 * q + t) * 64];
+                fl[t] = cur[512 + (4 * q + t) * 64];
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                acc[8 * HALF + 4 * q + t] = mfma16_f16x3(fh[t], fl[t], bh, bl, acc[8 * HALF + 4 * q + t]);
+            if (q == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+        finish();
+    }
+    // one output tile: its 8 k-blocks from the step's 8 slots
+    __device__ __forceinline__ void run_out(floatx4& o, const uint4 (&ah)[mw8::kH], const uint4 (&al)[mw8::kH]) {
+        const uint4* cur = start();
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            uint4 fh[4], fl[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                fh[k] = cur[(4 * q + k) * 64];
+                fl[k] = cur[512 + (4 * q + k) * 64];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o = mfma16_f16x3(fh[k], fl[k], ah[4 * q + k], al[4 * q + k], o);
+            if (q == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+        finish();
+    }
+};
+
+__device__ __forceinline__ float ray_max4_mw8(float m) {             // lanes j, j + 16, j + 32, j + 48
+    m = fmaxf(m, __shfl_xor(m, 16));
+    return fmaxf(m, __shfl_xor(m, 32));
+}
+
+// leaky's max in place on the accumulator register ("+v"): the statement
+// then writes only a register whose MFMA result the multiply before it has
+// already waited for -- with a separate output, hipcc was free to pick a
+// register a still-running MFMA of the layer reads as SrcC (write-after-read,
+// tools/isa_hazards.py R3, found when this kernel was written)
+__device__ __forceinline__ void leaky_inplace(float& x) {
+    const float t = x * 0.01f;
+    asm("v_max_f32 %0, %0, %1" : "+v"(x) : "v"(t));
+}
+
+// leaky_relu on a layer's 16 tiles, then the next layer's B operands (k-block
+// b <- tiles 2 b, 2 b + 1) at the ray's scale; returns its exponent
+__device__ __forceinline__ int epilogue_w8(floatx4 (&acc)[16], uint4 (&ah)[mw8::kH], uint4 (&al)[mw8::kH]) {
+    float m = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = acc[t][r];
+            leaky_inplace(v);
+            acc[t][r] = v;
+            m = fmaxf(m, fabsf(acc[t][r]));
+        }
+    const int k = scale_exp_of_max(ray_max4_mw8(m));
+    const float s = exp2i(k);
+#pragma unroll
+    for (int b = 0; b < mw8::kH; ++b) {
+        const float v[8] = {acc[2 * b][0], acc[2 * b][1], acc[2 * b][2], acc[2 * b][3],
+                            acc[2 * b + 1][0], acc[2 * b + 1][1], acc[2 * b + 1][2], acc[2 * b + 1][3]};
+        split8_f16<true>(v, s, ah[b], al[b]);
+    }
+    return k;
+}
+
+// WAVES 8: one 512-thread workgroup per CU (128 ray slots), the layer-0
+// inputs through LDS.  WAVES 4: two independent 256-thread workgroups per CU
+// (64 slots each, its own weight ring and step barriers, the inputs in
+// registers): the two waves of a SIMD belong to different workgroups and
+// drift out of phase, so one's gathers run under the other's MFMAs, where the
+// 8 waves of one workgroup move in lockstep from barrier to barrier.
+template <int OT, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_mask_head_w8(MaskArgs a) {
+    // LDS: the weight ring | (WAVES 8) each wave's layer-0 inputs of the
+    // current sample (fp32, [k-block][part][lane]) | the level descriptors
+    constexpr bool XLDS = WAVES == 8;
+    constexpr int kXw = XLDS ? mw8::kL0 * 2 * 64 : 0;
+    __shared__ uint4 smem[mw8::kNbuf * kStepVec + WAVES * kXw + kDescVec];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int j = lane & 15, g = lane >> 4;
+    const uint32_t slot = blockIdx.x * (uint32_t)(WAVES * mw8::kRays) + (uint32_t)(wave * mw8::kRays + j);
+    const bool live = slot < a.N;
+    const uint32_t ss = live ? slot : a.N - 1u, N = a.N;
+    uint4* const Xw = smem + mw8::kNbuf * kStepVec + wave * kXw;
+    LevelDesc* const sLv = reinterpret_cast<LevelDesc*>(smem + mw8::kNbuf * kStepVec + WAVES * kXw);
+    if (tid < 16) sLv[tid] = a.grid.lv[tid];
+    MaskStreamW8<OT, WAVES> st{a.packed, smem, wave, lane, 0u, (uint32_t)kT * (uint32_t)mw8::steps(OT)};
+    st.begin();
+
+    const int kw = a.kexp[0] + a.kexp[1] + a.kexp[2];             // the weight tensors' log2 scales
+    floatx4 sum[OT];
+#pragma unroll
+    for (int o = 0; o < OT; ++o) sum[o] = floatx4{};
+    floatx4 acc[16];
+    uint4 ah[mw8::kH], al[mw8::kH];
+    // 32-bit byte offsets from the uniform array bases (saddr loads; the host
+    // launches this form for N < 2^21: 2 KiB of geo rows per ray)
+    const char* const ub = reinterpret_cast<const char*>(a.u_in);
+    const char* const wb = reinterpret_cast<const char*>(a.w_in);
+    const char* const gb = reinterpret_cast<const char*>(a.geo_in);
+    auto ld = [](const char* b, uint32_t off) { return *reinterpret_cast<const float*>(b + off); };
+#pragma unroll 1
+    for (int k = 0; k < kT; ++k) {
+        uint32_t ko = (uint32_t)k;
+        asm volatile("" : "+s"(ko));
+        const uint32_t uo = (ko * 3u * N + ss) * 4u;
+        const float ux = ld(ub, uo), uy = ld(ub, uo + 4u * N), uz = ld(ub, uo + 8u * N);
+        const float w = live ? ld(wb, (ko * N + ss) * 4u) : 0.0f;
+        // this lane's input group, opaque per sample: the level descriptors
+        // (LDS) and geo offsets are re-formed each sample instead of living
+        // through the loop as ~30 hoisted registers (they spilled)
+        uint32_t gq = (uint32_t)g;
+        asm volatile("" : "+v"(gq));
+        // layer-0 inputs: levels 4 b + g (b < 4), one level at a time, its 8
+        // corner rows in two halves of 4 (the sums in lookup_level3's corner
+        // order, as gather8_finish): 32 row registers in flight
+        float xm = 0.0f;
+        float xr[XLDS ? 1 : mw8::kL0][8];                          // WAVES 4: the inputs in registers
+        auto put = [&](int b, const float* f) {
+            if constexpr (XLDS) {
+                Xw[(2 * b) * 64 + lane] = make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]),
+                                                     __float_as_uint(f[2]), __float_as_uint(f[3]));
+                Xw[(2 * b + 1) * 64 + lane] = make_uint4(__float_as_uint(f[4]), __float_as_uint(f[5]),
+                                                         __float_as_uint(f[6]), __float_as_uint(f[7]));
+            } else {
+#pragma unroll
+                for (int m = 0; m < 8; ++m) xr[b][m] = f[m];
+            }
+#pragma unroll
+            for (int m = 0; m < 8; ++m) xm = fmaxf(xm, fabsf(f[m]));
+        };
+        const char* const eb = reinterpret_cast<const char*>(a.grid.emb);
+#pragma unroll
+        for (int b0 = 0; b0 < 4; b0 += MW8_LEVELS) {
+            // MW8_LEVELS levels' 8 corner rows in flight, then their sums (the
+            // corner order of lookup_level3, as gather8_finish)
+            uint32_t off[MW8_LEVELS][8];
+            float cw[MW8_LEVELS][8];
+            float4 e[MW8_LEVELS][8][2];
+#pragma unroll
+            for (int l = 0; l < MW8_LEVELS; ++l) {
+                corner_rows<8>(sLv[4 * (b0 + l) + gq], ux, uy, uz, off[l], cw[l]);
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    e[l][c][0] = *reinterpret_cast<const float4*>(eb + off[l][c]);
+                    e[l][c][1] = *reinterpret_cast<const float4*>(eb + off[l][c] + 16u);
+                }
+            }
+#pragma unroll
+            for (int l = 0; l < MW8_LEVELS; ++l) {
+                f2v acc2[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc2[i] = f2v{0.0f, 0.0f};
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const f2v wc = {cw[l][c], cw[l][c]};
+                    acc2[0] = __builtin_elementwise_fma(wc, f2v{e[l][c][0].x, e[l][c][0].y}, acc2[0]);
+                    acc2[1] = __builtin_elementwise_fma(wc, f2v{e[l][c][0].z, e[l][c][0].w}, acc2[1]);
+                    acc2[2] = __builtin_elementwise_fma(wc, f2v{e[l][c][1].x, e[l][c][1].y}, acc2[2]);
+                    acc2[3] = __builtin_elementwise_fma(wc, f2v{e[l][c][1].z, e[l][c][1].w}, acc2[3]);
+                }
+                const float f[8] = {acc2[0].x, acc2[0].y, acc2[1].x, acc2[1].y,
+                                    acc2[2].x, acc2[2].y, acc2[3].x, acc2[3].y};
+                put(b0 + l, f);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        {
+            float f[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const uint32_t gi = 8u * gq + (uint32_t)m;         // geo_feat index; >= 15: padding
+                f[m] = gi < 15u ? ld(gb, ((ko * 16u + gi + 1u) * N + ss) * 4u) : 0.0f;
+            }
+            put(4, f);
+        }
+        const int k0 = scale_exp_of_max(ray_max4_mw8(xm));
+        const float s0 = exp2i(k0);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) acc[t] = floatx4{};
+#pragma unroll
+        for (int b = 0; b < mw8::kL0; ++b) {
+            float v[8];
+            if constexpr (XLDS) {
+                const uint4 u0 = Xw[(2 * b) * 64 + lane], u1 = Xw[(2 * b + 1) * 64 + lane];
+                v[0] = __uint_as_float(u0.x), v[1] = __uint_as_float(u0.y), v[2] = __uint_as_float(u0.z);
+                v[3] = __uint_as_float(u0.w), v[4] = __uint_as_float(u1.x), v[5] = __uint_as_float(u1.y);
+                v[6] = __uint_as_float(u1.z), v[7] = __uint_as_float(u1.w);
+            } else {
+#pragma unroll
+                for (int m = 0; m < 8; ++m) v[m] = xr[b][m];
+            }
+            uint4 xh, xl;
+            split8_f16<true>(v, s0, xh, xl);
+            st.template run<0>(acc, xh, xl);
+            st.template run<1>(acc, xh, xl);
+        }
+        const int k1 = epilogue_w8(acc, ah, al);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) acc[t] = floatx4{};
+#pragma unroll
+        for (int b = 0; b < mw8::kH; ++b) {
+            st.template run<0>(acc, ah[b], al[b]);
+            st.template run<1>(acc, ah[b], al[b]);
+        }
+        const int k2 = epilogue_w8(acc, ah, al);
+        // the logits carry 2^(k0 + k1 + k2 + the weight scales); w * 2^-e is exact
+        const float wo = w * exp2i(-(k0 + k1 + k2 + kw));
+#pragma unroll
+        for (int o = 0; o < OT; ++o) {
+            floatx4 lo = {};
+            st.run_out(lo, ah, al);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sum[o][r] = __builtin_fmaf(wo, lo[r], sum[o][r]);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!live) return;
+    float* dst = a.out + (size_t)a.tiles(slot) * a.K;
+#pragma unroll
+    for (int o = 0; o < OT; ++o)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t u = (uint32_t)(16 * o + 4 * g + r);
+            if (u < a.K) dst[u] = sum[o][r];
+        }
+}
+
 }  // namespace
 
 namespace samnerf {
 
-size_t mask_head_packed_floats() { return (size_t)kMaskCopies * kPackVec * 4 + 4; }
+size_t mask_head_packed_floats() {
+    const size_t h32 = (size_t)kMaskCopies * kPackVec * 4 + 4;
+    const size_t hw8 = (size_t)mw8::steps(2) * kStepVec * 4 + 4;             // k_mask_head_w8's steps
+    return h32 > hw8 ? h32 : hw8;
+}
 
 int mask_head_forward(const samnerf_model* m, const GridDesc<16>& grid, const float* u_f, const float* w_f,
                       const float* geo_f, uint32_t N, float* out, RayTiles tiles, float* packed,
@@ -579,6 +987,21 @@ int mask_head_forward(const samnerf_model* m, const GridDesc<16>& grid, const fl
         k_mask_pack_f32<<<div_up(nfrag, 256), 256, 0, s>>>(m->mask_w[0], m->mask_w[1], m->mask_w[2],
                                                            m->mask_out, pk);
         k_mask_head<true><<<div_up(N, (uint32_t)kSlots), 256, 0, s>>>(a);
+    } else if (SAMNERF_MASK_W8 && N < (1u << 21)) {
+        // 1: one 8-wave workgroup per CU (7.57-7.60 ms per mask view against
+        // 7.86-7.94 for k_mask_head, profiles/r6m_mask_w8_ab.txt); 2: two
+        // 4-wave workgroups per CU (the inputs in registers spill: 9.1-9.2 ms)
+        constexpr int W = SAMNERF_MASK_W8 == 2 ? 4 : 8;
+        const uint32_t grid = div_up(N, (uint32_t)(W * mw8::kRays));
+        if (m->mask_out > 16u) {
+            k_mask_pack_w8<2><<<1, 1024, 0, s>>>(m->mask_w[0], m->mask_w[1], m->mask_w[2], m->mask_out, pk);
+            a.kexp = reinterpret_cast<const int*>(pk + (size_t)mw8::steps(2) * kStepVec);
+            k_mask_head_w8<2, W><<<grid, 64 * W, 0, s>>>(a);
+        } else {
+            k_mask_pack_w8<1><<<1, 1024, 0, s>>>(m->mask_w[0], m->mask_w[1], m->mask_w[2], m->mask_out, pk);
+            a.kexp = reinterpret_cast<const int*>(pk + (size_t)mw8::steps(1) * kStepVec);
+            k_mask_head_w8<1, W><<<grid, 64 * W, 0, s>>>(a);
+        }
     } else {
         k_mask_pack_h16<<<1, 1024, 0, s>>>(m->mask_w[0], m->mask_w[1], m->mask_w[2], m->mask_out, pk);
         k_mask_head<false><<<div_up(N, (uint32_t)kSlots), 256, 0, s>>>(a);
