@@ -69,11 +69,13 @@ ALG_BYTES_PER_RAY = {
 ALG_BYTES_RAY_TOTAL = 226_348
 # SAM head (network.py:36-75): 163->256, 256->256, 419->256, 256->256, 256->256
 HEAD_FLOP_PER_RAY = 2 * 256 * (163 + 256 + 419 + 256 + 256)  # 691,200
-# MFMA issue of the head per 32 rays (one wave): 86 k-blocks of 16 (K padded
-# 176 + 256 + 432 + 256 + 256) x 8 output tiles x 3 fp16 products of the f16x3
-# form (v_mfma_f32_32x32x16_f16, 32 cycles, the bf16 rate); exact mode: 688
-# k-steps of 2 x 8 tiles on v_mfma_f32_32x32x2_f32 (64 cycles).
-HEAD_MFMA_CYCLES_PER_32 = {0: 86 * 8 * 3 * 32, 1: 688 * 8 * 64}
+# MFMA issue cycles of the SAM head's structure per 32 rays: f16x3 on the
+# product's k_sam_head_w8 (two 16-ray waves: 44 32-deep k-blocks -- K padded
+# 192 + 256 + 448 + 256 + 256 -- x 16 output tiles x 3 fp16 products on
+# v_mfma_f32_16x16x32_f16, 16 cycles; round 5's k_sam_head_h16q: 86 16-deep
+# k-blocks x 8 tiles x 3 x 32 cycles); exact mode: 688 k-steps of 2 x 8 tiles
+# on v_mfma_f32_32x32x2_f32 (64 cycles)
+HEAD_MFMA_CYCLES_PER_32 = {0: 2 * 44 * 16 * 3 * 16, 1: 688 * 8 * 64}
 BF16_MFMA_PEAK_TFS = 2500.0    # MI355X_MICROARCH.md: dense BF16/F16 ~2.5 PF
 F32_MFMA_PEAK_TFS = 157.3      # MI355X_MICROARCH.md: F32 matrix = vector peak
 DTYPE = {0: "fp32-equivalent: fp32 in the reference's op order for everything that decides a "
@@ -926,9 +928,9 @@ def rooflines(stage_avg, band_rays, head_mode, rates, clocks=None, timed_clock=N
                             "achieved_fp32_equiv": HEAD_FLOP_PER_RAY * band_rays / (ms * 1e-3) / 1e12,
                             "peak": F32_MFMA_PEAK_TFS if head_mode == 1 else BF16_MFMA_PEAK_TFS,
                             "achieved": None,
-                            "basis": "MFMA issue cycles of the head's structure (f16x3: 86 k-blocks x 8 "
-                                     "tiles x 3 v_mfma_f32_32x32x16_f16 per 32 rays) / (1024 SIMDs x "
-                                     "2.4 GHz x time)"}
+                            "basis": "MFMA issue cycles of the head's structure (f16x3, k_sam_head_w8: 44 "
+                                     "32-deep k-blocks x 16 tiles x 3 v_mfma_f32_16x16x32_f16 per 16 rays) / "
+                                     "(1024 SIMDs x 2.4 GHz x time)"}
             cand["mfma"]["achieved"] = cand["mfma"]["frac"] * cand["mfma"]["peak"]   # at the structure's rate
             if "mfma_busy_cycles_per_ray" in r:
                 cand["mfma"]["pmc_mfma_busy_frac"] = r["mfma_busy_cycles_per_ray"] * band_rays / cyc_avail(ms)

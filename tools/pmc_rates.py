@@ -27,7 +27,7 @@ STAGE_KERNELS = {                     # substring of the kernel name -> stage
     "k_prop_sigma<64": "prop1", "k_prop_pdf<64": "prop1",
     "k_final": "final",
     "k_sgrid": "s_grid",
-    "k_head_wmax": "sam_head", "k_pack_h16": "sam_head", "k_sam_head": "sam_head",
+    "k_head_wmax": "sam_head", "k_pack_h16": "sam_head", "k_pack_w8": "sam_head", "k_sam_head": "sam_head",
 }
 RAYS = 262144
 

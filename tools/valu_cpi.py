@@ -29,7 +29,7 @@ STAGES = {
     "prop1": ("raymarch.hip", "_ZN12_GLOBAL__N_112k_prop_sigmaILi64ELb0ELi0ELj3ELj28EEEvNS_8PropArgsE"),
     "final": ("raymarch.hip", "_ZN12_GLOBAL__N_17k_finalILi32ELi1ELb0ELb0ELb0ELb0ELi0ELi1ELb0EEEvNS_9FinalArgsE"),
     "s_grid": ("raymarch.hip", "_ZN12_GLOBAL__N_112k_sgrid_box4ILi32ELb0EEEvNS_9SgridArgsE"),
-    "sam_head": ("sam_head.hip", None),     # the k_sam_head_h16q<4, false, true> instantiation
+    "sam_head": ("sam_head.hip", None),     # the product head: k_sam_head_w8<4, 8, true> (round 6)
 }
 FAST = ("v_fma_f32", "v_fmac_f32", "v_mul_f32", "v_add_f32", "v_sub_f32", "v_subrev_f32", "v_add_u32",
         "v_sub_u32", "v_subrev_u32", "v_xor_b32", "v_and_b32", "v_or_b32")
@@ -115,8 +115,8 @@ def main():
                    "profiles/r5v_valu_rate.json at 8 waves per SIMD; tools/valu_cpi.py)", "stages": {}}
     for st, (f, name) in STAGES.items():
         if name is None:
-            name = next(m for m in re.findall(r"^(\S*k_sam_head_h16q\S*):", asm[f], re.M)
-                        if "ILi4ELb0ELb1E" in m)
+            name = next(m for m in re.findall(r"^(\S*k_sam_head_w8\S*):", asm[f], re.M)
+                        if "ILi4ELi8ELb1E" in m)
         region, kind = hot_region(kernel_body(asm[f], name))
         v = [o for o in ops(region) if is_valu(o)]
         cyc = sum(cycles(o, rates) for o in v)
