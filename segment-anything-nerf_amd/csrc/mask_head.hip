@@ -587,12 +587,12 @@ k_mask_head(MaskArgs a) {
 // 4-wave workgroups per CU (SAMNERF_MASK_W8=2) drift apart but must keep the
 // inputs in registers (no LDS for two rings and two input stages) and spill:
 // 9.1-9.2 ms.  Two levels' corner rows in flight instead of one: the same
-// time (MW8_LEVELS=2, 200 registers).
+// time (200 registers); the next sample's gathers issued under this
+// sample's layer-1 MFMAs (software-pipelined into the free LDS input stage):
+// 7.55-7.59 against 7.44-7.53 ms (profiles/r6o_mask_pipe_ab.txt) -- the
+// gathers are not what bounds this form.
 #ifndef SAMNERF_MASK_W8
 #define SAMNERF_MASK_W8 1
-#endif
-#ifndef MW8_LEVELS
-#define MW8_LEVELS 1                          // levels' corner rows in flight per lane (1, 2 or 4)
 #endif
 namespace mw8 {
 constexpr int kRays = 16;                                      // ray slots per wave
@@ -830,81 +830,94 @@ k_mask_head_w8(MaskArgs a) {
     const char* const wb = reinterpret_cast<const char*>(a.w_in);
     const char* const gb = reinterpret_cast<const char*>(a.geo_in);
     auto ld = [](const char* b, uint32_t off) { return *reinterpret_cast<const float*>(b + off); };
+    const char* const eb = reinterpret_cast<const char*>(a.grid.emb);
+    // sample kk's position (slot order, [32][3][N])
+    auto position = [&](uint32_t kk, float& px, float& py, float& pz) {
+        asm volatile("" : "+s"(kk));
+        const uint32_t uo = (kk * 3u * N + ss) * 4u;
+        px = ld(ub, uo), py = ld(ub, uo + 4u * N), pz = ld(ub, uo + 8u * N);
+    };
+    // level 4 b + g's 8 corner rows (issue) and their sum in lookup_level3's
+    // corner order (as gather8_finish); gq: this lane's group, opaque per call
+    // (the descriptors re-read from LDS, not hoisted through the loop)
+    struct Rows {
+        float4 e[8][2];
+        float cw[8];
+    };
+    auto issue_level = [&](int b, float px, float py, float pz, Rows& r) {
+        uint32_t gq = (uint32_t)g;
+        asm volatile("" : "+v"(gq));
+        uint32_t off[8];
+        corner_rows<8>(sLv[4 * b + gq], px, py, pz, off, r.cw);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            r.e[c][0] = *reinterpret_cast<const float4*>(eb + off[c]);
+            r.e[c][1] = *reinterpret_cast<const float4*>(eb + off[c] + 16u);
+        }
+    };
+    auto sum_level = [&](const Rows& r, float* f) {
+        f2v acc2[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc2[i] = f2v{0.0f, 0.0f};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const f2v wc = {r.cw[c], r.cw[c]};
+            acc2[0] = __builtin_elementwise_fma(wc, f2v{r.e[c][0].x, r.e[c][0].y}, acc2[0]);
+            acc2[1] = __builtin_elementwise_fma(wc, f2v{r.e[c][0].z, r.e[c][0].w}, acc2[1]);
+            acc2[2] = __builtin_elementwise_fma(wc, f2v{r.e[c][1].x, r.e[c][1].y}, acc2[2]);
+            acc2[3] = __builtin_elementwise_fma(wc, f2v{r.e[c][1].z, r.e[c][1].w}, acc2[3]);
+        }
+        f[0] = acc2[0].x, f[1] = acc2[0].y, f[2] = acc2[1].x, f[3] = acc2[1].y;
+        f[4] = acc2[2].x, f[5] = acc2[2].y, f[6] = acc2[3].x, f[7] = acc2[3].y;
+    };
+    float xr[XLDS ? 1 : mw8::kL0][8];                              // WAVES 4: the inputs in registers
+    auto put = [&](int b, const float* f, float& xm) {
+        if constexpr (XLDS) {
+            Xw[(2 * b) * 64 + lane] = make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]),
+                                                 __float_as_uint(f[2]), __float_as_uint(f[3]));
+            Xw[(2 * b + 1) * 64 + lane] = make_uint4(__float_as_uint(f[4]), __float_as_uint(f[5]),
+                                                     __float_as_uint(f[6]), __float_as_uint(f[7]));
+        } else {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) xr[b][m] = f[m];
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m) xm = fmaxf(xm, fabsf(f[m]));
+    };
+    auto geo = [&](uint32_t kk, float& xm) {
+        uint32_t gq = (uint32_t)g;
+        asm volatile("" : "+v"(gq));
+        asm volatile("" : "+s"(kk));
+        float f[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const uint32_t gi = 8u * gq + (uint32_t)m;             // geo_feat index; >= 15: padding
+            f[m] = gi < 15u ? ld(gb, ((kk * 16u + gi + 1u) * N + ss) * 4u) : 0.0f;
+        }
+        put(4, f, xm);
+    };
+    // all of sample kk's inputs, one level's rows in flight at a time
+    auto inputs = [&](uint32_t kk, float& xm) {
+        float px, py, pz;
+        position(kk, px, py, pz);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            Rows r;
+            issue_level(b, px, py, pz, r);
+            float f[8];
+            sum_level(r, f);
+            put(b, f, xm);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        geo(kk, xm);
+    };
 #pragma unroll 1
     for (int k = 0; k < kT; ++k) {
         uint32_t ko = (uint32_t)k;
         asm volatile("" : "+s"(ko));
-        const uint32_t uo = (ko * 3u * N + ss) * 4u;
-        const float ux = ld(ub, uo), uy = ld(ub, uo + 4u * N), uz = ld(ub, uo + 8u * N);
         const float w = live ? ld(wb, (ko * N + ss) * 4u) : 0.0f;
-        // this lane's input group, opaque per sample: the level descriptors
-        // (LDS) and geo offsets are re-formed each sample instead of living
-        // through the loop as ~30 hoisted registers (they spilled)
-        uint32_t gq = (uint32_t)g;
-        asm volatile("" : "+v"(gq));
-        // layer-0 inputs: levels 4 b + g (b < 4), one level at a time, its 8
-        // corner rows in two halves of 4 (the sums in lookup_level3's corner
-        // order, as gather8_finish): 32 row registers in flight
         float xm = 0.0f;
-        float xr[XLDS ? 1 : mw8::kL0][8];                          // WAVES 4: the inputs in registers
-        auto put = [&](int b, const float* f) {
-            if constexpr (XLDS) {
-                Xw[(2 * b) * 64 + lane] = make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]),
-                                                     __float_as_uint(f[2]), __float_as_uint(f[3]));
-                Xw[(2 * b + 1) * 64 + lane] = make_uint4(__float_as_uint(f[4]), __float_as_uint(f[5]),
-                                                         __float_as_uint(f[6]), __float_as_uint(f[7]));
-            } else {
-#pragma unroll
-                for (int m = 0; m < 8; ++m) xr[b][m] = f[m];
-            }
-#pragma unroll
-            for (int m = 0; m < 8; ++m) xm = fmaxf(xm, fabsf(f[m]));
-        };
-        const char* const eb = reinterpret_cast<const char*>(a.grid.emb);
-#pragma unroll
-        for (int b0 = 0; b0 < 4; b0 += MW8_LEVELS) {
-            // MW8_LEVELS levels' 8 corner rows in flight, then their sums (the
-            // corner order of lookup_level3, as gather8_finish)
-            uint32_t off[MW8_LEVELS][8];
-            float cw[MW8_LEVELS][8];
-            float4 e[MW8_LEVELS][8][2];
-#pragma unroll
-            for (int l = 0; l < MW8_LEVELS; ++l) {
-                corner_rows<8>(sLv[4 * (b0 + l) + gq], ux, uy, uz, off[l], cw[l]);
-#pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    e[l][c][0] = *reinterpret_cast<const float4*>(eb + off[l][c]);
-                    e[l][c][1] = *reinterpret_cast<const float4*>(eb + off[l][c] + 16u);
-                }
-            }
-#pragma unroll
-            for (int l = 0; l < MW8_LEVELS; ++l) {
-                f2v acc2[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) acc2[i] = f2v{0.0f, 0.0f};
-#pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    const f2v wc = {cw[l][c], cw[l][c]};
-                    acc2[0] = __builtin_elementwise_fma(wc, f2v{e[l][c][0].x, e[l][c][0].y}, acc2[0]);
-                    acc2[1] = __builtin_elementwise_fma(wc, f2v{e[l][c][0].z, e[l][c][0].w}, acc2[1]);
-                    acc2[2] = __builtin_elementwise_fma(wc, f2v{e[l][c][1].x, e[l][c][1].y}, acc2[2]);
-                    acc2[3] = __builtin_elementwise_fma(wc, f2v{e[l][c][1].z, e[l][c][1].w}, acc2[3]);
-                }
-                const float f[8] = {acc2[0].x, acc2[0].y, acc2[1].x, acc2[1].y,
-                                    acc2[2].x, acc2[2].y, acc2[3].x, acc2[3].y};
-                put(b0 + l, f);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        {
-            float f[8];
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const uint32_t gi = 8u * gq + (uint32_t)m;         // geo_feat index; >= 15: padding
-                f[m] = gi < 15u ? ld(gb, ((ko * 16u + gi + 1u) * N + ss) * 4u) : 0.0f;
-            }
-            put(4, f);
-        }
+        inputs(ko, xm);
         const int k0 = scale_exp_of_max(ray_max4_mw8(xm));
         const float s0 = exp2i(k0);
 #pragma unroll
