@@ -137,7 +137,7 @@ def _float64_twin_errors(nets_fp32, cpu, ro, rd, gt, global_step=1, bins=None):
                 continue
             e[k] = ((a.grad.detach().cpu().double() - b.grad).norm() / b.grad.norm().clamp_min(1e-300)).item()
         errs[name] = e
-    return errs, float(loss64)
+    return errs, float(loss64.detach())
 
 
 @pytest.mark.parametrize("lam", [(1.0, 0.02, 0.0), (1.0, 0.0, 0.0), (0.0, 0.0, 0.0), (1.0, 0.02, 1e-3)],
