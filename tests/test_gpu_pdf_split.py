@@ -90,3 +90,34 @@ def test_split_phase_a_nan_density(hip_lib, cuda, monkeypatch):
         same = torch.equal(a, b) if not a.is_floating_point() else \
             bool(((a == b) | (torch.isnan(a) & torch.isnan(b))).all())
         assert same, k
+
+
+def test_sgrid_box4_path_counters_cover_every_level_sample(hip_lib, cuda, monkeypatch):
+    """The diagnostic build's k_sgrid_box4 path counters (SAMNERF_SGRID_PATHS,
+    tools/sgrid_paths.py): every (wave, sample, level) of a view is counted in
+    exactly one of the uniform / box / direct paths, or skipped with its wave's
+    sample; the render's outputs equal the product's (the counters only add
+    atomics in the diagnostic build)."""
+    from samnerf_amd import _lib, ops
+    from samnerf_amd.fused import FusedRenderer
+    spec = synth.ModelSpec(with_sam=True)
+    net = make_net(spec, synth.make_params(spec, seed=7, emb_scale=0.5, ln_jitter=0.0), cuda)
+    h = w = 256                                            # N >= 32768: the box form runs
+    pose, intr = synth.gui_camera(w, h, rot=synth.random_rotation(6))
+    ro, rd = ops.get_rays(pose, intr, h, w, device=cuda)
+    prod = FusedRenderer(net).render(ro, rd, view_width=w)
+    cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+    monkeypatch.setenv("SAMNERF_SGRID_PATHS", f"{cnt.data_ptr():x}")
+    with _lib.diag_library():
+        diag = FusedRenderer(net).render(ro, rd, view_width=w)
+    monkeypatch.delenv("SAMNERF_SGRID_PATHS")
+    torch.cuda.synchronize()
+    c = cnt.cpu().tolist()
+    groups = (h * w) // 64
+    # per 64-ray group: 4 level groups x 32 samples (4 quarter-waves x 8), each
+    # counted once per level (4) or once as a skipped wave-sample of its group
+    assert c[0] + c[1] + c[2] + 4 * c[3] == groups * 32 * 16, c
+    assert c[1] > 0, c
+    assert c[4] >= c[5] > 0, c                             # padded slots >= cells of the staged boxes
+    for k in ("image", "depth", "weights_sum", "samvit"):
+        assert torch.equal(prod[k], diag[k]), k
